@@ -1,0 +1,363 @@
+"""bench.py — QUIC FEC XOR encode+recover throughput on MI355X (device-resident).
+
+Metric (BASELINE.json): "FEC XOR encode+recover GiB/s (device-resident) on
+batched 1350B packet groups".  One step = one encode pass + one single-loss
+recover pass over G = 2^20 groups x 10 x 1350 B per GPU (BASELINE configs[1] +
+configs[2]), inputs already resident in HBM.  Algorithmic bytes (SURVEY.md
+§8(d)): encode 10*1350 read + 1350 written = 14,850 B/group; recover
+9*1350 + 1350 read + 1350 written = 14,850 B/group.
+
+Multi-GPU: one process per GPU (torchrun), each rank owns the contiguous group
+range [rank*G, (rank+1)*G) — independent FEC groups, no collective on the data
+path (weak scaling).  Timing: barrier + synchronize on both sides of exactly K
+steps, max over ranks.
+
+Also reported (same JSON line): the encode kernel's roofline (HIP events on
+the stream the kernels run on), the CPU baseline (oracle on host cores, rank 0,
+N=1), the end-to-end pinned-host rate, and the ragged (k 5-15, len 64-1350)
+batch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md (spec 8.0 TB/s)
+SEED_FIXED, SEED_RAGGED, SEED_DROP = 0x51554943, 0x51554944, 0x51554945
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--groups", type=int, default=1 << 20, help="FEC groups per GPU")
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--L", type=int, default=1350)
+    p.add_argument("--nontemporal", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--no-ragged", action="store_true")
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--profile-only", action="store_true",
+                   help="only the device-resident steps (for rocprofv3 runs)")
+    return p.parse_args()
+
+
+def drop_indices(g0, n, k):
+    from libquic_amd import synth
+    return synth.drop_indices(SEED_DROP, np.arange(g0, g0 + n, dtype=np.uint64), k).astype(np.uint8)
+
+
+def cpu_baseline(k, L, seconds):
+    """Oracle (C restatement) on the host cores, bounded sample (rank 0, N=1)."""
+    from oracle import oracle_c as OC
+    lib = OC.lib()
+    threads = min(16, os.cpu_count() or 1)
+    n = 1 << 16  # 65,536 groups = 885 MB of rows
+    rows = OC.synth_fixed(SEED_FIXED, 0, n, k, L)
+    par = np.zeros(n * L, np.uint8)
+    out = np.zeros(n * L, np.uint8)
+    miss = drop_indices(0, n, k)
+    bytes_per_pass = 2 * n * (k * L + L)  # encode + recover algorithmic bytes
+
+    def run(th):
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            lib.qo_encode_fixed_mt(OC._p(rows), k, L, n, OC._p(par), th)
+            lib.qo_recover_fixed_mt(OC._p(rows), OC._p(par), OC._p(miss), k, L, n, OC._p(out), th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                return reps * bytes_per_pass / el / 2**30, reps
+
+    mt, reps_mt = run(threads)
+    st, reps_st = run(1)
+    # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
+    one = rows[: k * L].copy()
+    p1 = np.zeros(L, np.uint8)
+    o1 = np.zeros(L, np.uint8)
+    m1 = miss[:1].copy()
+    it = 20000
+    t0 = time.perf_counter()
+    for _ in range(it):
+        lib.qo_encode_fixed(OC._p(one), k, L, L, k * L, 1, OC._p(p1), L)
+        lib.qo_recover_fixed(OC._p(one), OC._p(p1), OC._p(m1), k, L, L, k * L, L, 1, OC._p(o1), L)
+    ns_group = (time.perf_counter() - t0) / it * 1e9
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"oracle encode+recover of {n} groups x {k} x {L} B, {reps_mt} passes "
+                  f"(~{seconds / 2:.0f} s) on {threads} threads",
+        "single_core_value": round(st, 3),
+        "configs0_ns_per_group_1core": round(ns_group, 1),
+        "cpu_model": cpu_model, "nproc": os.cpu_count(),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from libquic_amd import qfec
+
+    ctx = qfec.Context(dev.index)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+
+    k, L, G = args.k, args.L, args.groups
+    g0 = rank * G
+    bytes_enc = G * (k * L + L)
+    bytes_rec = G * ((k - 1) * L + 2 * L)
+
+    rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
+    par = torch.empty(G * L, dtype=torch.uint8, device=dev)
+    out = torch.empty(G * L, dtype=torch.uint8, device=dev)
+    miss_np = drop_indices(g0, G, k)
+    miss = torch.from_numpy(miss_np).to(dev)
+    ctx.synth_fixed(rows, k, L, g0, G, SEED_FIXED)
+    ctx.sync()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        ctx.encode(rows, k, L, G, par, nontemporal=args.nontemporal)
+        if ev:
+            ev[1].record(stream)
+        ctx.recover(rows, par, miss, k, L, G, out, nontemporal=args.nontemporal)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+
+    verified = None
+    if not args.no_verify:
+        # round trip on every group + parity XOR rows == 0 (device, untimed)
+        r3 = rows.view(G, k, L)
+        ok = torch.equal(r3[torch.arange(G, device=dev), miss.long()], out.view(G, L))
+        acc = par.view(G, L).clone()
+        for i in range(k):
+            acc ^= r3[:, i]
+        ok = ok and not bool(acc.any())
+        del acc
+        verified = bool(ok)  # bit-exact vs the oracle is tests/test_hip_fixed.py's job
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(events[s])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    enc_ms = np.array([e[0].elapsed_time(e[1]) for e in events])
+    rec_ms = np.array([e[1].elapsed_time(e[2]) for e in events])
+    ctx.sync()
+
+    total_bytes = world * args.steps * (bytes_enc + bytes_rec)
+    value = total_bytes / 2**30 / elapsed
+    enc_avg_s = float(enc_ms.mean()) / 1e3
+    rec_avg_s = float(rec_ms.mean()) / 1e3
+    enc_gbs = bytes_enc / enc_avg_s / 1e9
+    rec_gbs = bytes_rec / rec_avg_s / 1e9
+
+    extra = {}
+    if not args.profile_only and rank == 0 and world == 1:
+        del rows
+        torch.cuda.empty_cache()
+        if not args.no_ragged:
+            extra["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
+        if not args.no_e2e:
+            extra["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
+        if not args.no_cpu_baseline:
+            extra["cpu_baseline"] = cpu_baseline(k, L, args.cpu_seconds)
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("groups") == G and tj.get("k") == k and tj.get("L") == L:
+            traffic = tj.get("encode_hbm_bytes_per_launch")
+
+    if rank == 0:
+        line = {
+            "metric": "FEC XOR encode+recover GiB/s (device-resident) on batched 1350B packet groups",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-based splitmix64 bytes generated in HBM)",
+            "config": {
+                "workload": f"{G} groups x {k} x {L} B per GPU: parity encode + single-loss "
+                            f"recover (BASELINE configs[1]+[2])",
+                "groups_per_gpu": G, "k": k, "L": L,
+                "parallelism": f"group-shard x{world} (no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "fixed_xor_kernel<10,encode>",
+                "achieved": round(enc_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_enc,
+                "avg_launch_us": round(enc_avg_s * 1e6, 2),
+            },
+            "encode_GiBps": round(bytes_enc / enc_avg_s / 2**30, 2),
+            "recover_GiBps": round(bytes_rec / rec_avg_s / 2**30, 2),
+            "recover_roofline_frac": round(rec_gbs / HBM_PEAK_GBS, 4),
+            "verified": verified,
+        }
+        line.update(extra)
+        if "cpu_baseline" not in line:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
+    """configs[3]: ragged batch, k 5-15, len 64-1350, packed CSR (device-resident)."""
+    from libquic_amd import synth
+    gs = np.arange(G, dtype=np.uint64)
+    ks, ptr, ln, off = synth.ragged_layout(0, G, 5, 15, 64, 1350, SEED_RAGGED)
+    total = int(off[-1]) + int(ln[-1])
+    plen_max = np.maximum.reduceat(ln, ptr[:-1].astype(np.int64))
+    miss = synth.drop_indices(SEED_DROP, gs, ks).astype(np.uint8)
+    t_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    t_len = torch.from_numpy(ln.view(np.int16)).to(dev)
+    t_ptr = torch.from_numpy(ptr.view(np.int32)).to(dev)
+    poff = np.arange(G, dtype=np.uint64) * np.uint64(1452)
+    t_poff = torch.from_numpy(poff.view(np.int64)).to(dev)
+    t_miss = torch.from_numpy(miss).to(dev)
+    data = torch.empty(total, dtype=torch.uint8, device=dev)
+    ctx.synth_ragged(data, t_off, t_len, t_ptr, 0, G, SEED_RAGGED)
+    par = torch.empty(G * 1452, dtype=torch.uint8, device=dev)
+    plen = torch.empty(G, dtype=torch.int16, device=dev)
+    out = torch.empty(G * 1452, dtype=torch.uint8, device=dev)
+
+    def run(ev=None):
+        if ev:
+            ev[0].record(stream)
+        ctx.encode_ragged(data, t_off, t_len, t_ptr, G, par, t_poff, plen)
+        if ev:
+            ev[1].record(stream)
+        ctx.recover_ragged(data, t_off, t_len, t_ptr, G, par, t_poff, plen, t_miss, out, t_poff)
+        if ev:
+            ev[2].record(stream)
+
+    run()
+    ctx.sync()
+    # verify: parity lengths and the round trip of a sample of groups
+    ok = np.array_equal(plen.cpu().numpy().view(np.uint16), plen_max)
+    out_h = out.cpu().numpy()
+    data_h = None
+    for g in np.random.default_rng(0).choice(G, 256, replace=False):
+        p = int(ptr[g]) + int(miss[g])
+        o, l_ = int(off[p]), int(ln[p])
+        if data_h is None:
+            data_h = data.cpu().numpy()
+        seg = out_h[g * 1452: g * 1452 + int(plen_max[g])]
+        ok = ok and np.array_equal(seg[:l_], data_h[o:o + l_]) and not seg[l_:].any()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    for s in range(steps):
+        run(evs[s])
+    torch.cuda.synchronize()
+    enc = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
+    rec = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
+    lens_sum = float(ln.astype(np.float64).sum())
+    pl_sum = float(plen_max.astype(np.float64).sum())
+    miss_len = float(ln[ptr[:-1].astype(np.int64) + miss.astype(np.int64)].astype(np.float64).sum())
+    b_enc = lens_sum + pl_sum
+    b_rec = (lens_sum - miss_len) + 2 * pl_sum
+    return {"groups": G, "k": "5-15", "len": "64-1350", "layout": "packed CSR",
+            "encode_GiBps": round(b_enc / enc / 2**30, 2),
+            "recover_GiBps": round(b_rec / rec / 2**30, 2),
+            "encode_frac": round(b_enc / enc / 1e9 / HBM_PEAK_GBS, 4),
+            "recover_frac": round(b_rec / rec / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_us": round(enc * 1e6, 1), "recover_us": round(rec * 1e6, 1),
+            "verified": bool(ok)}
+
+
+def bench_e2e(ctx, torch, k, L, G=1 << 18):
+    """Host-resident path: pinned host rows -> H2D -> kernel -> D2H (QFEC_PTR_HOST)."""
+    rows = torch.empty(G * k * L, dtype=torch.uint8).pin_memory()
+    # fill from the device generator (plumbing) to avoid a slow host fill
+    d = torch.empty(G * k * L, dtype=torch.uint8, device="cuda")
+    ctx.synth_fixed(d, k, L, 0, G, SEED_FIXED)
+    ctx.sync()
+    rows.copy_(d)
+    del d
+    par = torch.empty(G * L, dtype=torch.uint8).pin_memory()
+    out = torch.empty(G * L, dtype=torch.uint8).pin_memory()
+    miss = drop_indices(0, G, k)
+    ctx.encode(rows, k, L, G, par, host=True)  # warm (allocates staging)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.encode(rows, k, L, G, par, host=True)
+    t_enc = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.recover(rows, par, miss, k, L, G, out, host=True)
+    t_rec = (time.perf_counter() - t0) / reps
+    r3 = rows.numpy().reshape(G, k, L)
+    ok = np.array_equal(out.numpy().reshape(G, L)[:4096], r3[np.arange(4096), miss[:4096]])
+    b = G * (k * L + L)
+    return {"groups": G, "encode_GiBps": round(b / t_enc / 2**30, 2),
+            "recover_GiBps": round(b / t_rec / 2**30, 2),
+            "pcie_bytes_encode": G * (k * L + L), "verified": bool(ok),
+            "note": "algorithmic bytes / wall time, pinned host buffers, 3-slot H2D/kernel/D2H"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * qfec.h — C-ABI of the MI355X-native QUIC forward-error-correction path.
+ *
+ * The boundary replaces libquic's FEC group (XOR parity encode + single-packet
+ * revive).  The reference's implementation is absent from the snapshot
+ * (/root/reference/Makefile:5332-5384 still lists the removed
+ * src/net/quic/quic_fec_group.cc and quic_fec_group_interface.cc;
+ * src/net/quic/core/quic_protocol.h:373 "FEC related fields are removed from
+ * wire format"), so each entry point cites the historical member it replaces
+ * and the in-tree hook site that called it:
+ *
+ *   qfec_encode_batch / _strided / qfec_encode_ragged
+ *       replaces QuicFecGroup::UpdateParity + QuicFecGroupInterface::XorBuffers
+ *       over every data packet of a group, then QuicFecGroup::PayloadParity().
+ *       Send-side hook: QuicPacketCreator::SerializePacket between
+ *       QuicFramer::BuildDataPacket and EncryptInPlace
+ *       (src/net/quic/core/quic_packet_creator.cc:517-563, :530, :549).
+ *   qfec_recover_batch / _strided / qfec_recover_ragged
+ *       replaces QuicFecGroup::UpdateFec + Update(received) + CanRevive() +
+ *       Revive().  Receive-side hook: QuicConnection::ProcessValidatedPacket
+ *       "Drop any FEC packet." (src/net/quic/core/quic_connection.cc:1388-1392).
+ *   qfec_xor_into
+ *       replaces QuicFecGroupInterface::XorBuffers(input, size, output).
+ *
+ * Semantics: parity[j] = XOR over packets with
+ * j < len_i of p_i[j]; parity_len = max len_i (zero padding, PADDING_FRAME = 0,
+ * quic_protocol.h:259; quic_data_writer.cc:136-143).  Revive output is
+ * parity_len bytes; bytes past the lost packet's own length are 0 and parse as
+ * one PADDING frame (quic_framer.cc:1224-1231).
+ *
+ * Errors mirror the framer's bool + RaiseError(code) + detailed string
+ * (quic_framer.cc:1128-1135): every call returns 0 on success or a negative
+ * QuicErrorCode (quic_protocol.h:530-550); qfec_last_error() returns the
+ * detailed string.  Nothing aborts.
+ *
+ * Ownership mirrors the reference's caller-owned ALIGNAS(64) packet buffers
+ * (quic_framer.cc:573, quic_packet_creator.cc:351,401) and non-owning
+ * StringPiece views: every buffer is borrowed for the duration of the call
+ * (device-pointer calls: until the work queued on the context stream has
+ * completed — see qfec_sync).  The context owns its device scratch, pinned
+ * staging and streams; the library never frees caller memory.
+ *
+ * Threading: the reference connection is single-threaded
+ * (quic_connection.h:14 "this class is not thread-safe"); a qfec_ctx is
+ * likewise thread-compatible — one context per host thread / device, no global
+ * locks on the hot path.
+ */
+#ifndef QFEC_H_
+#define QFEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QFEC_ABI_VERSION 1
+
+/* Limits (quic_protocol.h:56, :66; quic_framer.cc:1126-1136). */
+#define QFEC_DEFAULT_MAX_PACKET_SIZE 1350u /* kDefaultMaxPacketSize */
+#define QFEC_MAX_PACKET_SIZE 1452u         /* kMaxPacketSize */
+#define QFEC_MAX_GROUP_PACKETS 255u        /* uint8 first_fec_protected_packet_offset */
+
+/* Return codes: 0 or -QuicErrorCode (quic_protocol.h). */
+#define QFEC_OK 0
+#define QFEC_ERR_INTERNAL (-1)         /* -QUIC_INTERNAL_ERROR: HIP failure, bad ctx */
+#define QFEC_ERR_INVALID_FEC_DATA (-5) /* -QUIC_INVALID_FEC_DATA */
+
+/* flags */
+#define QFEC_PTR_DEVICE 0u  /* all buffer arguments are device pointers (default) */
+#define QFEC_PTR_HOST 1u    /* all buffer arguments are host pointers: the call
+                               stages through the context (pinned, chunked,
+                               overlapped H2D / kernel / D2H) and returns when the
+                               results are back in host memory */
+#define QFEC_NONTEMPORAL 2u /* stream rows with non-temporal loads (device ptrs) */
+
+typedef struct qfec_ctx qfec_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+/* Create a context bound to HIP device `device`.  NULL on failure (no device,
+ * HIP error); the reason is then available from qfec_last_error(NULL). */
+qfec_ctx* qfec_create(int device);
+void qfec_destroy(qfec_ctx* ctx);
+/* Use an existing hipStream_t (e.g. torch's current stream) for device-pointer
+ * calls.  NULL restores the context's own stream. */
+int qfec_set_stream(qfec_ctx* ctx, void* hip_stream);
+void* qfec_get_stream(qfec_ctx* ctx);
+/* Wait for all queued work; returns the first error latched by a kernel
+ * (e.g. a missing index >= k or a ragged length > kMaxPacketSize found on the
+ * device) since the previous qfec_sync, then clears it. */
+int qfec_sync(qfec_ctx* ctx);
+const char* qfec_strerror(int code);
+const char* qfec_last_error(const qfec_ctx* ctx);
+int qfec_abi_version(void);
+
+/* ---- fixed-shape batches ---------------------------------------------- */
+/* rows:    n_groups x k x L bytes, group g row i at rows + g*k*L + i*L
+ * parity:  n_groups x L bytes
+ * Encode:  parity[g] = XOR_i rows[g][i]. */
+int qfec_encode_batch(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
+                      uint64_t n_groups, uint8_t* parity_out, uint32_t flags);
+
+/* Recover: out[g] = parity[g] XOR_{i != missing[g]} rows[g][i].
+ * rows[g][missing[g]] is never read (the lost packet's slot).  missing[g] < k. */
+int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity,
+                       const uint8_t* missing_idx, uint32_t k, uint32_t L, uint64_t n_groups,
+                       uint8_t* out, uint32_t flags);
+
+/* Strided forms (padding study: row_stride >= L, group_stride >= k*row_stride,
+ * parity/out strides >= L; all in bytes). */
+int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
+                              uint64_t row_stride, uint64_t group_stride, uint64_t n_groups,
+                              uint8_t* parity_out, uint64_t parity_stride, uint32_t flags);
+int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity,
+                               const uint8_t* missing_idx, uint32_t k, uint32_t L,
+                               uint64_t row_stride, uint64_t group_stride,
+                               uint64_t parity_stride, uint64_t n_groups, uint8_t* out,
+                               uint64_t out_stride, uint32_t flags);
+
+/* ---- ragged batches (CSR) ---------------------------------------------- */
+/* Group g holds packets p in [grp_ptr[g], grp_ptr[g+1]) (1..255 of them);
+ * packet p is pkt_len[p] (1..1452) bytes at bytes + pkt_off[p].
+ * Encode writes parity_len_out[g] = max len and that many parity bytes at
+ * parity_out + parity_off[g]. */
+int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
+                       const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
+                       uint8_t* parity_out, const uint64_t* parity_off,
+                       uint16_t* parity_len_out, uint32_t flags);
+/* Recover writes parity_len[g] bytes at out + out_off[g]:
+ * parity XOR every received packet of the group (zero padded).  The lost
+ * packet's pkt_off / pkt_len entries (index grp_ptr[g] + missing_idx[g]) are
+ * never read.  Every received packet must satisfy len <= parity_len[g]. */
+int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
+                        const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
+                        const uint8_t* parity, const uint64_t* parity_off,
+                        const uint16_t* parity_len, const uint8_t* missing_idx, uint8_t* out,
+                        const uint64_t* out_off, uint32_t flags);
+
+/* ---- single buffer ------------------------------------------------------ */
+/* out[j] ^= in[j] for j < n (QuicFecGroupInterface::XorBuffers). */
+int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, uint32_t flags);
+
+/* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
+/* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of
+ * splitmix64(seed ^ ((g*256 + i) << 32) ^ (j/8)) — generated on the device so
+ * that host and device agree without a 14 GB transfer.
+ * Fills groups g0 .. g0+n_groups-1 into rows[(g-g0)*group_stride + i*row_stride]. */
+int qfec_synth_fixed(qfec_ctx* ctx, uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
+                     uint64_t group_stride, uint64_t g0, uint64_t n_groups, uint64_t seed);
+/* Fill the packets of a ragged CSR batch whose group g (global index g0+g)
+ * packet i has pkt_len[grp_ptr[g]+i] bytes at pkt_off[...]. */
+int qfec_synth_ragged(qfec_ctx* ctx, uint8_t* bytes, const uint64_t* pkt_off,
+                      const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t g0,
+                      uint64_t n_groups, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QFEC_H_ */

@@ -1,0 +1,83 @@
+"""Build the native library in-tree: libquic_amd/libqfec.so (gfx950).
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
+container; the .so travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libqfec.so")
+ARCH = os.environ.get("QFEC_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["qfec_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc", "quic_fec_wire.cc"]
+HEADERS = ["qfec_internal.h", "quic_fec_group.h", "quic_fec_wire.h"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build libqfec.so)")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=cwd)
+
+
+def build_lib(force: bool = False, extra_flags=()) -> str:
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(ROOT, "include", "qfec.h"), __file__]
+    if force or _stale(LIB, deps):
+        objs = []
+        for s in srcs:
+            o = os.path.join(CSRC, "build", os.path.basename(s) + ".o")
+            os.makedirs(os.path.dirname(o), exist_ok=True)
+            if force or _stale(o, [s] + deps[len(srcs):]):
+                _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                      "-I", os.path.join(ROOT, "include"), *extra_flags, "-c", s, "-o", o])
+            objs.append(o)
+        tmp = LIB + ".tmp"
+        _run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_cpp_tests(force: bool = False) -> str:
+    """tests/cpp/test_quic_fec_group: C++ host-mirror tests (run on the GPU box)."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_quic_fec_group.cc")
+    out = os.path.join(ROOT, "tests", "cpp", "build", "test_quic_fec_group")
+    if not os.path.exists(src):
+        return ""
+    deps = [src, LIB, os.path.join(CSRC, "quic_fec_group.h"), os.path.join(CSRC, "quic_fec_wire.h"),
+            os.path.join(ROOT, "oracle", "qfec_oracle.c")]
+    if force or _stale(out, deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        oobj = os.path.join(os.path.dirname(out), "qfec_oracle.o")
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-c", os.path.join(ROOT, "oracle", "qfec_oracle.c"),
+              "-o", oobj])
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+              "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), src, oobj,
+              "-L", HERE, "-lqfec", "-Wl,-rpath,$ORIGIN/../../../libquic_amd",
+              "-Wl,-rpath-link,/opt/rocm/lib", "-lpthread", "-o", out])
+    return out
+
+
+if __name__ == "__main__":
+    build_lib(force="--force" in sys.argv)
+    build_cpp_tests(force="--force" in sys.argv)

@@ -1,0 +1,656 @@
+// qfec_capi.cpp — the C-ABI (include/qfec.h): context, argument validation,
+// error mapping, the host-pointer (pinned, chunked, overlapped) path and the
+// dispatch to the gfx950 kernels in qfec_kernels.hip.
+//
+// Error behaviour mirrors QuicFramer: a bool-style failure with a QuicErrorCode
+// and a detailed string (quic_framer.cc:1128-1135 set_detailed_error +
+// RaiseError); QUIC_BUG (quic_bug_tracker.h:10-11) is never used — nothing
+// aborts.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/qfec.h"
+#include "qfec_internal.h"
+
+namespace {
+
+thread_local char g_tls_error[512] = "";
+
+constexpr int kSlots = 3;                         // host path pipeline depth
+constexpr size_t kStageBytes = 64ull << 20;       // per-slot input staging
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* d_in = nullptr;   // device input staging
+  uint8_t* d_aux = nullptr;  // device parity-in / missing staging
+  uint8_t* d_out = nullptr;  // device output staging
+  uint8_t* h_in = nullptr;   // pinned input bounce buffer
+  uint8_t* h_aux = nullptr;
+  uint8_t* h_out = nullptr;
+  bool busy = false;
+};
+
+}  // namespace
+
+struct qfec_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t* d_err = nullptr;
+  uint32_t* h_err = nullptr;  // pinned
+  char last_error[512] = "";
+  Slot slots[kSlots];
+  bool staging_ready = false;
+};
+
+namespace {
+
+int fail(qfec_ctx* ctx, int code, const char* fmt, ...) {
+  char* buf = ctx ? ctx->last_error : g_tls_error;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, 512, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define QFEC_HIP(ctx, expr)                                                         \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      return fail((ctx), QFEC_ERR_INTERNAL, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+int bind(qfec_ctx* ctx) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  QFEC_HIP(ctx, hipSetDevice(ctx->device));
+  return QFEC_OK;
+}
+
+bool is_pinned_or_device(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeDevice ||
+         attr.type == hipMemoryTypeManaged;
+}
+
+int ensure_staging(qfec_ctx* ctx) {
+  if (ctx->staging_ready) return QFEC_OK;
+  for (auto& s : ctx->slots) {
+    QFEC_HIP(ctx, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    QFEC_HIP(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    QFEC_HIP(ctx, hipMalloc(&s.d_in, kStageBytes));
+    QFEC_HIP(ctx, hipMalloc(&s.d_aux, kStageBytes / 8));
+    QFEC_HIP(ctx, hipMalloc(&s.d_out, kStageBytes / 4));
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_in, kStageBytes, hipHostMallocDefault));
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_aux, kStageBytes / 8, hipHostMallocDefault));
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_out, kStageBytes / 4, hipHostMallocDefault));
+  }
+  ctx->staging_ready = true;
+  return QFEC_OK;
+}
+
+int check_fixed(qfec_ctx* ctx, uint32_t k, uint32_t L, uint64_t row_stride,
+                uint64_t group_stride, uint64_t parity_stride, uint64_t out_stride) {
+  if (k < 1 || k > QFEC_MAX_GROUP_PACKETS)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "FEC group size %u outside [1, %u]", k,
+                QFEC_MAX_GROUP_PACKETS);
+  if (L < 1 || L > QFEC_MAX_PACKET_SIZE)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "Illegal payload size: %u (max %u)", L,
+                QFEC_MAX_PACKET_SIZE);
+  if (row_stride < L || (k > 1 && group_stride < (uint64_t)(k - 1) * row_stride + L) ||
+      (k == 1 && group_stride < L) || parity_stride < L || out_stride < L)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "strides smaller than the payload length");
+  return QFEC_OK;
+}
+
+int latch_error(qfec_ctx* ctx, uint32_t bits) {
+  if (bits == 0) return QFEC_OK;
+  if (bits & qfec::kErrMissingIndex)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "missing packet index >= FEC group size");
+  if (bits & qfec::kErrGroupSize)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "FEC group with 0 or more than 255 packets");
+  if (bits & qfec::kErrParityLength)
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "Illegal FEC redundancy length");
+  return fail(ctx, QFEC_ERR_INVALID_FEC_DATA,
+              "Illegal payload size (0, > kMaxPacketSize or > redundancy length)");
+}
+
+// Read and clear the device error word after `stream` has drained.
+int collect_error(qfec_ctx* ctx, hipStream_t stream) {
+  QFEC_HIP(ctx, hipMemcpyAsync(ctx->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               stream));
+  QFEC_HIP(ctx, hipStreamSynchronize(stream));
+  const uint32_t bits = *ctx->h_err;
+  if (bits) {
+    QFEC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), stream));
+    QFEC_HIP(ctx, hipStreamSynchronize(stream));
+  }
+  return latch_error(ctx, bits);
+}
+
+// ---- host-pointer path for fixed batches ---------------------------------
+// Chunks of whole groups rotate over kSlots streams: H2D (rows [+ parity,
+// missing]) -> kernel -> D2H on one stream per slot, so chunk c+1's H2D runs
+// under chunk c's kernel and D2H.  Caller memory that is already pinned is
+// DMA'd directly; pageable memory bounces through the slot's pinned buffers.
+int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const uint8_t* missing,
+               uint32_t k, uint32_t L, uint64_t row_stride, uint64_t group_stride,
+               uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
+  int rc = ensure_staging(ctx);
+  if (rc) return rc;
+  const bool recover = parity != nullptr;
+  const bool rows_pinned = is_pinned_or_device(rows);
+  const bool par_pinned = recover && is_pinned_or_device(parity);
+  const bool out_pinned = is_pinned_or_device(out);
+  // groups per chunk bounded by every staging buffer
+  uint64_t cg = kStageBytes / group_stride;
+  cg = std::min<uint64_t>(cg, (kStageBytes / 4) / L);
+  if (recover) cg = std::min<uint64_t>(cg, (kStageBytes / 8) / (L + 1));
+  if (cg == 0) return fail(ctx, QFEC_ERR_INTERNAL, "staging too small");
+
+  struct Pending {
+    uint64_t g0 = 0, cnt = 0;
+    bool live = false;
+  } pend[kSlots];
+
+  auto finish = [&](int si) -> int {
+    Slot& s = ctx->slots[si];
+    if (!pend[si].live) return QFEC_OK;
+    QFEC_HIP(ctx, hipEventSynchronize(s.done));
+    if (!out_pinned) {
+      for (uint64_t g = 0; g < pend[si].cnt; ++g)
+        std::memcpy(out + (pend[si].g0 + g) * out_stride, s.h_out + g * L, L);
+    }
+    pend[si].live = false;
+    return QFEC_OK;
+  };
+
+  int slot = 0;
+  for (uint64_t g0 = 0; g0 < n; g0 += cg, slot = (slot + 1) % kSlots) {
+    const uint64_t cnt = std::min(cg, n - g0);
+    Slot& s = ctx->slots[slot];
+    if ((rc = finish(slot))) return rc;
+    // rows: packed [cnt][k][L] on the device side
+    const uint64_t dgs = (uint64_t)k * L;
+    const bool packed = row_stride == L && group_stride == dgs;
+    if (rows_pinned && packed) {
+      // contiguous pinned caller layout: one DMA for the whole chunk
+      QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, rows + g0 * dgs, cnt * dgs, hipMemcpyHostToDevice,
+                                   s.stream));
+    } else if (rows_pinned && group_stride == (uint64_t)k * row_stride) {
+      // uniformly strided rows: one 2-D DMA (pitch row_stride -> L)
+      QFEC_HIP(ctx, hipMemcpy2DAsync(s.d_in, L, rows + g0 * group_stride, row_stride, L,
+                                     cnt * k, hipMemcpyHostToDevice, s.stream));
+    } else if (rows_pinned) {
+      for (uint64_t g = 0; g < cnt; ++g)
+        QFEC_HIP(ctx, hipMemcpy2DAsync(s.d_in + g * dgs, L, rows + (g0 + g) * group_stride,
+                                       row_stride, L, k, hipMemcpyHostToDevice, s.stream));
+    } else {
+      for (uint64_t g = 0; g < cnt; ++g) {
+        const uint8_t* src = rows + (g0 + g) * group_stride;
+        if (row_stride == L) {
+          std::memcpy(s.h_in + g * dgs, src, dgs);
+        } else {
+          for (uint32_t i = 0; i < k; ++i)
+            std::memcpy(s.h_in + g * dgs + i * L, src + i * row_stride, L);
+        }
+      }
+      QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, s.h_in, cnt * dgs, hipMemcpyHostToDevice, s.stream));
+    }
+    uint8_t* d_par = nullptr;
+    uint8_t* d_miss = nullptr;
+    if (recover) {
+      d_par = s.d_aux;
+      d_miss = s.d_aux + cnt * L;
+      if (par_pinned) {
+        QFEC_HIP(ctx, hipMemcpy2DAsync(d_par, L, parity + g0 * parity_stride, parity_stride, L,
+                                       cnt, hipMemcpyHostToDevice, s.stream));
+      } else {
+        for (uint64_t g = 0; g < cnt; ++g)
+          std::memcpy(s.h_aux + g * L, parity + (g0 + g) * parity_stride, L);
+      }
+      std::memcpy(s.h_aux + cnt * L, missing + g0, cnt);
+      if (!par_pinned)
+        QFEC_HIP(ctx, hipMemcpyAsync(d_par, s.h_aux, cnt * L + cnt, hipMemcpyHostToDevice,
+                                     s.stream));
+      else
+        QFEC_HIP(ctx, hipMemcpyAsync(d_miss, s.h_aux + cnt * L, cnt, hipMemcpyHostToDevice,
+                                     s.stream));
+    }
+    qfec::FixedArgs a{};
+    a.rows = s.d_in;
+    a.parity = d_par;
+    a.missing = d_miss;
+    a.out = s.d_out;
+    a.row_stride = L;
+    a.group_stride = dgs;
+    a.parity_stride = L;
+    a.out_stride = L;
+    a.n_groups = cnt;
+    a.k = k;
+    a.L = L;
+    a.err = ctx->d_err;
+    QFEC_HIP(ctx, qfec::launch_fixed(a, false, s.stream));
+    if (out_pinned && out_stride == L) {
+      QFEC_HIP(ctx, hipMemcpyAsync(out + g0 * L, s.d_out, cnt * L, hipMemcpyDeviceToHost,
+                                   s.stream));
+    } else if (out_pinned) {
+      QFEC_HIP(ctx, hipMemcpy2DAsync(out + g0 * out_stride, out_stride, s.d_out, L, L, cnt,
+                                     hipMemcpyDeviceToHost, s.stream));
+    } else {
+      QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * L, hipMemcpyDeviceToHost, s.stream));
+    }
+    QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    pend[slot].g0 = g0;
+    pend[slot].cnt = cnt;
+    pend[slot].live = true;
+  }
+  for (int si = 0; si < kSlots; ++si)
+    if ((rc = finish(si))) return rc;
+  return collect_error(ctx, ctx->slots[0].stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int qfec_abi_version(void) { return QFEC_ABI_VERSION; }
+
+const char* qfec_strerror(int code) {
+  switch (code) {
+    case QFEC_OK:
+      return "QUIC_NO_ERROR";
+    case QFEC_ERR_INTERNAL:
+      return "QUIC_INTERNAL_ERROR";
+    case QFEC_ERR_INVALID_FEC_DATA:
+      return "QUIC_INVALID_FEC_DATA";
+    default:
+      return "QUIC_UNKNOWN_ERROR";
+  }
+}
+
+const char* qfec_last_error(const qfec_ctx* ctx) { return ctx ? ctx->last_error : g_tls_error; }
+
+qfec_ctx* qfec_create(int device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) {
+    fail(nullptr, QFEC_ERR_INTERNAL, "no HIP device available (%s)",
+         e != hipSuccess ? hipGetErrorString(e) : "device count 0");
+    return nullptr;
+  }
+  if (device < 0 || device >= count) {
+    fail(nullptr, QFEC_ERR_INTERNAL, "device %d out of range [0, %d)", device, count);
+    return nullptr;
+  }
+  qfec_ctx* ctx = new qfec_ctx();
+  ctx->device = device;
+  bool ok = hipSetDevice(device) == hipSuccess &&
+            hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&ctx->d_err, sizeof(uint32_t)) == hipSuccess &&
+            hipMemset(ctx->d_err, 0, sizeof(uint32_t)) == hipSuccess &&
+            hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+  if (!ok) {
+    fail(nullptr, QFEC_ERR_INTERNAL, "HIP initialisation failed on device %d", device);
+    qfec_destroy(ctx);
+    return nullptr;
+  }
+  ctx->stream = ctx->own_stream;
+  return ctx;
+}
+
+void qfec_destroy(qfec_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  for (auto& s : ctx->slots) {
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.d_in) (void)hipFree(s.d_in);
+    if (s.d_aux) (void)hipFree(s.d_aux);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.h_in) (void)hipHostFree(s.h_in);
+    if (s.h_aux) (void)hipHostFree(s.h_aux);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+  }
+  if (ctx->d_err) (void)hipFree(ctx->d_err);
+  if (ctx->h_err) (void)hipHostFree(ctx->h_err);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+int qfec_set_stream(qfec_ctx* ctx, void* hip_stream) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  return QFEC_OK;
+}
+
+void* qfec_get_stream(qfec_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int qfec_sync(qfec_ctx* ctx) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  return collect_error(ctx, ctx->stream);
+}
+
+int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
+                              uint64_t row_stride, uint64_t group_stride, uint64_t n_groups,
+                              uint8_t* parity_out, uint64_t parity_stride, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if ((rc = check_fixed(ctx, k, L, row_stride, group_stride, parity_stride, parity_stride)))
+    return rc;
+  if (n_groups == 0) return QFEC_OK;
+  if (!rows || !parity_out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST)
+    return fixed_host(ctx, rows, nullptr, nullptr, k, L, row_stride, group_stride, 0, n_groups,
+                      parity_out, parity_stride);
+  qfec::FixedArgs a{};
+  a.rows = rows;
+  a.out = parity_out;
+  a.row_stride = row_stride;
+  a.group_stride = group_stride;
+  a.out_stride = parity_stride;
+  a.n_groups = n_groups;
+  a.k = k;
+  a.L = L;
+  a.err = ctx->d_err;
+  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_NONTEMPORAL) != 0, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_encode_batch(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
+                      uint64_t n_groups, uint8_t* parity_out, uint32_t flags) {
+  return qfec_encode_batch_strided(ctx, rows, k, L, L, (uint64_t)k * L, n_groups, parity_out, L,
+                                   flags);
+}
+
+int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity,
+                               const uint8_t* missing_idx, uint32_t k, uint32_t L,
+                               uint64_t row_stride, uint64_t group_stride,
+                               uint64_t parity_stride, uint64_t n_groups, uint8_t* out,
+                               uint64_t out_stride, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if ((rc = check_fixed(ctx, k, L, row_stride, group_stride, parity_stride, out_stride)))
+    return rc;
+  if (n_groups == 0) return QFEC_OK;
+  if (!rows || !parity || !missing_idx || !out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST) {
+    for (uint64_t g = 0; g < n_groups; ++g)
+      if (missing_idx[g] >= k)
+        return fail(ctx, QFEC_ERR_INVALID_FEC_DATA,
+                    "missing packet index %u >= FEC group size %u (group %llu)", missing_idx[g],
+                    k, (unsigned long long)g);
+    return fixed_host(ctx, rows, parity, missing_idx, k, L, row_stride, group_stride,
+                      parity_stride, n_groups, out, out_stride);
+  }
+  qfec::FixedArgs a{};
+  a.rows = rows;
+  a.parity = parity;
+  a.missing = missing_idx;
+  a.out = out;
+  a.row_stride = row_stride;
+  a.group_stride = group_stride;
+  a.parity_stride = parity_stride;
+  a.out_stride = out_stride;
+  a.n_groups = n_groups;
+  a.k = k;
+  a.L = L;
+  a.err = ctx->d_err;
+  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_NONTEMPORAL) != 0, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity,
+                       const uint8_t* missing_idx, uint32_t k, uint32_t L, uint64_t n_groups,
+                       uint8_t* out, uint32_t flags) {
+  return qfec_recover_batch_strided(ctx, rows, parity, missing_idx, k, L, L, (uint64_t)k * L, L,
+                                    n_groups, out, L, flags);
+}
+
+// ---- ragged ---------------------------------------------------------------
+namespace {
+
+// Host-pointer ragged path: stage the whole batch through one device
+// allocation (ragged batches in the host path are bounded by the caller's
+// batch; the device-pointer path is the throughput path).
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_t* pkt_off,
+                const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n,
+                const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
+                const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
+                uint8_t* out, const uint64_t* out_off) {
+  const uint32_t np = grp_ptr[n] - grp_ptr[0];
+  const uint32_t pb = grp_ptr[0];
+  // byte span of the packets and of the output region
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint64_t g = 0; g < n; ++g) {
+    if (grp_ptr[g + 1] < grp_ptr[g])
+      return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "grp_ptr not monotone at group %llu",
+                  (unsigned long long)g);
+    for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) {
+      if (recover && p - grp_ptr[g] == missing[g]) continue;
+      lo = std::min(lo, pkt_off[p]);
+      hi = std::max(hi, pkt_off[p] + pkt_len[p]);
+    }
+  }
+  if (lo == UINT64_MAX) lo = hi = 0;
+  uint64_t olo = UINT64_MAX, ohi = 0, plo = UINT64_MAX, phi = 0;
+  for (uint64_t g = 0; g < n; ++g) {
+    const uint64_t o = recover ? out_off[g] : parity_off[g];
+    olo = std::min(olo, o);
+    ohi = std::max(ohi, o + QFEC_MAX_PACKET_SIZE);
+    if (recover) {
+      plo = std::min(plo, parity_off[g]);
+      phi = std::max(phi, parity_off[g] + parity_len[g]);
+    }
+  }
+  // The output span may not be fully written (gaps between groups): seed the
+  // device copy with the caller's bytes so the D2H leaves gaps unchanged.  The
+  // upper bound is clipped to the last byte any group can write.
+  uint64_t owrite_hi = 0;
+  for (uint64_t g = 0; g < n; ++g) {
+    uint32_t mx = 0;
+    if (recover) {
+      mx = parity_len[g];
+    } else {
+      for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) mx = std::max<uint32_t>(mx, pkt_len[p]);
+    }
+    owrite_hi = std::max(owrite_hi, (recover ? out_off[g] : parity_off[g]) + mx);
+  }
+  ohi = std::min(ohi, owrite_hi);
+  if (olo > ohi) olo = ohi;
+  DevBuf d_bytes, d_off, d_len, d_ptr, d_par, d_poff, d_plen, d_miss, d_out, d_ooff;
+  std::vector<uint32_t> ptr(grp_ptr, grp_ptr + n + 1);
+  for (auto& v : ptr) v -= pb;
+  std::vector<uint64_t> off(pkt_off + pb, pkt_off + pb + np);
+  for (auto& v : off) v -= (v >= lo ? lo : v);  // the lost packet's entry is never read
+  std::vector<uint64_t> ooff(n);
+  for (uint64_t g = 0; g < n; ++g) ooff[g] = (recover ? out_off[g] : parity_off[g]) - olo;
+  hipStream_t st = ctx->stream;
+  QFEC_HIP(ctx, hipMalloc(&d_bytes.p, std::max<uint64_t>(hi - lo, 1)));
+  QFEC_HIP(ctx, hipMalloc(&d_off.p, std::max<size_t>(np, 1) * 8));
+  QFEC_HIP(ctx, hipMalloc(&d_len.p, std::max<size_t>(np, 1) * 2));
+  QFEC_HIP(ctx, hipMalloc(&d_ptr.p, (n + 1) * 4));
+  QFEC_HIP(ctx, hipMalloc(&d_out.p, std::max<uint64_t>(ohi - olo, 1)));
+  QFEC_HIP(ctx, hipMalloc(&d_ooff.p, n * 8));
+  QFEC_HIP(ctx, hipMalloc(&d_plen.p, n * 2));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_bytes.p, bytes + lo, hi - lo, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_off.p, off.data(), np * 8, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_len.p, pkt_len + pb, np * 2, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_ptr.p, ptr.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, (recover ? out : parity_out) + olo, ohi - olo,
+                               hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_ooff.p, ooff.data(), n * 8, hipMemcpyHostToDevice, st));
+  qfec::RaggedArgs a{};
+  a.bytes = static_cast<const uint8_t*>(d_bytes.p);
+  a.pkt_off = static_cast<const uint64_t*>(d_off.p);
+  a.pkt_len = static_cast<const uint16_t*>(d_len.p);
+  a.grp_ptr = static_cast<const uint32_t*>(d_ptr.p);
+  a.n_groups = n;
+  a.err = ctx->d_err;
+  a.out = static_cast<uint8_t*>(d_out.p);
+  std::vector<uint64_t> poff;
+  if (recover) {
+    poff.resize(n);
+    for (uint64_t g = 0; g < n; ++g) poff[g] = parity_off[g] - plo;
+    QFEC_HIP(ctx, hipMalloc(&d_par.p, std::max<uint64_t>(phi - plo, 1)));
+    QFEC_HIP(ctx, hipMalloc(&d_poff.p, n * 8));
+    QFEC_HIP(ctx, hipMalloc(&d_miss.p, n));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_par.p, parity + plo, phi - plo, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_poff.p, poff.data(), n * 8, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_miss.p, missing, n, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_plen.p, parity_len, n * 2, hipMemcpyHostToDevice, st));
+    a.parity = static_cast<const uint8_t*>(d_par.p);
+    a.parity_off = static_cast<const uint64_t*>(d_poff.p);
+    a.parity_len = static_cast<const uint16_t*>(d_plen.p);
+    a.missing = static_cast<const uint8_t*>(d_miss.p);
+    a.out_off = static_cast<const uint64_t*>(d_ooff.p);
+  } else {
+    a.parity_off = static_cast<const uint64_t*>(d_ooff.p);
+    a.parity_len_out = static_cast<uint16_t*>(d_plen.p);
+  }
+  QFEC_HIP(ctx, qfec::launch_ragged(a, recover, st));
+  QFEC_HIP(ctx, hipMemcpyAsync((recover ? out : parity_out) + olo, d_out.p, ohi - olo,
+                               hipMemcpyDeviceToHost, st));
+  if (!recover)
+    QFEC_HIP(ctx, hipMemcpyAsync(parity_len_out, d_plen.p, n * 2, hipMemcpyDeviceToHost, st));
+  return collect_error(ctx, st);
+}
+
+}  // namespace
+
+int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
+                       const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
+                       uint8_t* parity_out, const uint64_t* parity_off,
+                       uint16_t* parity_len_out, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n_groups == 0) return QFEC_OK;
+  if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity_out || !parity_off || !parity_len_out)
+    return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST)
+    return ragged_host(ctx, false, bytes, pkt_off, pkt_len, grp_ptr, n_groups, nullptr,
+                       parity_out, parity_off, nullptr, parity_len_out, nullptr, nullptr,
+                       nullptr);
+  qfec::RaggedArgs a{};
+  a.bytes = bytes;
+  a.pkt_off = pkt_off;
+  a.pkt_len = pkt_len;
+  a.grp_ptr = grp_ptr;
+  a.parity_off = parity_off;
+  a.parity_len_out = parity_len_out;
+  a.out = parity_out;
+  a.n_groups = n_groups;
+  a.err = ctx->d_err;
+  QFEC_HIP(ctx, qfec::launch_ragged(a, false, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
+                        const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
+                        const uint8_t* parity, const uint64_t* parity_off,
+                        const uint16_t* parity_len, const uint8_t* missing_idx, uint8_t* out,
+                        const uint64_t* out_off, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n_groups == 0) return QFEC_OK;
+  if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity || !parity_off || !parity_len ||
+      !missing_idx || !out || !out_off)
+    return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST) {
+    for (uint64_t g = 0; g < n_groups; ++g) {
+      const uint32_t k = grp_ptr[g + 1] - grp_ptr[g];
+      if (grp_ptr[g + 1] < grp_ptr[g] || k == 0 || k > QFEC_MAX_GROUP_PACKETS)
+        return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "FEC group %llu has %u packets",
+                    (unsigned long long)g, k);
+      if (missing_idx[g] >= k)
+        return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "missing packet index %u >= %u",
+                    missing_idx[g], k);
+      if (parity_len[g] == 0 || parity_len[g] > QFEC_MAX_PACKET_SIZE)
+        return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "Illegal FEC redundancy length %u",
+                    parity_len[g]);
+    }
+    return ragged_host(ctx, true, bytes, pkt_off, pkt_len, grp_ptr, n_groups, parity, nullptr,
+                       parity_off, parity_len, nullptr, missing_idx, out, out_off);
+  }
+  qfec::RaggedArgs a{};
+  a.bytes = bytes;
+  a.pkt_off = pkt_off;
+  a.pkt_len = pkt_len;
+  a.grp_ptr = grp_ptr;
+  a.parity = parity;
+  a.parity_off = parity_off;
+  a.parity_len = parity_len;
+  a.missing = missing_idx;
+  a.out = out;
+  a.out_off = out_off;
+  a.n_groups = n_groups;
+  a.err = ctx->d_err;
+  QFEC_HIP(ctx, qfec::launch_ragged(a, true, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n == 0) return QFEC_OK;
+  if (!in || !out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST) {
+    DevBuf d_in, d_out;
+    QFEC_HIP(ctx, hipMalloc(&d_in.p, n));
+    QFEC_HIP(ctx, hipMalloc(&d_out.p, n));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_in.p, in, n, hipMemcpyHostToDevice, ctx->stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, out, n, hipMemcpyHostToDevice, ctx->stream));
+    QFEC_HIP(ctx, qfec::launch_xor_into(static_cast<const uint8_t*>(d_in.p), n,
+                                        static_cast<uint8_t*>(d_out.p), ctx->stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(out, d_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return QFEC_OK;
+  }
+  QFEC_HIP(ctx, qfec::launch_xor_into(in, n, out, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_synth_fixed(qfec_ctx* ctx, uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
+                     uint64_t group_stride, uint64_t g0, uint64_t n_groups, uint64_t seed) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if ((rc = check_fixed(ctx, k, L, row_stride, group_stride, L, L))) return rc;
+  if (g0 + n_groups > (1ull << 24))
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "synthetic group index beyond 2^24");
+  QFEC_HIP(ctx, qfec::launch_synth_fixed(rows, k, L, row_stride, group_stride, g0, n_groups, seed,
+                                         ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_synth_ragged(qfec_ctx* ctx, uint8_t* bytes, const uint64_t* pkt_off,
+                      const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t g0,
+                      uint64_t n_groups, uint64_t seed) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (g0 + n_groups > (1ull << 24))
+    return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "synthetic group index beyond 2^24");
+  QFEC_HIP(ctx, qfec::launch_synth_ragged(bytes, pkt_off, pkt_len, grp_ptr, g0, n_groups, seed,
+                                          ctx->stream));
+  return QFEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// qfec_internal.h — launch interface between the C-ABI (qfec_capi.cpp) and
+// the gfx950 kernels (qfec_kernels.hip).  Not installed; not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qfec {
+
+// Bits latched into the context's device error word by kernels.
+enum : uint32_t {
+  kErrMissingIndex = 1u,  // missing_idx >= k
+  kErrPacketLength = 2u,  // ragged packet length 0 or > kMaxPacketSize, or > parity_len
+  kErrGroupSize = 4u,     // ragged group with 0 or > 255 packets
+  kErrParityLength = 8u,  // ragged parity_len 0 or > kMaxPacketSize
+};
+
+// Fixed-shape encode / recover.  parity == nullptr selects encode.
+struct FixedArgs {
+  const uint8_t* rows;
+  const uint8_t* parity;   // recover only: parity rows
+  const uint8_t* missing;  // recover only: lost slot per group
+  uint8_t* out;
+  uint64_t row_stride;
+  uint64_t group_stride;
+  uint64_t parity_stride;
+  uint64_t out_stride;
+  uint64_t n_groups;
+  uint32_t k;
+  uint32_t L;
+  uint32_t* err;
+};
+
+struct RaggedArgs {
+  const uint8_t* bytes;
+  const uint64_t* pkt_off;
+  const uint16_t* pkt_len;
+  const uint32_t* grp_ptr;
+  const uint8_t* parity;      // recover: parity bytes
+  const uint64_t* parity_off; // encode: where to write; recover: where to read
+  const uint16_t* parity_len; // recover: lengths in
+  uint16_t* parity_len_out;   // encode: lengths out
+  const uint8_t* missing;     // recover
+  uint8_t* out;               // encode: parity_out; recover: revived packets
+  const uint64_t* out_off;    // recover
+  uint64_t n_groups;
+  uint32_t* err;
+};
+
+hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
+hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);
+hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_synth_fixed(uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
+                              uint64_t group_stride, uint64_t g0, uint64_t n, uint64_t seed,
+                              hipStream_t s);
+hipError_t launch_synth_ragged(uint8_t* bytes, const uint64_t* pkt_off, const uint16_t* pkt_len,
+                               const uint32_t* grp_ptr, uint64_t g0, uint64_t n, uint64_t seed,
+                               hipStream_t s);
+
+}  // namespace qfec

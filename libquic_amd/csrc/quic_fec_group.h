@@ -1,0 +1,140 @@
+// quic_fec_group.h — C++ host mirror of libquic's (removed) QuicFecGroup,
+// backed by the MI355X C-ABI (include/qfec.h).
+//
+// The reference snapshot no longer ships src/net/quic/quic_fec_group.{h,cc} or
+// quic_fec_group_interface.{h,cc} (named only by /root/reference/Makefile:5332-5384);
+// the surface below keeps the historical member names and meanings
+//  so the two hook sites can call it unchanged:
+//   send:    QuicPacketCreator::SerializePacket, after BuildDataPacket
+//            (quic_packet_creator.cc:530) and before EncryptInPlace (:549):
+//              group.Update(level, header, plaintext_after_header);
+//              ... PayloadParity() when the group closes.
+//   receive: QuicConnection::ProcessValidatedPacket (quic_connection.cc:1388-1392),
+//            which today drops FEC packets:
+//              header.fec_flag ? group.UpdateFec(level, header, redundancy)
+//                              : group.Update(level, header, decrypted_payload);
+//              if (group.CanRevive()) group.Revive(&header, buf, kMaxPacketSize);
+//
+// Difference in *where* the XOR runs: the historical class XORed every payload
+// into a 1452-byte accumulator on the connection thread.  Here a group only
+// keeps the payload bytes; the XOR runs on the GPU, either for one group when
+// PayloadParity()/Revive() is asked, or for many groups (across connections)
+// in ONE ragged kernel launch via QuicFecGroup::ComputeAll().  Results are
+// byte-identical; there is no CPU fallback — without a
+// device the group reports failure.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/qfec.h"
+
+namespace net {
+
+// quic_protocol.h mirrors (the reference's own types, same values).
+typedef uint64_t QuicPacketNumber;                 // quic_protocol.h:44
+typedef QuicPacketNumber QuicFecGroupNumber;       // historical v<=31 header field
+typedef uint64_t QuicPacketCount;
+const QuicPacketNumber kInvalidPacketNumber = 0;   // quic_protocol.h:752-753
+const size_t kMaxPacketSize = QFEC_MAX_PACKET_SIZE;  // quic_protocol.h:66
+
+enum EncryptionLevel : int8_t {  // quic_protocol.h:1173-1179
+  ENCRYPTION_NONE = 0,
+  ENCRYPTION_INITIAL = 1,
+  ENCRYPTION_FORWARD_SECURE = 2,
+  NUM_ENCRYPTION_LEVELS,
+};
+
+enum InFecGroup { NOT_IN_FEC_GROUP, IN_FEC_GROUP };  // historical v<=31 header field
+
+// The FEC-relevant part of QuicPacketHeader (quic_protocol.h:756-770) plus the
+// v<=31 group fields parsed by QuicFramer::ProcessAuthenticatedHeader
+// (quic_framer.cc:1122-1137: fec_group = packet_number - offset).
+struct QuicPacketHeader {
+  QuicPacketNumber packet_number = 0;
+  bool entropy_flag = false;
+  bool fec_flag = false;
+  InFecGroup is_in_fec_group = NOT_IN_FEC_GROUP;
+  QuicFecGroupNumber fec_group = 0;
+};
+
+// Non-owning byte view (base::StringPiece).
+struct StringPiece {
+  const char* ptr = nullptr;
+  size_t len = 0;
+  StringPiece() = default;
+  StringPiece(const char* p, size_t n) : ptr(p), len(n) {}
+  StringPiece(const std::string& s) : ptr(s.data()), len(s.size()) {}  // NOLINT
+  const char* data() const { return ptr; }
+  size_t size() const { return len; }
+  bool empty() const { return len == 0; }
+};
+
+class QuicFecGroup {
+ public:
+  // `ctx` may be null: a per-thread context on device 0 is created on first use.
+  explicit QuicFecGroup(QuicFecGroupNumber fec_group_number, qfec_ctx* ctx = nullptr);
+  ~QuicFecGroup();
+  QuicFecGroup(const QuicFecGroup&) = delete;
+  QuicFecGroup& operator=(const QuicFecGroup&) = delete;
+
+  // A data packet decrypted at `encryption_level`.  False if the packet was
+  // already seen, lies outside the protected range, or its payload is longer
+  // than kMaxPacketSize ("Illegal payload size").
+  bool Update(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+              StringPiece decrypted_payload);
+  // The FEC packet: protects [fec_group_number, header.packet_number).  False if
+  // a redundancy was already seen or a received packet is outside that range.
+  bool UpdateFec(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                 StringPiece redundancy);
+  // Exactly one protected packet is missing and the redundancy is present.
+  bool CanRevive() const;
+  // Every protected packet has been received or revived.
+  bool IsFinished() const;
+  // Writes the missing packet (zero padded to the redundancy length) and
+  // returns its length; 0 if it cannot be revived or `len` is too small.
+  size_t Revive(QuicPacketHeader* header, char* decrypted_payload, size_t len);
+  // True if this group protects packets with numbers below `num`.
+  bool IsWaitingForPacketBefore(QuicPacketNumber num) const;
+  // XOR of every payload folded in so far (data and redundancy), zero padded;
+  // on the send side this is the FEC packet's redundancy.  Computed on the GPU.
+  StringPiece PayloadParity() const;
+  QuicPacketCount NumReceivedPackets() const { return received_packets_.size(); }
+  EncryptionLevel EffectiveEncryptionLevel() const { return effective_encryption_level_; }
+  QuicFecGroupNumber FecGroupNumber() const { return fec_group_number_; }
+
+  // Compute the accumulators of many groups in ONE ragged launch (the batch
+  // path the GPU wants: groups from many connections).  Returns a qfec_*
+  // code; afterwards PayloadParity()/Revive() of every group are free.
+  static int ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups);
+
+  // Detailed reason of the last failure (QuicFramer::detailed_error style).
+  const std::string& detailed_error() const { return detailed_error_; }
+
+ private:
+  bool Fold(StringPiece payload);
+  int EnsureParity() const;
+  QuicPacketCount NumMissingPackets() const;
+  qfec_ctx* context() const;
+
+  QuicFecGroupNumber fec_group_number_;
+  qfec_ctx* ctx_;
+  std::set<QuicPacketNumber> received_packets_;
+  QuicPacketNumber min_protected_packet_ = kInvalidPacketNumber;
+  QuicPacketNumber max_protected_packet_ = kInvalidPacketNumber;
+  EncryptionLevel effective_encryption_level_ = NUM_ENCRYPTION_LEVELS;
+  // Folded payloads, packed, with their lengths (data packets and redundancy).
+  std::vector<uint8_t> bytes_;
+  std::vector<uint16_t> lens_;
+  // GPU-computed accumulator (valid when !dirty_).
+  mutable std::vector<uint8_t> parity_;
+  mutable size_t payload_parity_len_ = 0;
+  mutable bool dirty_ = false;
+  mutable std::string detailed_error_;
+};
+
+}  // namespace net

@@ -1,0 +1,216 @@
+"""ctypes binding of the qfec C-ABI (include/qfec.h) — test / bench plumbing.
+
+The product is the native library ``libquic_amd/libqfec.so`` (HIP kernels +
+C-ABI + the C++ QuicFecGroup host mirror).  This module only forwards calls;
+it never computes FEC bytes itself and has no CPU fallback: if the library or
+the GPU is missing, every call raises.
+
+Buffers may be torch tensors (device or pinned host) or numpy arrays (host);
+the caller picks ``host=True`` for host pointers (QFEC_PTR_HOST).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqfec.so")
+
+QFEC_OK = 0
+QFEC_ERR_INTERNAL = -1
+QFEC_ERR_INVALID_FEC_DATA = -5
+QFEC_PTR_DEVICE = 0
+QFEC_PTR_HOST = 1
+QFEC_NONTEMPORAL = 2
+MAX_PACKET_SIZE = 1452
+DEFAULT_MAX_PACKET_SIZE = 1350
+MAX_GROUP_PACKETS = 255
+
+# Every symbol include/qfec.h declares: (name, restype, argtypes)
+_vp, _u8p = C.c_void_p, C.c_void_p
+SIGNATURES = [
+    ("qfec_abi_version", C.c_int, []),
+    ("qfec_create", C.c_void_p, [C.c_int]),
+    ("qfec_destroy", None, [C.c_void_p]),
+    ("qfec_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("qfec_get_stream", C.c_void_p, [C.c_void_p]),
+    ("qfec_sync", C.c_int, [C.c_void_p]),
+    ("qfec_strerror", C.c_char_p, [C.c_int]),
+    ("qfec_last_error", C.c_char_p, [C.c_void_p]),
+    ("qfec_encode_batch", C.c_int,
+     [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_recover_batch", C.c_int,
+     [_vp, _u8p, _u8p, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_encode_batch_strided", C.c_int,
+     [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, _u8p, C.c_uint64,
+      C.c_uint32]),
+    ("qfec_recover_batch_strided", C.c_int,
+     [_vp, _u8p, _u8p, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+      C.c_uint64, _u8p, C.c_uint64, C.c_uint32]),
+    ("qfec_encode_ragged", C.c_int,
+     [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _vp, C.c_uint32]),
+    ("qfec_recover_ragged", C.c_int,
+     [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _vp, _u8p, _u8p, _vp, C.c_uint32]),
+    ("qfec_xor_into", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_synth_fixed", C.c_int,
+     [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+      C.c_uint64]),
+    ("qfec_synth_ragged", C.c_int,
+     [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
+]
+
+_lib = None
+
+
+class QfecError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+class InvalidFecData(QfecError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libqfec.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ImportError(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (the HIP path has no CPU fallback)")
+        lib = C.CDLL(path)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _ptr(x):
+    """Address of a torch tensor / numpy array / int / None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        assert x.flags["C_CONTIGUOUS"], "numpy buffers must be C-contiguous"
+        return x.ctypes.data
+    raise TypeError(f"unsupported buffer {type(x)!r}")
+
+
+class Context:
+    """One qfec_ctx (one device, one stream).  Thread-compatible, not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.ctx = self.lib.qfec_create(device)
+        if not self.ctx:
+            raise QfecError(QFEC_ERR_INTERNAL, self.lib.qfec_last_error(None).decode())
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            self.lib.qfec_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing --------------------------------------------------------
+    def _check(self, rc: int):
+        if rc != QFEC_OK:
+            msg = self.lib.qfec_last_error(self.ctx).decode()
+            if rc == QFEC_ERR_INVALID_FEC_DATA:
+                raise InvalidFecData(rc, msg)
+            raise QfecError(rc, msg)
+        return rc
+
+    def set_stream(self, stream):
+        """stream: torch.cuda.Stream / raw hipStream_t int / None (own stream)."""
+        h = None if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream")
+                                         else int(stream))
+        return self._check(self.lib.qfec_set_stream(self.ctx, h))
+
+    def sync(self):
+        return self._check(self.lib.qfec_sync(self.ctx))
+
+    # -- fixed -------------------------------------------------------------
+    def encode(self, rows, k, L, n_groups, parity_out, *, row_stride=None, group_stride=None,
+               parity_stride=None, host=False, nontemporal=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_NONTEMPORAL if nontemporal else 0)
+        if row_stride is None and group_stride is None and parity_stride is None:
+            rc = self.lib.qfec_encode_batch(self.ctx, _ptr(rows), k, L, n_groups,
+                                            _ptr(parity_out), fl)
+        else:
+            rs = L if row_stride is None else row_stride
+            gs = k * rs if group_stride is None else group_stride
+            ps = L if parity_stride is None else parity_stride
+            rc = self.lib.qfec_encode_batch_strided(self.ctx, _ptr(rows), k, L, rs, gs, n_groups,
+                                                    _ptr(parity_out), ps, fl)
+        return self._check(rc)
+
+    def recover(self, rows, parity, missing, k, L, n_groups, out, *, row_stride=None,
+                group_stride=None, parity_stride=None, out_stride=None, host=False,
+                nontemporal=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_NONTEMPORAL if nontemporal else 0)
+        if row_stride is None and group_stride is None and parity_stride is None \
+                and out_stride is None:
+            rc = self.lib.qfec_recover_batch(self.ctx, _ptr(rows), _ptr(parity), _ptr(missing),
+                                             k, L, n_groups, _ptr(out), fl)
+        else:
+            rs = L if row_stride is None else row_stride
+            gs = k * rs if group_stride is None else group_stride
+            ps = L if parity_stride is None else parity_stride
+            os_ = L if out_stride is None else out_stride
+            rc = self.lib.qfec_recover_batch_strided(self.ctx, _ptr(rows), _ptr(parity),
+                                                     _ptr(missing), k, L, rs, gs, ps, n_groups,
+                                                     _ptr(out), os_, fl)
+        return self._check(rc)
+
+    # -- ragged ------------------------------------------------------------
+    def encode_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity_out, parity_off,
+                      parity_len_out, *, host=False):
+        rc = self.lib.qfec_encode_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
+                                         _ptr(grp_ptr), n_groups, _ptr(parity_out),
+                                         _ptr(parity_off), _ptr(parity_len_out),
+                                         QFEC_PTR_HOST if host else 0)
+        return self._check(rc)
+
+    def recover_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity, parity_off,
+                       parity_len, missing, out, out_off, *, host=False):
+        rc = self.lib.qfec_recover_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
+                                          _ptr(grp_ptr), n_groups, _ptr(parity),
+                                          _ptr(parity_off), _ptr(parity_len), _ptr(missing),
+                                          _ptr(out), _ptr(out_off),
+                                          QFEC_PTR_HOST if host else 0)
+        return self._check(rc)
+
+    def xor_into(self, src, n, dst, *, host=False):
+        return self._check(self.lib.qfec_xor_into(self.ctx, _ptr(src), n, _ptr(dst),
+                                                  QFEC_PTR_HOST if host else 0))
+
+    # -- synthetic inputs ----------------------------------------------------
+    def synth_fixed(self, rows, k, L, g0, n_groups, seed, *, row_stride=None, group_stride=None):
+        rs = L if row_stride is None else row_stride
+        gs = k * rs if group_stride is None else group_stride
+        return self._check(self.lib.qfec_synth_fixed(self.ctx, _ptr(rows), k, L, rs, gs, g0,
+                                                     n_groups, seed))
+
+    def synth_ragged(self, data, pkt_off, pkt_len, grp_ptr, g0, n_groups, seed):
+        return self._check(self.lib.qfec_synth_ragged(self.ctx, _ptr(data), _ptr(pkt_off),
+                                                      _ptr(pkt_len), _ptr(grp_ptr), g0,
+                                                      n_groups, seed))

@@ -1,0 +1,147 @@
+"""ctypes loader for the C oracle (oracle/build/libqfec_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by libquic_amd/.  See qfec_oracle.h for
+the contract and the "parity unpinned" status.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "libqfec_oracle.so")
+_lib = None
+
+u8p = C.POINTER(C.c_uint8)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        L.qo_splitmix64.restype = C.c_uint64
+        L.qo_splitmix64.argtypes = [C.c_uint64]
+        L.qo_synth_fixed.restype = None
+        L.qo_synth_fixed.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                     C.c_uint64, C.c_uint64, C.c_void_p]
+        L.qo_synth_row.restype = None
+        L.qo_synth_row.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]
+        L.qo_ragged_k.restype = C.c_uint32
+        L.qo_ragged_k.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
+        L.qo_ragged_len.restype = C.c_uint32
+        L.qo_ragged_len.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.qo_drop_index.restype = C.c_uint32
+        L.qo_drop_index.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+        L.qo_encode_fixed.restype = C.c_int
+        L.qo_encode_fixed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64,
+                                      C.c_uint64, C.c_void_p, C.c_uint64]
+        L.qo_recover_fixed.restype = C.c_int
+        L.qo_recover_fixed.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                       C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
+                                       C.c_uint64]
+        L.qo_encode_ragged.restype = C.c_int
+        L.qo_encode_ragged.argtypes = [C.c_void_p] * 4 + [C.c_uint64] + [C.c_void_p] * 3
+        L.qo_recover_ragged.restype = C.c_int
+        L.qo_recover_ragged.argtypes = [C.c_void_p] * 4 + [C.c_uint64] + [C.c_void_p] * 6
+        L.qo_encode_fixed_mt.restype = C.c_int
+        L.qo_encode_fixed_mt.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,
+                                         C.c_void_p, C.c_int]
+        L.qo_recover_fixed_mt.restype = C.c_int
+        L.qo_recover_fixed_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.c_uint32, C.c_uint64, C.c_void_p, C.c_int]
+        L.qo_fnv1a64.restype = C.c_uint64
+        L.qo_fnv1a64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.qo_group_digest.restype = C.c_uint64
+        L.qo_group_digest.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p,
+                                      C.c_void_p, C.c_int]
+        L.qo_fixed_digests.restype = None
+        L.qo_fixed_digests.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                       C.c_uint32, C.c_int, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def synth_fixed(seed, g0, n, k, L, row_stride=None, group_stride=None):
+    rs = L if row_stride is None else row_stride
+    gs = k * rs if group_stride is None else group_stride
+    rows = np.zeros(n * gs, dtype=np.uint8)
+    lib().qo_synth_fixed(seed, g0, n, k, L, rs, gs, _p(rows))
+    return rows
+
+
+def encode_fixed(rows, k, L, n, row_stride=None, group_stride=None, parity_stride=None):
+    rs = L if row_stride is None else row_stride
+    gs = k * rs if group_stride is None else group_stride
+    ps = L if parity_stride is None else parity_stride
+    par = np.zeros(n * ps, dtype=np.uint8)
+    rc = lib().qo_encode_fixed(_p(rows), k, L, rs, gs, n, _p(par), ps)
+    return rc, par
+
+
+def recover_fixed(rows, parity, missing, k, L, n, row_stride=None, group_stride=None,
+                  parity_stride=None, out_stride=None):
+    rs = L if row_stride is None else row_stride
+    gs = k * rs if group_stride is None else group_stride
+    ps = L if parity_stride is None else parity_stride
+    os_ = L if out_stride is None else out_stride
+    out = np.zeros(n * os_, dtype=np.uint8)
+    missing = np.ascontiguousarray(missing, dtype=np.uint8)
+    rc = lib().qo_recover_fixed(_p(rows), _p(parity), _p(missing), k, L, rs, gs, ps, n,
+                                _p(out), os_)
+    return rc, out
+
+
+def encode_ragged(data, pkt_off, pkt_len, grp_ptr, parity_off, parity_size):
+    n = grp_ptr.size - 1
+    par = np.zeros(parity_size, dtype=np.uint8)
+    plen = np.zeros(n, dtype=np.uint16)
+    rc = lib().qo_encode_ragged(_p(data), _p(pkt_off), _p(pkt_len), _p(grp_ptr), n, _p(par),
+                                _p(parity_off), _p(plen))
+    return rc, par, plen
+
+
+def recover_ragged(data, pkt_off, pkt_len, grp_ptr, parity, parity_off, parity_len, missing,
+                   out_off, out_size):
+    n = grp_ptr.size - 1
+    out = np.zeros(out_size, dtype=np.uint8)
+    missing = np.ascontiguousarray(missing, dtype=np.uint8)
+    rc = lib().qo_recover_ragged(_p(data), _p(pkt_off), _p(pkt_len), _p(grp_ptr), n, _p(parity),
+                                 _p(parity_off), _p(parity_len), _p(missing), _p(out),
+                                 _p(out_off))
+    return rc, out
+
+
+def fnv1a64(buf: np.ndarray, h: int = 0) -> int:
+    buf = np.ascontiguousarray(buf)
+    return int(lib().qo_fnv1a64(_p(buf), buf.nbytes, h))
+
+
+def group_digest(base, n, stride=0, L=0, off=None, lens=None, threads=None):
+    """Checksum of per-group checksums (see qfec_oracle.h)."""
+    threads = threads or min(16, os.cpu_count() or 1)
+    return int(lib().qo_group_digest(_p(base), n, stride, L,
+                                     None if off is None else _p(off),
+                                     None if lens is None else _p(lens), threads))
+
+
+def fixed_digests(seed, drop_seed, g0, n, k, L, threads=None):
+    threads = threads or min(16, os.cpu_count() or 1)
+    a, b = C.c_uint64(0), C.c_uint64(0)
+    lib().qo_fixed_digests(seed, drop_seed, g0, n, k, L, threads, C.byref(a), C.byref(b))
+    return int(a.value), int(b.value)

@@ -1,0 +1,192 @@
+"""GPU parity tests of the ragged (CSR) HIP path and of the C++ QuicFecGroup
+host mirror, through the C-ABI, against the golden fixtures and the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle_c as OC
+from oracle import qfec_np as Q
+from libquic_amd import qfec
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).ravel().copy()).to(DEV)
+
+
+_SIGNED = {np.dtype(np.uint8): np.uint8, np.dtype(np.uint16): np.int16,
+           np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+
+
+def dview(a):
+    """device copy of an index array (bits preserved; torch lacks wide unsigned types)"""
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(_SIGNED[a.dtype]).copy()).to(DEV)
+
+
+def run_ragged(ctx, z, host=False):
+    n = z["grp_ptr"].size - 1
+    psize = z["parity"].size
+    if host:
+        par = np.zeros(psize, np.uint8)
+        plen = np.zeros(n, np.uint16)
+        ctx.encode_ragged(z["data"], z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par,
+                          z["parity_off"], plen, host=True)
+        out = np.zeros(z["recovered"].size, np.uint8)
+        ctx.recover_ragged(z["data"], z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par,
+                           z["parity_off"], plen, z["missing"], out, z["out_off"], host=True)
+        return par, plen, out
+    d = {k: dview(v) for k, v in z.items() if k in ("pkt_off", "pkt_len", "grp_ptr", "parity_off",
+                                                   "missing", "out_off")}
+    data = dev(z["data"])
+    par = torch.zeros(psize, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int16, device=DEV)
+    ctx.encode_ragged(data, d["pkt_off"], d["pkt_len"], d["grp_ptr"], n, par, d["parity_off"],
+                      plen)
+    out = torch.zeros(z["recovered"].size, dtype=torch.uint8, device=DEV)
+    ctx.recover_ragged(data, d["pkt_off"], d["pkt_len"], d["grp_ptr"], n, par, d["parity_off"],
+                       plen, d["missing"], out, d["out_off"])
+    ctx.sync()
+    torch.cuda.synchronize()
+    return par.cpu().numpy(), plen.cpu().numpy().view(np.uint16), out.cpu().numpy()
+
+
+def sub(golden, tag):
+    return {k[len(tag) + 1:]: v for k, v in golden.items() if k.startswith(tag + "_")}
+
+
+@pytest.mark.parametrize("tag", ["main", "tiny"])
+@pytest.mark.parametrize("host", [False, True])
+def test_golden_ragged(ctx, golden_ragged, tag, host):
+    z = sub(golden_ragged, tag)
+    par, plen, out = run_ragged(ctx, z, host=host)
+    assert np.array_equal(plen, z["parity_len"])
+    assert np.array_equal(par, z["parity"])
+    assert np.array_equal(out, z["recovered"])
+
+
+def synth_batch(n, kmin=5, kmax=15, lmin=64, lmax=1350, g0=0, seed=Q.SEED_RAGGED):
+    """CSR shapes from the seeded generators; bytes filled on the host by the oracle."""
+    gs = np.arange(g0, g0 + n, dtype=np.uint64)
+    ks = Q.ragged_k(seed, gs, kmin, kmax)
+    ptr = np.zeros(n + 1, np.uint32)
+    ptr[1:] = np.cumsum(ks)
+    gidx = np.repeat(gs, ks)
+    iidx = np.arange(ptr[-1]) - np.repeat(ptr[:-1].astype(np.int64), ks)
+    ln = Q.ragged_len(seed, gidx, iidx, lmin, lmax).astype(np.uint16)
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    return ks, ptr, ln, off
+
+
+def test_ragged_synth_vs_oracle(ctx):
+    n = 20_000
+    ks, ptr, ln, off = synth_batch(n, g0=77)
+    total = int(off[-1] + ln[-1])
+    data_d = torch.zeros(total, dtype=torch.uint8, device=DEV)
+    ctx.synth_ragged(data_d, dview(off), dview(ln), dview(ptr), 77, n, Q.SEED_RAGGED)
+    ctx.sync()
+    data = data_d.cpu().numpy()
+    # device bytes == oracle bytes for a sample of packets
+    for p in np.random.default_rng(0).choice(ln.size, 200, replace=False):
+        g = int(np.searchsorted(ptr, p, side="right") - 1)
+        i = int(p - ptr[g])
+        want = np.zeros(int(ln[p]), np.uint8)
+        OC.lib().qo_synth_row(Q.SEED_RAGGED, 77 + g, i, int(ln[p]), OC._p(want))
+        assert np.array_equal(data[int(off[p]):int(off[p]) + int(ln[p])], want)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(77, 77 + n), ks).astype(np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1452)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged(ctx, z)
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
+
+
+def test_ragged_edges(ctx):
+    # k = 1, k = 255, len 1..1452, len < 16 mixed with long packets, scattered offsets
+    rng = np.random.default_rng(3)
+    groups = [[1452], [1], [15, 1452, 16, 17], [3] * 255, list(rng.integers(1, 1453, 255)),
+              [64, 1350], [16], [17, 1]]
+    ln = np.array([l for g in groups for l in g], np.uint16)
+    ptr = np.zeros(len(groups) + 1, np.uint32)
+    ptr[1:] = np.cumsum([len(g) for g in groups])
+    gap = rng.integers(0, 40, ln.size).astype(np.uint64)  # unaligned, gapped offsets
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gap[:-1])
+    data = rng.integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    n = len(groups)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1500) + np.uint64(3)
+    miss = np.array([rng.integers(0, len(g)) for g in groups], np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1500 + 3)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1500 + 3)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    for host in (False, True):
+        par, plen, out = run_ragged(ctx, z, host=host)
+        assert np.array_equal(plen, want_l)
+        assert np.array_equal(par, want_p)
+        assert np.array_equal(out, want_o)
+
+
+def test_ragged_errors(ctx):
+    def call(ln, ptr, miss=None, plen=None):
+        n = ptr.size - 1
+        off = np.zeros(ln.size, np.uint64)
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+        data = np.zeros(max(int(ln.astype(np.int64).sum()), 1), np.uint8)
+        poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+        if miss is None:
+            ctx.encode_ragged(dev(data), dview(off), dview(ln), dview(ptr), n,
+                              torch.zeros(n * 1452, dtype=torch.uint8, device=DEV),
+                              dview(poff), torch.zeros(n, dtype=torch.int16, device=DEV))
+        else:
+            ctx.recover_ragged(dev(data), dview(off), dview(ln), dview(ptr), n,
+                               torch.zeros(n * 1452, dtype=torch.uint8, device=DEV),
+                               dview(poff), dview(plen), dview(miss),
+                               torch.zeros(n * 1452, dtype=torch.uint8, device=DEV), dview(poff))
+        ctx.sync()
+
+    with pytest.raises(qfec.InvalidFecData):
+        call(np.array([1453], np.uint16), np.array([0, 1], np.uint32))      # > kMaxPacketSize
+    with pytest.raises(qfec.InvalidFecData):
+        call(np.array([0, 5], np.uint16), np.array([0, 2], np.uint32))      # empty payload
+    with pytest.raises(qfec.InvalidFecData):
+        call(np.array([5], np.uint16), np.array([0, 1, 1], np.uint32))      # group of 0 packets
+    with pytest.raises(qfec.InvalidFecData):
+        call(np.array([5] * 256, np.uint16), np.array([0, 256], np.uint32))  # 256 packets
+    with pytest.raises(qfec.InvalidFecData):  # missing index >= k
+        call(np.array([5, 5], np.uint16), np.array([0, 2], np.uint32), np.array([2], np.uint8),
+             np.array([5], np.uint16))
+    with pytest.raises(qfec.InvalidFecData):  # received packet longer than the redundancy
+        call(np.array([5, 9], np.uint16), np.array([0, 2], np.uint32), np.array([0], np.uint8),
+             np.array([5], np.uint16))
+    with pytest.raises(qfec.InvalidFecData):  # redundancy length 0
+        call(np.array([5, 5], np.uint16), np.array([0, 2], np.uint32), np.array([0], np.uint8),
+             np.array([0], np.uint16))
+    # valid call after errors works
+    call(np.array([5, 5], np.uint16), np.array([0, 2], np.uint32))
+
+
+def test_cpp_quic_fec_group():
+    """C++ host mirror (QuicFecGroup + wire format) against the oracle."""
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "test_quic_fec_group")
+    assert os.path.exists(exe), "build with __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stderr
+    assert " 0 failures" in r.stdout
