@@ -42,7 +42,8 @@ def parse():
     p.add_argument("--groups", type=int, default=1 << 20, help="FEC groups per GPU")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--L", type=int, default=1350)
-    p.add_argument("--nontemporal", action="store_true")
+    p.add_argument("--cached", action="store_true",
+                   help="default cache policy instead of nt loads/stores")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-ragged", action="store_true")
@@ -84,16 +85,7 @@ def cpu_baseline(k, L, seconds):
     mt, reps_mt = run(threads)
     st, reps_st = run(1)
     # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
-    one = rows[: k * L].copy()
-    p1 = np.zeros(L, np.uint8)
-    o1 = np.zeros(L, np.uint8)
-    m1 = miss[:1].copy()
-    it = 20000
-    t0 = time.perf_counter()
-    for _ in range(it):
-        lib.qo_encode_fixed(OC._p(one), k, L, L, k * L, 1, OC._p(p1), L)
-        lib.qo_recover_fixed(OC._p(one), OC._p(p1), OC._p(m1), k, L, L, k * L, L, 1, OC._p(o1), L)
-    ns_group = (time.perf_counter() - t0) / it * 1e9
+    ns_group = lib.qo_time_single_group_ns(k, L, 200000)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -150,10 +142,10 @@ def main():
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        ctx.encode(rows, k, L, G, par, nontemporal=args.nontemporal)
+        ctx.encode(rows, k, L, G, par, cached=args.cached)
         if ev:
             ev[1].record(stream)
-        ctx.recover(rows, par, miss, k, L, G, out, nontemporal=args.nontemporal)
+        ctx.recover(rows, par, miss, k, L, G, out, cached=args.cached)
         if ev:
             ev[2].record(stream)
 

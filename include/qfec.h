@@ -73,7 +73,10 @@ extern "C" {
                                stages through the context (pinned, chunked,
                                overlapped H2D / kernel / D2H) and returns when the
                                results are back in host memory */
-#define QFEC_NONTEMPORAL 2u /* stream rows with non-temporal loads (device ptrs) */
+#define QFEC_CACHED 2u      /* fixed-shape device calls: use the default cache
+                               policy instead of non-temporal (nt) loads and
+                               stores — for small batches whose output is
+                               consumed straight away from L2 / MALL */
 
 typedef struct qfec_ctx qfec_ctx;
 
@@ -83,9 +86,12 @@ typedef struct qfec_ctx qfec_ctx;
 qfec_ctx* qfec_create(int device);
 void qfec_destroy(qfec_ctx* ctx);
 /* Use an existing hipStream_t (e.g. torch's current stream) for device-pointer
- * calls.  NULL restores the context's own stream. */
+ * calls; NULL is HIP's null (default) stream, as in the HIP API.  A new
+ * context uses a non-blocking stream of its own, returned by
+ * qfec_own_stream() (pass it back to restore it). */
 int qfec_set_stream(qfec_ctx* ctx, void* hip_stream);
 void* qfec_get_stream(qfec_ctx* ctx);
+void* qfec_own_stream(qfec_ctx* ctx);
 /* Wait for all queued work; returns the first error latched by a kernel
  * (e.g. a missing index >= k or a ragged length > kMaxPacketSize found on the
  * device) since the previous qfec_sync, then clears it. */

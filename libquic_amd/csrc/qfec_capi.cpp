@@ -212,7 +212,10 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
     if (recover) {
       d_par = s.d_aux;
       d_miss = s.d_aux + cnt * L;
-      if (par_pinned) {
+      if (par_pinned && parity_stride == L) {
+        QFEC_HIP(ctx, hipMemcpyAsync(d_par, parity + g0 * L, cnt * L, hipMemcpyHostToDevice,
+                                     s.stream));
+      } else if (par_pinned) {
         QFEC_HIP(ctx, hipMemcpy2DAsync(d_par, L, parity + g0 * parity_stride, parity_stride, L,
                                        cnt, hipMemcpyHostToDevice, s.stream));
       } else {
@@ -240,7 +243,7 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
     a.k = k;
     a.L = L;
     a.err = ctx->d_err;
-    QFEC_HIP(ctx, qfec::launch_fixed(a, false, s.stream));
+    QFEC_HIP(ctx, qfec::launch_fixed(a, true, s.stream));
     if (out_pinned && out_stride == L) {
       QFEC_HIP(ctx, hipMemcpyAsync(out + g0 * L, s.d_out, cnt * L, hipMemcpyDeviceToHost,
                                    s.stream));
@@ -331,11 +334,13 @@ void qfec_destroy(qfec_ctx* ctx) {
 
 int qfec_set_stream(qfec_ctx* ctx, void* hip_stream) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
-  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  ctx->stream = static_cast<hipStream_t>(hip_stream);
   return QFEC_OK;
 }
 
 void* qfec_get_stream(qfec_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+void* qfec_own_stream(qfec_ctx* ctx) { return ctx ? (void*)ctx->own_stream : nullptr; }
 
 int qfec_sync(qfec_ctx* ctx) {
   int rc = bind(ctx);
@@ -365,7 +370,7 @@ int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, ui
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
-  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_NONTEMPORAL) != 0, ctx->stream));
+  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
   return QFEC_OK;
 }
 
@@ -408,7 +413,7 @@ int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
-  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_NONTEMPORAL) != 0, ctx->stream));
+  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
   return QFEC_OK;
 }
 

@@ -47,6 +47,7 @@ struct RaggedArgs {
   uint32_t* err;
 };
 
+// nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);
 hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);

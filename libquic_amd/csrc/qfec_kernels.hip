@@ -55,29 +55,13 @@ __device__ __forceinline__ u32x4 ld16t(const uint8_t* p) {
 
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 
-// Logical right shift of a 16-byte little-endian vector by `sh` bytes (0..15),
-// zero fill.  Used for the window that ends at a short packet's last byte.
-__device__ __forceinline__ u32x4 shr_bytes(u32x4 v, uint32_t sh) {
-  uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
-  uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
-  const uint32_t bits = sh * 8u;
-  uint64_t nlo, nhi;
-  if (bits >= 64u) {
-    nlo = hi >> (bits - 64u);
-    nhi = 0;
-  } else if (bits == 0u) {
-    nlo = lo;
-    nhi = hi;
+template <bool NT>
+__device__ __forceinline__ void st16t(uint8_t* p, u32x4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
   } else {
-    nlo = (lo >> bits) | (hi << (64u - bits));
-    nhi = hi >> bits;
+    st16(p, v);
   }
-  u32x4 r;
-  r.x = (uint32_t)nlo;
-  r.y = (uint32_t)(nlo >> 32);
-  r.z = (uint32_t)nhi;
-  r.w = (uint32_t)(nhi >> 32);
-  return r;
 }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
@@ -154,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
       for (; i < k; ++i) acc ^= ld16t<NT>(src + i * a.row_stride);
     }
   }
-  st16(a.out + g * a.out_stride + off, acc);
+  st16t<NT>(a.out + g * a.out_stride + off, acc);
 }
 
 // Fixed shape, L < 16 (degenerate tiny packets): one lane per output byte.
@@ -184,19 +168,36 @@ __global__ __launch_bounds__(kBlock) void fixed_small_kernel(FixedArgs a) {
 // ---------------------------------------------------------------------------
 // Ragged CSR: one wave per group.
 // ---------------------------------------------------------------------------
-// Bytes [win, win+16) of a zero-padded packet of `len` bytes (len >= 16).
-__device__ __forceinline__ u32x4 window16(const uint8_t* row, uint32_t len, uint32_t win) {
-  u32x4 v = {0u, 0u, 0u, 0u};
-  if (win < len) {
-    const bool full = win + 16u <= len;
-    const uint32_t ld = full ? win : len - 16u;
-    v = ld16(row + ld);
-    if (!full) v = shr_bytes(v, win + 16u - len);
-  }
-  return v;
+// Right shift of a 16-byte vector by sh bytes (0..15), zero fill, branch-free:
+// a word select by sh/4, then v_alignbyte_b32 by sh%4.
+__device__ __forceinline__ u32x4 shr_bytes_bf(u32x4 v, uint32_t sh) {
+  const uint32_t q = sh >> 2, r = sh & 3u;
+  const uint32_t s0 = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+  const uint32_t s1 = q == 0 ? v.y : q == 1 ? v.z : q == 2 ? v.w : 0u;
+  const uint32_t s2 = q == 0 ? v.z : q == 1 ? v.w : 0u;
+  const uint32_t s3 = q == 0 ? v.w : 0u;
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(s1, s0, r);
+  o.y = __builtin_amdgcn_alignbyte(s2, s1, r);
+  o.z = __builtin_amdgcn_alignbyte(s3, s2, r);
+  o.w = __builtin_amdgcn_alignbyte(0u, s3, r);
+  return o;
 }
 
-// Same for len < 16 (uniform branch per packet; rare).
+// Bytes [win, win+16) of a zero-padded packet of `len` bytes, len >= 16.
+// Always ONE 16-byte load inside the packet (no exec-masked branch): a window
+// that crosses the packet end loads the 16 bytes ending at its last byte and
+// shifts them down; a window past the end is zeroed by a select.
+template <bool NT>
+__device__ __forceinline__ u32x4 window16(const uint8_t* row, uint32_t len, uint32_t win) {
+  const bool full = win + 16u <= len;
+  u32x4 v = ld16t<NT>(row + (full ? win : len - 16u));
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  v = win < len ? v : z;
+  return full ? v : shr_bytes_bf(v, min(win + 16u - len, 15u));
+}
+
+// Same for len < 16 (wave-uniform branch per packet; rare).
 __device__ __forceinline__ u32x4 window16_small(const uint8_t* row, uint32_t len, uint32_t win) {
   uint8_t b[16];
 #pragma unroll
@@ -206,7 +207,11 @@ __device__ __forceinline__ u32x4 window16_small(const uint8_t* row, uint32_t len
   return v;
 }
 
-template <bool RECOVER>
+// Lane l of the wave owns parity windows at 16*l and 16*l + 1024 (plen <= 1452
+// needs at most two), clamped so the last window ends at parity_len.  The
+// group's packet lengths/offsets are loaded once, one packet per lane, and
+// broadcast per row with v_readlane (no per-row scalar-load latency).
+template <bool RECOVER, bool NT>
 __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) +
@@ -234,8 +239,9 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
     }
     uint32_t bad = 0;
     for (uint32_t i = lane; i < k; i += 64u) {
+      if (i == m) continue;  // the lost packet's entries are never read
       const uint32_t l = a.pkt_len[p0 + i];
-      if (i != m) bad |= (l == 0u || l > plen) ? 1u : 0u;
+      bad |= (l == 0u || l > plen) ? 1u : 0u;
     }
     if (wave_or(bad)) {
       if (lane == 0) atomicOr(a.err, kErrPacketLength);
@@ -259,19 +265,43 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
   uint8_t* dst = a.out + (RECOVER ? a.out_off[g] : a.parity_off[g]);
 
   if (plen >= 16u) {
-    for (uint32_t w0 = 0; w0 < plen; w0 += 1024u) {
-      const uint32_t w = w0 + lane * 16u;
-      const uint32_t win = min(w, plen - 16u);
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      if constexpr (RECOVER) acc = ld16(par + win);
-      for (uint32_t i = 0; i < k; ++i) {
-        if (i == m) continue;  // wave-uniform
-        const uint32_t len = a.pkt_len[p0 + i];
-        const uint8_t* row = a.bytes + a.pkt_off[p0 + i];
-        acc ^= (len >= 16u) ? window16(row, len, win) : window16_small(row, len, win);
-      }
-      if (w < plen) st16(dst + win, acc);
+    const uint32_t w = lane * 16u;
+    const uint32_t win0 = min(w, plen - 16u);
+    const uint32_t win1 = min(w + 1024u, plen - 16u);
+    const bool two = plen > 1024u;  // wave-uniform
+    const uint32_t lo1 = min(1024u, plen - 16u);  // lowest byte any second window covers
+    u32x4 acc0 = {0u, 0u, 0u, 0u}, acc1 = {0u, 0u, 0u, 0u};
+    if constexpr (RECOVER) {
+      acc0 = ld16t<NT>(par + win0);
+      if (two) acc1 = ld16t<NT>(par + win1);
     }
+    for (uint32_t c = 0; c < k; c += 64u) {
+      const uint32_t cnt = min(64u, k - c);
+      uint32_t lenr = 0, offlo = 0, offhi = 0;
+      if (lane < cnt && c + lane != m) {
+        lenr = a.pkt_len[p0 + c + lane];
+        const uint64_t o = a.pkt_off[p0 + c + lane];
+        offlo = (uint32_t)o;
+        offhi = (uint32_t)(o >> 32);
+      }
+#pragma unroll 2
+      for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)i);
+        if (len == 0u) continue;  // the lost packet (wave-uniform)
+        const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)i)
+                              << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)i);
+        const uint8_t* row = a.bytes + off;
+        if (len >= 16u) {
+          acc0 ^= window16<NT>(row, len, win0);
+          if (two && len > lo1) acc1 ^= window16<NT>(row, len, win1);
+        } else {
+          acc0 ^= window16_small(row, len, win0);
+        }
+      }
+    }
+    if (w < plen) st16t<NT>(dst + win0, acc0);
+    if (two && w + 1024u < plen) st16t<NT>(dst + win1, acc1);
   } else {
     // Whole group fits in one window: one lane per byte.
     if (lane < plen) {
@@ -451,9 +481,11 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
     }
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
     if (recover)
-      hipLaunchKernelGGL(ragged_xor_kernel<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((ragged_xor_kernel<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0,
+                         s, a);
     else
-      hipLaunchKernelGGL(ragged_xor_kernel<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((ragged_xor_kernel<false, true>), dim3((uint32_t)blocks), dim3(kBlock),
+                         0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

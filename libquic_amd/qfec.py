@@ -21,7 +21,7 @@ QFEC_ERR_INTERNAL = -1
 QFEC_ERR_INVALID_FEC_DATA = -5
 QFEC_PTR_DEVICE = 0
 QFEC_PTR_HOST = 1
-QFEC_NONTEMPORAL = 2
+QFEC_CACHED = 2
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
 MAX_GROUP_PACKETS = 255
@@ -34,6 +34,7 @@ SIGNATURES = [
     ("qfec_destroy", None, [C.c_void_p]),
     ("qfec_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("qfec_get_stream", C.c_void_p, [C.c_void_p]),
+    ("qfec_own_stream", C.c_void_p, [C.c_void_p]),
     ("qfec_sync", C.c_int, [C.c_void_p]),
     ("qfec_strerror", C.c_char_p, [C.c_int]),
     ("qfec_last_error", C.c_char_p, [C.c_void_p]),
@@ -140,18 +141,22 @@ class Context:
         return rc
 
     def set_stream(self, stream):
-        """stream: torch.cuda.Stream / raw hipStream_t int / None (own stream)."""
-        h = None if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream")
-                                         else int(stream))
-        return self._check(self.lib.qfec_set_stream(self.ctx, h))
+        """stream: torch.cuda.Stream (its handle; torch's default stream is HIP's
+        null stream, handle 0) / raw hipStream_t int / None (the context's own
+        non-blocking stream)."""
+        if stream is None:
+            h = self.lib.qfec_own_stream(self.ctx)
+        else:
+            h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        return self._check(self.lib.qfec_set_stream(self.ctx, h or None))
 
     def sync(self):
         return self._check(self.lib.qfec_sync(self.ctx))
 
     # -- fixed -------------------------------------------------------------
     def encode(self, rows, k, L, n_groups, parity_out, *, row_stride=None, group_stride=None,
-               parity_stride=None, host=False, nontemporal=False):
-        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_NONTEMPORAL if nontemporal else 0)
+               parity_stride=None, host=False, cached=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_CACHED if cached else 0)
         if row_stride is None and group_stride is None and parity_stride is None:
             rc = self.lib.qfec_encode_batch(self.ctx, _ptr(rows), k, L, n_groups,
                                             _ptr(parity_out), fl)
@@ -165,8 +170,8 @@ class Context:
 
     def recover(self, rows, parity, missing, k, L, n_groups, out, *, row_stride=None,
                 group_stride=None, parity_stride=None, out_stride=None, host=False,
-                nontemporal=False):
-        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_NONTEMPORAL if nontemporal else 0)
+                cached=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_CACHED if cached else 0)
         if row_stride is None and group_stride is None and parity_stride is None \
                 and out_stride is None:
             rc = self.lib.qfec_recover_batch(self.ctx, _ptr(rows), _ptr(parity), _ptr(missing),

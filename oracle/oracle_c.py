@@ -61,6 +61,8 @@ def lib():
                                           C.c_uint32, C.c_uint64, C.c_void_p, C.c_int]
         L.qo_fnv1a64.restype = C.c_uint64
         L.qo_fnv1a64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.qo_time_single_group_ns.restype = C.c_double
+        L.qo_time_single_group_ns.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
         L.qo_group_digest.restype = C.c_uint64
         L.qo_group_digest.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p,
                                       C.c_void_p, C.c_int]

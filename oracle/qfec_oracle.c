@@ -16,11 +16,13 @@
  *   - revive = parity XOR every received payload; its length is parity_len and
  *     the zero tail parses as one PADDING frame (quic_framer.cc:1224-1231).
  */
+#define _POSIX_C_SOURCE 199309L
 #include "qfec_oracle.h"
 
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 uint64_t qo_splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -345,4 +347,27 @@ void qo_fixed_digests(uint64_t seed, uint64_t drop_seed, uint64_t g0, uint64_t n
   *recovered_digest = qo_fnv1a64((const uint8_t*)rh, n * sizeof(uint64_t), 0);
   free(ph);
   free(rh);
+}
+
+double qo_time_single_group_ns(uint32_t k, uint32_t L, uint64_t iters) {
+  uint8_t* rows = (uint8_t*)malloc((size_t)k * L);
+  uint8_t par[QO_MAX_PACKET_SIZE], out[QO_MAX_PACKET_SIZE];
+  qo_synth_fixed(0x51554943u, 0, 1, k, L, L, (uint64_t)k * L, rows);
+  uint8_t m = (uint8_t)qo_drop_index(0x51554945u, 0, k);
+  volatile uint8_t sink = 0;
+  for (int w = 0; w < 1000; ++w) {
+    qo_encode_fixed(rows, k, L, L, (uint64_t)k * L, 1, par, L);
+    qo_recover_fixed(rows, par, &m, k, L, L, (uint64_t)k * L, L, 1, out, L);
+  }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (uint64_t it = 0; it < iters; ++it) {
+    qo_encode_fixed(rows, k, L, L, (uint64_t)k * L, 1, par, L);
+    qo_recover_fixed(rows, par, &m, k, L, L, (uint64_t)k * L, L, 1, out, L);
+    sink ^= out[it % L];
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  (void)sink;
+  free(rows);
+  return ((t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec)) / (double)iters;
 }

@@ -82,6 +82,10 @@ int qo_encode_fixed_mt(const uint8_t* rows, uint32_t k, uint32_t L, uint64_t n,
 int qo_recover_fixed_mt(const uint8_t* rows, const uint8_t* parity, const uint8_t* missing,
                         uint32_t k, uint32_t L, uint64_t n, uint8_t* out, int threads);
 
+/* configs[0] timer: mean ns for encode + recover of ONE group of k x L
+ * (1 core), over `iters` repetitions after a warm-up. */
+double qo_time_single_group_ns(uint32_t k, uint32_t L, uint64_t iters);
+
 /* FNV-1a 64 over a buffer (checksums for large-size property tests) */
 uint64_t qo_fnv1a64(const uint8_t* p, size_t n, uint64_t h);
 

@@ -43,5 +43,6 @@ def ctx():
         pytest.fail("GPU test selected but no HIP device is visible")
     from libquic_amd import qfec
     c = qfec.Context(0)
+    c.set_stream(torch.cuda.current_stream())  # order with torch's copies/fills
     yield c
     c.close()

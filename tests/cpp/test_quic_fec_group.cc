@@ -72,15 +72,19 @@ static void ReviveCase(qfec_ctx* ctx, int k, int lost, int fec_pos) {
   std::string redundancy = OracleParity(pays);
   QuicFecGroup group(first, ctx);
   int seen = 0;
+  bool fec_done = false;
   for (int i = 0; i < k; ++i) {
-    if (seen == fec_pos)
+    if (!fec_done && seen == fec_pos) {
       EXPECT(group.UpdateFec(ENCRYPTION_FORWARD_SECURE, Header(first + k, first, true),
                              redundancy));
+      fec_done = true;
+    }
     if (i == lost) continue;
+    EXPECT(!group.CanRevive() || fec_done);
     EXPECT(group.Update(ENCRYPTION_FORWARD_SECURE, Header(first + i, first, false), pays[i]));
     ++seen;
   }
-  if (seen == fec_pos)
+  if (!fec_done)
     EXPECT(group.UpdateFec(ENCRYPTION_FORWARD_SECURE, Header(first + k, first, true), redundancy));
   EXPECT(group.CanRevive());
   EXPECT(!group.IsFinished());

@@ -91,12 +91,12 @@ def test_unaligned_buffers(ctx, shift):
     assert np.array_equal(out.reshape(n, L), rows.reshape(n, k, L)[np.arange(n), miss])
 
 
-def test_nontemporal_same_result(ctx):
+def test_cached_policy_same_result(ctx):
     k, L, n = 10, 1350, 300
     rows = OC.synth_fixed(3, 0, n, k, L)
     miss = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
     p1, o1 = run_fixed(ctx, rows, k, L, n, miss)
-    p2, o2 = run_fixed(ctx, rows, k, L, n, miss, nontemporal=True)
+    p2, o2 = run_fixed(ctx, rows, k, L, n, miss, cached=True)
     assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
 
 

@@ -19,7 +19,7 @@ cat "$OUT/smoke.log"
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok_or_fail $? bench
 cat "$OUT/bench.json"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof" -o run \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
   -- python bench.py --profile-only --steps 10 --no-verify > "$OUT/prof.log" 2>&1
 ok_or_fail $? rocprof_stats
 find "$OUT/prof" -name '*stats*' | head
