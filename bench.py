@@ -104,6 +104,141 @@ def cpu_baseline(k, L, seconds):
     }
 
 
+class HipFixedWorkload:
+    """The product path on one GPU: G groups x k x L resident in HBM; one step =
+    encode (qfec_encode_batch) + single-loss recover (qfec_recover_batch), both
+    on `stream`, bracketed by HIP events on that same stream."""
+
+    def __init__(self, torch, dev, g0, G, k, L, cached=False):
+        from libquic_amd import qfec
+        self.torch, self.dev, self.g0, self.G, self.k, self.L = torch, dev, g0, G, k, L
+        self.cached = cached
+        self.ctx = qfec.Context(dev.index)
+        self.stream = torch.cuda.current_stream()
+        self.ctx.set_stream(self.stream)
+        self.rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
+        self.par = torch.empty(G * L, dtype=torch.uint8, device=dev)
+        self.out = torch.empty(G * L, dtype=torch.uint8, device=dev)
+        self.miss = torch.from_numpy(drop_indices(g0, G, k)).to(dev)
+        self.ctx.synth_fixed(self.rows, k, L, g0, G, SEED_FIXED)
+        self.ctx.sync()
+        self.bytes_encode = G * (k * L + L)
+        self.bytes_recover = G * ((k - 1) * L + 2 * L)
+
+    def new_events(self):
+        return [self.torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step(self, ev=None):
+        k, L, G = self.k, self.L, self.G
+        if ev:
+            ev[0].record(self.stream)
+        self.ctx.encode(self.rows, k, L, G, self.par, cached=self.cached)
+        if ev:
+            ev[1].record(self.stream)
+        self.ctx.recover(self.rows, self.par, self.miss, k, L, G, self.out, cached=self.cached)
+        if ev:
+            ev[2].record(self.stream)
+
+    def synchronize(self):
+        self.ctx.sync()
+        self.torch.cuda.synchronize()
+
+    def kernel_seconds(self, events):
+        enc = np.array([e[0].elapsed_time(e[1]) for e in events]).mean() / 1e3
+        rec = np.array([e[1].elapsed_time(e[2]) for e in events]).mean() / 1e3
+        return float(enc), float(rec)
+
+    def verify(self):
+        """Round trip on every group + parity XOR all rows == 0 (device, untimed).
+        Bit-exactness against the oracle is tests/test_hip_fixed.py's job."""
+        torch, G, k, L = self.torch, self.G, self.k, self.L
+        r3 = self.rows.view(G, k, L)
+        ok = torch.equal(r3[torch.arange(G, device=self.dev), self.miss.long()],
+                         self.out.view(G, L))
+        acc = self.par.view(G, L).clone()
+        for i in range(k):
+            acc ^= r3[:, i]
+        return bool(ok) and not bool(acc.any())
+
+    def release(self):
+        del self.rows
+        self.torch.cuda.empty_cache()
+
+
+def timed_steps(work, steps, warmup, barrier, reduce_max):
+    """The measurement contract: W untimed steps, then exactly K steps bracketed
+    by barrier + synchronize on both sides; elapsed = max over ranks."""
+    for _ in range(warmup):
+        work.step()
+    work.synchronize()
+    events = [work.new_events() for _ in range(steps)]
+    barrier()
+    work.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        work.step(events[s])
+    work.synchronize()
+    elapsed = reduce_max(time.perf_counter() - t0)
+    barrier()
+    return elapsed, events
+
+
+def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_recover,
+                enc_s=None, rec_s=None, traffic=None, verified=None):
+    """The JSON line (rank 0).  value = algorithmic bytes of ALL ranks / max time."""
+    total = world * steps * (bytes_encode + bytes_recover)
+    line = {
+        "metric": "FEC XOR encode+recover GiB/s (device-resident) on batched 1350B packet groups",
+        "value": round(total / 2**30 / elapsed, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (counter-based splitmix64 bytes generated in HBM)",
+        "config": {
+            "workload": f"{G} groups x {k} x {L} B per GPU: parity encode + single-loss "
+                        f"recover (BASELINE configs[1]+[2])",
+            "groups_per_gpu": G, "k": k, "L": L,
+            "parallelism": f"group-shard x{world} (no collective)",
+        },
+        "roofline": None,
+        "verified": verified,
+    }
+    if enc_s:
+        enc_gbs = bytes_encode / enc_s / 1e9
+        rec_gbs = bytes_recover / rec_s / 1e9
+        line["roofline"] = {
+            "bound": "hbm",
+            "kernel": "fixed_xor_kernel<10, false, true, false> (encode, k=10, nt)",
+            "achieved": round(enc_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_encode,
+            "avg_launch_us": round(enc_s * 1e6, 2),
+        }
+        line["encode_GiBps"] = round(bytes_encode / enc_s / 2**30, 2)
+        line["recover_GiBps"] = round(bytes_recover / rec_s / 2**30, 2)
+        line["recover_roofline_frac"] = round(rec_gbs / HBM_PEAK_GBS, 4)
+    return line
+
+
+def measured_traffic(G, k, L):
+    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("groups") == G and tj.get("k") == k and tj.get("L") == L:
+            return tj.get("encode_hbm_bytes_per_launch")
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -120,138 +255,40 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from libquic_amd import qfec
+    def barrier():
+        if world > 1:
+            dist.barrier()
 
-    ctx = qfec.Context(dev.index)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream)
+    def reduce_max(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     k, L, G = args.k, args.L, args.groups
-    g0 = rank * G
-    bytes_enc = G * (k * L + L)
-    bytes_rec = G * ((k - 1) * L + 2 * L)
+    work = HipFixedWorkload(torch, dev, rank * G, G, k, L, cached=args.cached)
+    work.step()
+    work.synchronize()
+    verified = None if args.no_verify else work.verify()
+    elapsed, events = timed_steps(work, args.steps, args.warmup, barrier, reduce_max)
+    enc_s, rec_s = work.kernel_seconds(events)
+    line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
+                       work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified)
 
-    rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
-    par = torch.empty(G * L, dtype=torch.uint8, device=dev)
-    out = torch.empty(G * L, dtype=torch.uint8, device=dev)
-    miss_np = drop_indices(g0, G, k)
-    miss = torch.from_numpy(miss_np).to(dev)
-    ctx.synth_fixed(rows, k, L, g0, G, SEED_FIXED)
-    ctx.sync()
-
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        ctx.encode(rows, k, L, G, par, cached=args.cached)
-        if ev:
-            ev[1].record(stream)
-        ctx.recover(rows, par, miss, k, L, G, out, cached=args.cached)
-        if ev:
-            ev[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-
-    verified = None
-    if not args.no_verify:
-        # round trip on every group + parity XOR rows == 0 (device, untimed)
-        r3 = rows.view(G, k, L)
-        ok = torch.equal(r3[torch.arange(G, device=dev), miss.long()], out.view(G, L))
-        acc = par.view(G, L).clone()
-        for i in range(k):
-            acc ^= r3[:, i]
-        ok = ok and not bool(acc.any())
-        del acc
-        verified = bool(ok)  # bit-exact vs the oracle is tests/test_hip_fixed.py's job
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(events[s])
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-    enc_ms = np.array([e[0].elapsed_time(e[1]) for e in events])
-    rec_ms = np.array([e[1].elapsed_time(e[2]) for e in events])
-    ctx.sync()
-
-    total_bytes = world * args.steps * (bytes_enc + bytes_rec)
-    value = total_bytes / 2**30 / elapsed
-    enc_avg_s = float(enc_ms.mean()) / 1e3
-    rec_avg_s = float(rec_ms.mean()) / 1e3
-    enc_gbs = bytes_enc / enc_avg_s / 1e9
-    rec_gbs = bytes_rec / rec_avg_s / 1e9
-
-    extra = {}
     if not args.profile_only and rank == 0 and world == 1:
-        del rows
-        torch.cuda.empty_cache()
+        work.release()
+        ctx, stream = work.ctx, work.stream
         if not args.no_ragged:
-            extra["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
+            line["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
         if not args.no_e2e:
-            extra["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
+            line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
         if not args.no_cpu_baseline:
-            extra["cpu_baseline"] = cpu_baseline(k, L, args.cpu_seconds)
-
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            tj = json.load(f)
-        if tj.get("groups") == G and tj.get("k") == k and tj.get("L") == L:
-            traffic = tj.get("encode_hbm_bytes_per_launch")
-
+            line["cpu_baseline"] = cpu_baseline(k, L, args.cpu_seconds)
+    line.setdefault("cpu_baseline", None)
     if rank == 0:
-        line = {
-            "metric": "FEC XOR encode+recover GiB/s (device-resident) on batched 1350B packet groups",
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (counter-based splitmix64 bytes generated in HBM)",
-            "config": {
-                "workload": f"{G} groups x {k} x {L} B per GPU: parity encode + single-loss "
-                            f"recover (BASELINE configs[1]+[2])",
-                "groups_per_gpu": G, "k": k, "L": L,
-                "parallelism": f"group-shard x{world} (no collective)",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "fixed_xor_kernel<10,encode>",
-                "achieved": round(enc_gbs, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_enc,
-                "avg_launch_us": round(enc_avg_s * 1e6, 2),
-            },
-            "encode_GiBps": round(bytes_enc / enc_avg_s / 2**30, 2),
-            "recover_GiBps": round(bytes_rec / rec_avg_s / 2**30, 2),
-            "recover_roofline_frac": round(rec_gbs / HBM_PEAK_GBS, 4),
-            "verified": verified,
-        }
-        line.update(extra)
-        if "cpu_baseline" not in line:
-            line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    ctx.close()
+    work.ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

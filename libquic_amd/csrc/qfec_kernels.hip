@@ -64,28 +64,46 @@ __device__ __forceinline__ void st16t(uint8_t* p, u32x4 v) {
   }
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+// Wave max of 11-bit values by ballots, MSB first (no LDS round trips).
+__device__ __forceinline__ uint32_t wave_max11(uint32_t v) {
+  uint32_t mx = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  for (int b = 10; b >= 0; --b) {
+    const uint32_t cand = mx | (1u << b);
+    if (__ballot(v >= cand) != 0ull) mx = cand;
+  }
+  return mx;
 }
 
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
-  return v;
-}
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
 // ---------------------------------------------------------------------------
 // Fixed shape, L >= 16.
 // ---------------------------------------------------------------------------
-template <int KC, bool RECOVER, bool NT>
+// SM (recover, gpb <= 8): lost-slot indices by scalar loads, see below.
+template <int KC, bool RECOVER, bool NT, bool SM>
 __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t C,
                                                            uint32_t gpb) {
   const uint32_t tid = threadIdx.x;
   const uint32_t gl = tid / C;  // group within the workgroup
   const uint32_t t = tid - gl * C;
-  const uint64_t g = (uint64_t)blockIdx.x * gpb + gl;
+  const uint64_t gb = (uint64_t)blockIdx.x * gpb;
+  const uint64_t g = gb + gl;
+  uint64_t mw0 = 0, mw1 = 0;
+  if constexpr (RECOVER) {
+    // SM: the block's lost-slot indices by (at most) two SCALAR loads of the
+    // aligned 8-byte words covering missing[gb .. gb+gpb) (gpb <= 8): every
+    // row address below depends on m, and a per-lane byte load here would
+    // put a vector-memory round trip in front of all of them (-7% measured).
+    // An aligned word holding a valid byte never crosses a page: no fault.
+    if constexpr (SM) {
+      const uint8_t* mp = a.missing + gb;
+      const uint32_t mis = (uint32_t)((uintptr_t)mp & 7u);  // pointer math keeps addrspace(1)
+      const uint64_t* wp = reinterpret_cast<const uint64_t*>(mp - mis);
+      mw0 = wp[0];
+      if (gb + 8u - mis < a.n_groups) mw1 = wp[1];
+    }
+  }
   if (gl >= gpb || g >= a.n_groups) return;
   const uint32_t off = min(t * 16u, a.L - 16u);
   const uint8_t* src = a.rows + g * a.group_stride + off;
@@ -93,7 +111,13 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
 
   u32x4 acc = {0u, 0u, 0u, 0u};
   if constexpr (RECOVER) {
-    const uint32_t m = a.missing[g];
+    uint32_t m;
+    if constexpr (SM) {
+      const uint32_t sh = gl + (uint32_t)((uintptr_t)(a.missing + gb) & 7u);
+      m = (uint32_t)((sh < 8u ? mw0 >> (8u * sh) : mw1 >> (8u * (sh - 8u))) & 0xFFu);
+    } else {
+      m = a.missing[g];
+    }
     if (m >= k) {
       if (t == 0) atomicOr(a.err, kErrMissingIndex);
       return;
@@ -169,18 +193,24 @@ __global__ __launch_bounds__(kBlock) void fixed_small_kernel(FixedArgs a) {
 // Ragged CSR: one wave per group.
 // ---------------------------------------------------------------------------
 // Right shift of a 16-byte vector by sh bytes (0..15), zero fill, branch-free:
-// a word select by sh/4, then v_alignbyte_b32 by sh%4.
+// one 64-bit select for the 8-byte step, then 64-bit funnel shifts
+// ((hi << 1) << (63 - s) is the UB-free hi << (64 - s), 0 at s = 0).
+// Written without multi-way selects: the compiler turns those into divergent
+// branches, each of which waits for the load (vmcnt(0)) and serialises rows.
 __device__ __forceinline__ u32x4 shr_bytes_bf(u32x4 v, uint32_t sh) {
-  const uint32_t q = sh >> 2, r = sh & 3u;
-  const uint32_t s0 = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
-  const uint32_t s1 = q == 0 ? v.y : q == 1 ? v.z : q == 2 ? v.w : 0u;
-  const uint32_t s2 = q == 0 ? v.z : q == 1 ? v.w : 0u;
-  const uint32_t s3 = q == 0 ? v.w : 0u;
+  uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  const bool big = sh >= 8u;
+  lo = big ? hi : lo;
+  hi = big ? 0ull : hi;
+  const uint32_t s = (sh & 7u) * 8u;
+  lo = (lo >> s) | ((hi << 1) << (63u - s));
+  hi = hi >> s;
   u32x4 o;
-  o.x = __builtin_amdgcn_alignbyte(s1, s0, r);
-  o.y = __builtin_amdgcn_alignbyte(s2, s1, r);
-  o.z = __builtin_amdgcn_alignbyte(s3, s2, r);
-  o.w = __builtin_amdgcn_alignbyte(0u, s3, r);
+  o.x = (uint32_t)lo;
+  o.y = (uint32_t)(lo >> 32);
+  o.z = (uint32_t)hi;
+  o.w = (uint32_t)(hi >> 32);
   return o;
 }
 
@@ -191,10 +221,11 @@ __device__ __forceinline__ u32x4 shr_bytes_bf(u32x4 v, uint32_t sh) {
 template <bool NT>
 __device__ __forceinline__ u32x4 window16(const uint8_t* row, uint32_t len, uint32_t win) {
   const bool full = win + 16u <= len;
-  u32x4 v = ld16t<NT>(row + (full ? win : len - 16u));
-  const u32x4 z = {0u, 0u, 0u, 0u};
-  v = win < len ? v : z;
-  return full ? v : shr_bytes_bf(v, min(win + 16u - len, 15u));
+  const u32x4 v = ld16t<NT>(row + (full ? win : len - 16u));
+  // sh = 0 for a full window (shift is then the identity); all-zero mask past the end.
+  const uint32_t sh = full ? 0u : min(win + 16u - len, 15u);
+  const uint32_t keep = win < len ? 0xFFFFFFFFu : 0u;
+  return shr_bytes_bf(v, sh) & keep;
 }
 
 // Same for len < 16 (wave-uniform branch per packet; rare).
@@ -207,10 +238,54 @@ __device__ __forceinline__ u32x4 window16_small(const uint8_t* row, uint32_t len
   return v;
 }
 
-// Lane l of the wave owns parity windows at 16*l and 16*l + 1024 (plen <= 1452
-// needs at most two), clamped so the last window ends at parity_len.  The
-// group's packet lengths/offsets are loaded once, one packet per lane, and
-// broadcast per row with v_readlane (no per-row scalar-load latency).
+// XOR rows [0, cnt) of one 64-packet metadata chunk into the lane's windows,
+// 8 rows per batch with every load of the batch in flight before the first
+// XOR (the loop used to wait on each row's load in turn).  Every packet of
+// the group is >= 16 bytes on this path.  Row j's length and offset come from
+// lane j's registers via v_readlane (wave-uniform scalars).
+// XOR rows [0, cnt) of one 64-packet metadata chunk into the lane's two
+// windows.  Rows go in batches of B with every load of the batch issued before
+// the first XOR; a lane loads only where its window overlaps the packet
+// (exec-masked), so lanes past the packet end and the second window of short
+// packets issue no memory requests at all.  Every packet is >= 16 B here.
+template <bool NT, int B>
+__device__ __forceinline__ void ragged_rows(const uint8_t* bytes, uint32_t lenr, uint32_t offlo,
+                                            uint32_t offhi, uint32_t cnt, uint32_t win0,
+                                            uint32_t win1, u32x4& acc0, u32x4& acc1) {
+  for (uint32_t i = 0; i < cnt; i += B) {
+    u32x4 r0[B], r1[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      r0[u] = u32x4{0u, 0u, 0u, 0u};
+      r1[u] = u32x4{0u, 0u, 0u, 0u};
+      if (i + u < cnt) {  // wave-uniform
+        const uint32_t j = i + u;
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)j);
+        const uint64_t off =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)j) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)j);
+        const uint8_t* row = bytes + off;
+        if (win0 < len) r0[u] = ld16t<NT>(row + (win0 + 16u <= len ? win0 : len - 16u));
+        if (win1 < len) r1[u] = ld16t<NT>(row + (win1 + 16u <= len ? win1 : len - 16u));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of their first use
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const uint32_t j = min(i + u, cnt - 1u);
+      const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)j);
+      acc0 ^= shr_bytes_bf(r0[u], win0 + 16u <= len ? 0u : min(win0 + 16u - len, 15u));
+      acc1 ^= shr_bytes_bf(r1[u], win1 + 16u <= len ? 0u : min(win1 + 16u - len, 15u));
+    }
+  }
+}
+
+// One wave per group.  Lane l owns parity windows at 16*l and 16*l + 1024
+// (parity_len <= 1452 needs at most two), clamped so the last window ends at
+// parity_len.  The group's RECEIVED packets are numbered r = 0..kr-1 (recover
+// skips the lost index m: packet p = r + (r >= m)), so the lost packet's
+// entries are never read and the row loop has no holes.  Packet metadata is
+// loaded once, one packet per lane, and broadcast with v_readlane.
 template <bool RECOVER, bool NT>
 __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -224,11 +299,10 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
     if (lane == 0) atomicOr(a.err, kErrGroupSize);
     return;
   }
-  uint32_t plen;
-  uint32_t m = 0xFFFFFFFFu;
+  uint32_t m = 0xFFFFFFFFu, plen = 0;
   if constexpr (RECOVER) {
-    plen = a.parity_len[g];
     m = a.missing[g];
+    plen = a.parity_len[g];
     if (m >= k) {
       if (lane == 0) atomicOr(a.err, kErrMissingIndex);
       return;
@@ -237,85 +311,92 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
       if (lane == 0) atomicOr(a.err, kErrParityLength);
       return;
     }
-    uint32_t bad = 0;
-    for (uint32_t i = lane; i < k; i += 64u) {
-      if (i == m) continue;  // the lost packet's entries are never read
-      const uint32_t l = a.pkt_len[p0 + i];
-      bad |= (l == 0u || l > plen) ? 1u : 0u;
-    }
-    if (wave_or(bad)) {
-      if (lane == 0) atomicOr(a.err, kErrPacketLength);
-      return;
-    }
-  } else {
-    uint32_t mx = 0, bad = 0;
-    for (uint32_t i = lane; i < k; i += 64u) {
-      const uint32_t l = a.pkt_len[p0 + i];
-      mx = max(mx, l);
-      bad |= (l == 0u || l > kMaxPacket) ? 1u : 0u;
-    }
-    mx = wave_max(mx);
-    if (wave_or(bad)) {
-      if (lane == 0) atomicOr(a.err, kErrPacketLength);
-      return;
-    }
-    plen = mx;
   }
+  const uint32_t kr = RECOVER ? k - 1u : k;  // received packets
+  // metadata of received packets 0..63 (every group of <= 64 packets)
+  uint32_t lenr = 0, offlo = 0, offhi = 0;
+  if (lane < kr) {
+    const uint32_t p = p0 + lane + (lane >= m ? 1u : 0u);
+    lenr = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    offlo = (uint32_t)o;
+    offhi = (uint32_t)(o >> 32);
+  }
+  // validation + parity length (+ whether any packet is shorter than 16 B)
+  uint32_t mx = lenr, bad = 0, small = 0;
+  if (lane < kr) {
+    bad = (lenr == 0u || lenr > (RECOVER ? plen : kMaxPacket)) ? 1u : 0u;
+    small = lenr < 16u ? 1u : 0u;
+  }
+  for (uint32_t r = 64u + lane; r < kr; r += 64u) {
+    const uint32_t l = a.pkt_len[p0 + r + (r >= m ? 1u : 0u)];
+    mx = max(mx, l);
+    bad |= (l == 0u || l > (RECOVER ? plen : kMaxPacket)) ? 1u : 0u;
+    small |= l < 16u ? 1u : 0u;
+  }
+  if (wave_any(bad != 0u)) {
+    if (lane == 0) atomicOr(a.err, kErrPacketLength);
+    return;
+  }
+  if constexpr (!RECOVER) {
+    plen = wave_max11(min(mx, 2047u));
+    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
+  }
+  const bool any_small = wave_any(small != 0u);
   const uint8_t* par = RECOVER ? a.parity + a.parity_off[g] : nullptr;
   uint8_t* dst = a.out + (RECOVER ? a.out_off[g] : a.parity_off[g]);
+  const uint32_t w = lane * 16u;
 
-  if (plen >= 16u) {
-    const uint32_t w = lane * 16u;
-    const uint32_t win0 = min(w, plen - 16u);
-    const uint32_t win1 = min(w + 1024u, plen - 16u);
-    const bool two = plen > 1024u;  // wave-uniform
-    const uint32_t lo1 = min(1024u, plen - 16u);  // lowest byte any second window covers
+  if (plen >= 16u && !any_small) {
+    // windows past parity_len are parked at 0xFFFF (no packet reaches them)
+    const uint32_t win0 = w < plen ? min(w, plen - 16u) : 0xFFFFu;
+    const uint32_t win1 = w + 1024u < plen ? min(w + 1024u, plen - 16u) : 0xFFFFu;
     u32x4 acc0 = {0u, 0u, 0u, 0u}, acc1 = {0u, 0u, 0u, 0u};
     if constexpr (RECOVER) {
-      acc0 = ld16t<NT>(par + win0);
-      if (two) acc1 = ld16t<NT>(par + win1);
+      if (win0 < plen) acc0 = ld16t<NT>(par + win0);
+      if (win1 < plen) acc1 = ld16t<NT>(par + win1);
     }
-    for (uint32_t c = 0; c < k; c += 64u) {
-      const uint32_t cnt = min(64u, k - c);
-      uint32_t lenr = 0, offlo = 0, offhi = 0;
-      if (lane < cnt && c + lane != m) {
-        lenr = a.pkt_len[p0 + c + lane];
-        const uint64_t o = a.pkt_off[p0 + c + lane];
-        offlo = (uint32_t)o;
-        offhi = (uint32_t)(o >> 32);
-      }
-#pragma unroll 2
-      for (uint32_t i = 0; i < cnt; ++i) {
-        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)i);
-        if (len == 0u) continue;  // the lost packet (wave-uniform)
-        const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)i)
-                              << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)i);
-        const uint8_t* row = a.bytes + off;
-        if (len >= 16u) {
-          acc0 ^= window16<NT>(row, len, win0);
-          if (two && len > lo1) acc1 ^= window16<NT>(row, len, win1);
-        } else {
-          acc0 ^= window16_small(row, len, win0);
+    for (uint32_t c = 0; c < kr; c += 64u) {
+      if (c > 0) {  // groups of more than 64 packets: next metadata chunk
+        lenr = offlo = offhi = 0;
+        const uint32_t r = c + lane;
+        if (r < kr) {
+          const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
+          lenr = a.pkt_len[p];
+          const uint64_t o = a.pkt_off[p];
+          offlo = (uint32_t)o;
+          offhi = (uint32_t)(o >> 32);
         }
       }
+      ragged_rows<NT, 4>(a.bytes, lenr, offlo, offhi, min(64u, kr - c), win0, win1, acc0, acc1);
     }
-    if (w < plen) st16t<NT>(dst + win0, acc0);
-    if (two && w + 1024u < plen) st16t<NT>(dst + win1, acc1);
+    if (win0 < plen) st16t<NT>(dst + win0, acc0);
+    if (win1 < plen) st16t<NT>(dst + win1, acc1);
+  } else if (plen >= 16u) {
+    // Some packet is shorter than 16 bytes (rare): per-row generic windows.
+    for (uint32_t w0 = 0; w0 < plen; w0 += 1024u) {
+      const uint32_t win = min(w + w0, plen - 16u);
+      u32x4 acc = {0u, 0u, 0u, 0u};
+      if constexpr (RECOVER) acc = ld16(par + win);
+      for (uint32_t r = 0; r < kr; ++r) {
+        const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
+        const uint32_t len = a.pkt_len[p];
+        const uint8_t* row = a.bytes + a.pkt_off[p];
+        acc ^= (len >= 16u) ? window16<false>(row, len, win) : window16_small(row, len, win);
+      }
+      if (w + w0 < plen) st16(dst + win, acc);
+    }
   } else {
     // Whole group fits in one window: one lane per byte.
     if (lane < plen) {
       uint8_t acc = RECOVER ? par[lane] : (uint8_t)0;
-      for (uint32_t i = 0; i < k; ++i) {
-        if (i == m) continue;
-        const uint32_t len = a.pkt_len[p0 + i];
-        if (lane < len) acc ^= a.bytes[a.pkt_off[p0 + i] + lane];
+      for (uint32_t r = 0; r < kr; ++r) {
+        const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
+        const uint32_t len = a.pkt_len[p];
+        if (lane < len) acc ^= a.bytes[a.pkt_off[p] + lane];
       }
       dst[lane] = acc;
     }
-  }
-  if constexpr (!RECOVER) {
-    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
   }
 }
 
@@ -387,13 +468,13 @@ __global__ __launch_bounds__(kBlock) void synth_ragged_kernel(uint8_t* bytes,
   }
 }
 
-template <bool RECOVER, bool NT>
+template <bool RECOVER, bool NT, bool SM>
 hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t blocks,
                           hipStream_t s) {
   switch (a.k) {
 #define QFEC_K_CASE(KV)                                                                     \
   case KV:                                                                                   \
-    hipLaunchKernelGGL((fixed_xor_kernel<KV, RECOVER, NT>), dim3((uint32_t)blocks),          \
+    hipLaunchKernelGGL((fixed_xor_kernel<KV, RECOVER, NT, SM>), dim3((uint32_t)blocks),      \
                        dim3(kBlock), 0, s, a, C, gpb);                                       \
     break;
     QFEC_K_CASE(2)
@@ -404,7 +485,7 @@ hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t
     QFEC_K_CASE(16)
 #undef QFEC_K_CASE
     default:
-      hipLaunchKernelGGL((fixed_xor_kernel<0, RECOVER, NT>), dim3((uint32_t)blocks),
+      hipLaunchKernelGGL((fixed_xor_kernel<0, RECOVER, NT, SM>), dim3((uint32_t)blocks),
                          dim3(kBlock), 0, s, a, C, gpb);
   }
   return hipGetLastError();
@@ -451,12 +532,15 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
     a.out = a0.out + g * a0.out_stride;
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
     hipError_t e;
-    if (recover)
-      e = nontemporal ? launch_fixed_k<true, true>(a, C, gpb, blocks, s)
-                      : launch_fixed_k<true, false>(a, C, gpb, blocks, s);
+    if (recover && gpb <= 8u)
+      e = nontemporal ? launch_fixed_k<true, true, true>(a, C, gpb, blocks, s)
+                      : launch_fixed_k<true, false, true>(a, C, gpb, blocks, s);
+    else if (recover)
+      e = nontemporal ? launch_fixed_k<true, true, false>(a, C, gpb, blocks, s)
+                      : launch_fixed_k<true, false, false>(a, C, gpb, blocks, s);
     else
-      e = nontemporal ? launch_fixed_k<false, true>(a, C, gpb, blocks, s)
-                      : launch_fixed_k<false, false>(a, C, gpb, blocks, s);
+      e = nontemporal ? launch_fixed_k<false, true, false>(a, C, gpb, blocks, s)
+                      : launch_fixed_k<false, false, false>(a, C, gpb, blocks, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -464,7 +548,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
 
 hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
   if (a0.n_groups == 0) return hipSuccess;
-  const uint64_t gpb = kBlock / 64;
+  const uint64_t gpb = kBlock / 64;  // one wave per group
   const uint64_t maxg = 0x7FFFFFFFull * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     RaggedArgs a = a0;

@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -19,10 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kind(name):
-    if "fixed_xor_kernel" in name:
-        return "recover" if ", true," in name or "<10, true" in name else "encode"
-    if "ragged_xor_kernel" in name:
-        return "ragged_recover" if "<true" in name else "ragged_encode"
+    """fixed_xor_kernel<K, RECOVER, NT, SM> / ragged_xor_kernel<RECOVER, NT>."""
+    m = re.search(r"fixed_xor_kernel<(-?\d+), (true|false)", name)
+    if m:
+        return "recover" if m.group(2) == "true" else "encode"
+    m = re.search(r"ragged_xor_kernel<(true|false)", name)
+    if m:
+        return "ragged_recover" if m.group(1) == "true" else "ragged_encode"
     return None
 
 

@@ -454,6 +454,54 @@ __global__ __launch_bounds__(256) void v_outlayout(const uint8_t* rows, uint8_t*
     stnt(out + (uint64_t)blockIdx.x * 4096u + gl * 1350u + off, acc);
 }
 
+// Recover variants.  R_all: load every row AND the parity (k+1 loads, no
+// address depends on missing[g]), drop row m with a select after the fact.
+__global__ __launch_bounds__(256) void r_all(const uint8_t* rows, const uint8_t* par,
+                                             const uint8_t* miss, uint8_t* out, uint64_t n,
+                                             uint32_t C, uint32_t gpb) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t gl = tid / C;
+  const uint32_t t = tid - gl * C;
+  const uint64_t g = (uint64_t)blockIdx.x * gpb + gl;
+  if (gl >= gpb || g >= n) return;
+  const uint32_t off = min(t * 16u, 1350u - 16u);
+  const uint8_t* src = rows + g * 13500u + off;
+  u32x4 v[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) v[i] = ldnt(src + i * 1350);
+  u32x4 acc = ldnt(par + g * 1350u + off);
+  const uint32_t m = miss[g];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) acc ^= (i == (int)m) ? u32x4{0, 0, 0, 0} : v[i];
+  stnt(out + g * 1350u + off, acc);
+}
+
+// R_blockm: the block's missing indices arrive by one scalar 8-byte load of
+// the aligned word that covers them (uniform), so no per-lane dependent load.
+__global__ __launch_bounds__(256) void r_blockm(const uint8_t* rows, const uint8_t* par,
+                                                const uint8_t* miss, uint8_t* out, uint64_t n,
+                                                uint32_t C, uint32_t gpb) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t gl = tid / C;
+  const uint32_t t = tid - gl * C;
+  const uint64_t gb = (uint64_t)blockIdx.x * gpb;
+  const uint64_t g = gb + gl;
+  // 16 bytes starting at the 8-aligned word below gb cover gb..gb+gpb-1 (gpb <= 8)
+  const uint64_t a8 = gb & ~7ull;
+  const uint64_t* mw = reinterpret_cast<const uint64_t*>(miss + a8);
+  const uint64_t w0 = __builtin_nontemporal_load(mw), w1 = (a8 + 8 < n) ? mw[1] : 0ull;
+  if (gl >= gpb || g >= n) return;
+  const uint32_t sh = (uint32_t)(g - a8);
+  const uint32_t m = (uint32_t)(((sh < 8) ? (w0 >> (8 * sh)) : (w1 >> (8 * (sh - 8)))) & 0xFF);
+  const uint32_t off = min(t * 16u, 1350u - 16u);
+  const uint8_t* src = rows + g * 13500u + off;
+  const uint8_t* pp = par + g * 1350u + off;
+  u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) acc ^= ldnt(i == (int)m ? pp : src + i * 1350);
+  stnt(out + g * 1350u + off, acc);
+}
+
 __global__ void fill(uint8_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n / 8;
        i += (uint64_t)gridDim.x * 256) {
@@ -512,7 +560,15 @@ int main(int argc, char** argv) {
   vs.push_back({"product encode", alg, [&] { prod(false, false, L); }});
   vs.push_back({"product encode NT", alg, [&] { prod(true, false, L); }});
   vs.push_back({"product recover", alg, [&] { prod(false, true, L); }});
-  vs.push_back({"product encode stride1360 (aligned rows)", alg, [&] { prod(false, false, 1360); }});
+  vs.push_back({"product recover NT", alg, [&] { prod(true, true, L); }});
+  vs.push_back({"r_all (k+1 loads, no addr dependency)", alg, [&] {
+                  hipLaunchKernelGGL(tune::r_all, dim3(blocks), dim3(256), 0, 0, rows, par, miss,
+                                     out, G, C, gpb);
+                }});
+  vs.push_back({"r_blockm (scalar missing word)", alg, [&] {
+                  hipLaunchKernelGGL(tune::r_blockm, dim3(blocks), dim3(256), 0, 0, rows, par,
+                                     miss, out, G, C, gpb);
+                }});
   vs.push_back({"v_block<512>", alg, [&] {
                   hipLaunchKernelGGL((tune::v_block<512, false, false>), dim3((G + 5) / 6),
                                      dim3(512), 0, 0, rows, out, G, C, 6u);
@@ -606,6 +662,14 @@ int main(int argc, char** argv) {
   vs.push_back({"v_out parity stride 1350 (=product NT)", alg, [&] {
                   hipLaunchKernelGGL((tune::v_outlayout<0, 1350>), dim3(blocks), dim3(256), 0, 0,
                                      rows, rows_pad, G, C, gpb);
+                }});
+  vs.push_back({"v_out parity stride 1350 -> out buffer", alg, [&] {
+                  hipLaunchKernelGGL((tune::v_outlayout<0, 1350>), dim3(blocks), dim3(256), 0, 0,
+                                     rows, out, G, C, gpb);
+                }});
+  vs.push_back({"v_block<256> NT load+store -> rows_pad", alg, [&] {
+                  hipLaunchKernelGGL((tune::v_block<256, true, true>), dim3(blocks), dim3(256), 0,
+                                     0, rows, rows_pad, G, C, gpb);
                 }});
   vs.push_back({"v_nostore (reads only, alg bytes=read)", (double)rows_b, [&] {
                   hipLaunchKernelGGL(tune::v_nostore, dim3(blocks), dim3(256), 0, 0, rows, out, G,
