@@ -238,60 +238,99 @@ __device__ __forceinline__ u32x4 window16_small(const uint8_t* row, uint32_t len
   return v;
 }
 
-// XOR rows [0, cnt) of one 64-packet metadata chunk into the lane's windows,
-// 8 rows per batch with every load of the batch in flight before the first
-// XOR (the loop used to wait on each row's load in turn).  Every packet of
-// the group is >= 16 bytes on this path.  Row j's length and offset come from
-// lane j's registers via v_readlane (wave-uniform scalars).
-// XOR rows [0, cnt) of one 64-packet metadata chunk into the lane's two
-// windows.  Rows go in batches of B with every load of the batch issued before
-// the first XOR; a lane loads only where its window overlaps the packet
-// (exec-masked), so lanes past the packet end and the second window of short
-// packets issue no memory requests at all.  Every packet is >= 16 B here.
-template <bool NT, int B>
-__device__ __forceinline__ void ragged_rows(const uint8_t* bytes, uint32_t lenr, uint32_t offlo,
-                                            uint32_t offhi, uint32_t cnt, uint32_t win0,
-                                            uint32_t win1, u32x4& acc0, u32x4& acc1) {
-  for (uint32_t i = 0; i < cnt; i += B) {
-    u32x4 r0[B], r1[B];
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-      r0[u] = u32x4{0u, 0u, 0u, 0u};
-      r1[u] = u32x4{0u, 0u, 0u, 0u};
-      if (i + u < cnt) {  // wave-uniform
-        const uint32_t j = i + u;
-        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)j);
-        const uint64_t off =
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)j) << 32) |
-            (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)j);
-        const uint8_t* row = bytes + off;
-        if (win0 < len) r0[u] = ld16t<NT>(row + (win0 + 16u <= len ? win0 : len - 16u));
-        if (win1 < len) r1[u] = ld16t<NT>(row + (win1 + 16u <= len ? win1 : len - 16u));
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of their first use
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-      const uint32_t j = min(i + u, cnt - 1u);
-      const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)lenr, (int)j);
-      acc0 ^= shr_bytes_bf(r0[u], win0 + 16u <= len ? 0u : min(win0 + 16u - len, 15u));
-      acc1 ^= shr_bytes_bf(r1[u], win1 + 16u <= len ? 0u : min(win1 + 16u - len, 15u));
-    }
-  }
+// Flat-window ragged kernel: one wave per group.
+//
+// A group's received packets are cut into 16-byte windows (packet i has
+// n_i = ceil(len_i/16); window t covers bytes [16t, 16t+16), the last one
+// loaded as the 16 bytes ending at the packet end and shifted down, zero
+// filled).  The windows of all packets are numbered consecutively
+// (flat index f; packet i owns [S_i, S_i + n_i)) and lane l takes
+// f = l, l+64, l+128, ...: every lane of every wave-instruction loads, and
+// consecutive lanes read consecutive bytes — across packet boundaries too in a
+// packed CSR batch.  Each loaded window is XORed into the group's parity
+// accumulator in LDS at byte 16t (ds_xor_b64; two packets' windows can meet
+// at the same t inside one instruction, hence the atomic).  The lane's packet
+// comes from a bitmask of packet starts (bit S_i set): with M the mask word of
+// the wave's 64 windows, packet = starts before + inclusive popcount(M) - 1
+// (v_mbcnt), then its offset/length/S from an LDS table.
+//
+// LDS per wave: accumulator 92 x 16 B, start mask 92 x 8 B, packet table
+// 64 x 16 B (3.2 KiB).  Groups of more than 64 received packets run in chunks
+// of 64 with the same accumulator.
+constexpr int kFlatWaves = kBlock / 64;
+constexpr int kParWin = 92;  // ceil(1452/16) = 91 windows (+1 spare)
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-// One wave per group.  Lane l owns parity windows at 16*l and 16*l + 1024
-// (parity_len <= 1452 needs at most two), clamped so the last window ends at
-// parity_len.  The group's RECEIVED packets are numbered r = 0..kr-1 (recover
-// skips the lost index m: packet p = r + (r >= m)), so the lost packet's
-// entries are never read and the row loop has no holes.  Packet metadata is
-// loaded once, one packet per lane, and broadcast with v_readlane.
-template <bool RECOVER, bool NT>
-__global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) +
-                     (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  return x;
+}
+
+// The accumulator is only ever accessed as uint32_t (plain and atomic): one
+// type, so the compiler cannot reorder the plain initialisation / final reads
+// across the atomic XORs on type-based alias grounds.  The XOR is four
+// ds_xor_b32 per window by default: a 2 x ds_xor_b64 build (X64) produced
+// wrong accumulators in ~1% of recover groups for one unroll depth (U = 4;
+// U = 1, 2, 8 and every b32 build exact) — tools/debug/ragged_variants.hip.
+template <bool X64>
+__device__ __forceinline__ void lds_xor16(uint32_t* acc, uint32_t t, u32x4 v) {
+  if constexpr (X64) {
+    uint64_t* p = reinterpret_cast<uint64_t*>(acc + 4u * t);
+    __hip_atomic_fetch_xor(p, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(p + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+  } else {
+    uint32_t* p = acc + 4u * t;
+    __hip_atomic_fetch_xor(p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(p + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(p + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+}
+__device__ __forceinline__ void lds_put16(uint32_t* acc, uint32_t t, u32x4 v) {
+  acc[4u * t] = v.x;
+  acc[4u * t + 1u] = v.y;
+  acc[4u * t + 2u] = v.z;
+  acc[4u * t + 3u] = v.w;
+}
+__device__ __forceinline__ u32x4 lds_get16(const uint32_t* acc, uint32_t t) {
+  return u32x4{acc[4u * t], acc[4u * t + 1u], acc[4u * t + 2u], acc[4u * t + 3u]};
+}
+
+// Bytes [16t, 16t+16) of a zero-padded packet (any len >= 1, 16t < len).
+template <bool NT>
+__device__ __forceinline__ u32x4 packet_window(const uint8_t* row, uint32_t len, uint32_t t) {
+  const uint32_t win = 16u * t;
+  if (len >= 16u) {
+    const bool full = win + 16u <= len;
+    const u32x4 v = ld16t<NT>(row + (full ? win : len - 16u));
+    return shr_bytes_bf(v, full ? 0u : win + 16u - len);
+  }
+  return window16_small(row, len, 0u);  // t == 0 (rare: packets below 16 B)
+}
+
+template <bool RECOVER, bool NT, int U = 4, int WAVES = kFlatWaves, bool X64 = false>
+__global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[WAVES][4 * kParWin];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
   if (g >= a.n_groups) return;
+  uint32_t* par = s_par[wv];
+  uint64_t* head = s_head[wv];
+  u32x4* meta = s_meta[wv];
+
   const uint32_t p0 = a.grp_ptr[g];
   const uint32_t p1 = a.grp_ptr[g + 1];
   const uint32_t k = p1 - p0;
@@ -300,6 +339,7 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
     return;
   }
   uint32_t m = 0xFFFFFFFFu, plen = 0;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
   if constexpr (RECOVER) {
     m = a.missing[g];
     plen = a.parity_len[g];
@@ -311,92 +351,126 @@ __global__ __launch_bounds__(kBlock) void ragged_xor_kernel(RaggedArgs a) {
       if (lane == 0) atomicOr(a.err, kErrParityLength);
       return;
     }
+    // accumulator := the parity row (zero past plen)
+    const uint8_t* prow = a.parity + a.parity_off[g];
+    for (uint32_t t = lane; t < kParWin; t += 64u)
+      lds_put16(par, t, 16u * t < plen ? packet_window<NT>(prow, plen, t) : zero);
+  } else {
+    for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16(par, t, zero);
   }
   const uint32_t kr = RECOVER ? k - 1u : k;  // received packets
-  // metadata of received packets 0..63 (every group of <= 64 packets)
-  uint32_t lenr = 0, offlo = 0, offhi = 0;
-  if (lane < kr) {
-    const uint32_t p = p0 + lane + (lane >= m ? 1u : 0u);
-    lenr = a.pkt_len[p];
-    const uint64_t o = a.pkt_off[p];
-    offlo = (uint32_t)o;
-    offhi = (uint32_t)(o >> 32);
-  }
-  // validation + parity length (+ whether any packet is shorter than 16 B)
-  uint32_t mx = lenr, bad = 0, small = 0;
-  if (lane < kr) {
-    bad = (lenr == 0u || lenr > (RECOVER ? plen : kMaxPacket)) ? 1u : 0u;
-    small = lenr < 16u ? 1u : 0u;
-  }
-  for (uint32_t r = 64u + lane; r < kr; r += 64u) {
-    const uint32_t l = a.pkt_len[p0 + r + (r >= m ? 1u : 0u)];
-    mx = max(mx, l);
-    bad |= (l == 0u || l > (RECOVER ? plen : kMaxPacket)) ? 1u : 0u;
-    small |= l < 16u ? 1u : 0u;
-  }
-  if (wave_any(bad != 0u)) {
-    if (lane == 0) atomicOr(a.err, kErrPacketLength);
-    return;
-  }
-  if constexpr (!RECOVER) {
-    plen = wave_max11(min(mx, 2047u));
-    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
-  }
-  const bool any_small = wave_any(small != 0u);
-  const uint8_t* par = RECOVER ? a.parity + a.parity_off[g] : nullptr;
-  uint8_t* dst = a.out + (RECOVER ? a.out_off[g] : a.parity_off[g]);
-  const uint32_t w = lane * 16u;
-
-  if (plen >= 16u && !any_small) {
-    // windows past parity_len are parked at 0xFFFF (no packet reaches them)
-    const uint32_t win0 = w < plen ? min(w, plen - 16u) : 0xFFFFu;
-    const uint32_t win1 = w + 1024u < plen ? min(w + 1024u, plen - 16u) : 0xFFFFu;
-    u32x4 acc0 = {0u, 0u, 0u, 0u}, acc1 = {0u, 0u, 0u, 0u};
-    if constexpr (RECOVER) {
-      if (win0 < plen) acc0 = ld16t<NT>(par + win0);
-      if (win1 < plen) acc1 = ld16t<NT>(par + win1);
+  const uint32_t lim = RECOVER ? plen : kMaxPacket;
+  uint32_t mx = 0;
+  for (uint32_t c = 0; c < kr; c += 64u) {
+    // packet table of this chunk: lane j = received packet c + j
+    const uint32_t r = c + lane;
+    uint32_t len = 0, offlo = 0, offhi = 0;
+    if (r < kr) {
+      const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
+      len = a.pkt_len[p];
+      const uint64_t o = a.pkt_off[p];
+      offlo = (uint32_t)o;
+      offhi = (uint32_t)(o >> 32);
     }
-    for (uint32_t c = 0; c < kr; c += 64u) {
-      if (c > 0) {  // groups of more than 64 packets: next metadata chunk
-        lenr = offlo = offhi = 0;
-        const uint32_t r = c + lane;
-        if (r < kr) {
-          const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
-          lenr = a.pkt_len[p];
-          const uint64_t o = a.pkt_off[p];
-          offlo = (uint32_t)o;
-          offhi = (uint32_t)(o >> 32);
+    const bool bad = r < kr && (len == 0u || len > lim);
+    if (wave_any(bad)) {
+      if (lane == 0) atomicOr(a.err, kErrPacketLength);
+      return;
+    }
+    mx = max(mx, len);
+    const uint32_t n = (len + 15u) >> 4;
+    const uint32_t incl = wave_incl_scan(n, lane);
+    const uint32_t S = incl - n;
+    const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t nit = (W + 63u) >> 6;
+    for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
+    if (r < kr) {
+      meta[lane] = u32x4{offlo, offhi, len, S};
+      __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t last = min(kr - c, 64u) - 1u;
+    uint32_t before = 0;  // packet starts in earlier wave-iterations
+    if (!wave_any(r < kr && len < 16u)) {
+      // Every packet >= 16 B: every lane loads 16 in-packet bytes each
+      // iteration (lanes past W re-read their packet's last window and drop
+      // it), U iterations' loads in flight before the first XOR.
+      for (uint32_t it = 0; it < nit; it += U) {
+        // phase 1: the U start-mask words (independent LDS reads)
+        uint64_t M[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) M[u] = it + u < nit ? head[it + u] : 0ull;
+        // phase 2: packet of each window, its table entry
+        u32x4 md[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
+          before += (uint32_t)__popcll(M[u]);
+          md[u] = meta[pi];
+        }
+        // phase 3: U in-packet 16-B loads, all in flight
+        u32x4 v[U];
+        uint32_t tt[U], sh[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t f = 64u * (it + u) + lane;
+          const uint32_t win = 16u * (f - md[u].w);
+          const bool full = win + 16u <= md[u].z;
+          v[u] = ld16t<NT>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) +
+                           (full ? win : md[u].z - 16u));
+          sh[u] = full ? 0u : min(win + 16u - md[u].z, 15u);
+          tt[u] = f < W ? f - md[u].w : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (tt[u] != 0xFFFFFFFFu) lds_xor16<X64>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+      }
+    } else {
+      // Some packet below 16 B (rare): generic per-lane windows.
+      for (uint32_t it = 0; it < nit; ++it) {
+        const uint64_t M = head[it];
+        const uint32_t f = 64u * it + lane;
+        const uint32_t pi = min(before + (uint32_t)__popcll(M & below) - 1u, last);
+        before += (uint32_t)__popcll(M);
+        if (f < W) {
+          const u32x4 md = meta[pi];
+          const uint32_t t = f - md.w;
+          lds_xor16<X64>(par, t, packet_window<false>(a.bytes + (((uint64_t)md.y << 32) | md.x),
+                                                  md.z, t));
         }
       }
-      ragged_rows<NT, 4>(a.bytes, lenr, offlo, offhi, min(64u, kr - c), win0, win1, acc0, acc1);
     }
-    if (win0 < plen) st16t<NT>(dst + win0, acc0);
-    if (win1 < plen) st16t<NT>(dst + win1, acc1);
-  } else if (plen >= 16u) {
-    // Some packet is shorter than 16 bytes (rare): per-row generic windows.
-    for (uint32_t w0 = 0; w0 < plen; w0 += 1024u) {
-      const uint32_t win = min(w + w0, plen - 16u);
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      if constexpr (RECOVER) acc = ld16(par + win);
-      for (uint32_t r = 0; r < kr; ++r) {
-        const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
-        const uint32_t len = a.pkt_len[p];
-        const uint8_t* row = a.bytes + a.pkt_off[p];
-        acc ^= (len >= 16u) ? window16<false>(row, len, win) : window16_small(row, len, win);
+  }
+  if constexpr (!RECOVER) {
+    plen = wave_max11(mx);
+    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
+  }
+  uint8_t* dst = a.out + (RECOVER ? a.out_off[g] : a.parity_off[g]);
+  if (plen >= 16u) {
+    const uint32_t nw = (plen + 15u) >> 4;
+    for (uint32_t t = lane; t < nw; t += 64u) {
+      if (16u * t + 16u <= plen) {
+        st16t<NT>(dst + 16u * t, lds_get16(par, t));
+      } else {
+        // tail: the 16 bytes ending at plen, from windows t-1 and t
+        const uint32_t o = plen - 16u * t;  // 1..15
+        const u32x4 lo = lds_get16(par, t - 1u), hi = lds_get16(par, t);
+        const uint64_t a0 = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+        const uint64_t a1 = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+        const uint64_t a2 = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+        const uint64_t a3 = (uint64_t)hi.z | ((uint64_t)hi.w << 32);
+        // bytes [o, o+16) of a0 a1 a2 a3
+        const uint64_t w0 = o < 8u ? a0 : a1, w1 = o < 8u ? a1 : a2, w2 = o < 8u ? a2 : a3;
+        const uint32_t s = (o & 7u) * 8u;
+        const uint64_t r0 = (w0 >> s) | ((w1 << 1) << (63u - s));
+        const uint64_t r1 = (w1 >> s) | ((w2 << 1) << (63u - s));
+        st16t<NT>(dst + plen - 16u, u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1,
+                                          (uint32_t)(r1 >> 32)});
       }
-      if (w + w0 < plen) st16(dst + win, acc);
     }
-  } else {
-    // Whole group fits in one window: one lane per byte.
-    if (lane < plen) {
-      uint8_t acc = RECOVER ? par[lane] : (uint8_t)0;
-      for (uint32_t r = 0; r < kr; ++r) {
-        const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
-        const uint32_t len = a.pkt_len[p];
-        if (lane < len) acc ^= a.bytes[a.pkt_off[p] + lane];
-      }
-      dst[lane] = acc;
-    }
+  } else if (lane < plen) {
+    dst[lane] = (uint8_t)(par[lane >> 2] >> (8u * (lane & 3u)));
   }
 }
 

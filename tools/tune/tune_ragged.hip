@@ -1,11 +1,11 @@
 // tune_ragged.hip — A/B study of the ragged (CSR) FEC XOR kernels: the current
-// product kernel, the earlier one-wave-per-group kernel (old_ragged.inc, git
-// a21687b), cache policies, and packed vs padded packet layouts (BASELINE
-// configs[3] padding study).  One process, interleaved rounds.
+// product (flat-window, LDS accumulator) kernel, the previous two-windows-per-
+// lane kernel (prev_ragged.inc, git fbed0d3), cache policies, and packed vs
+// padded packet layouts (BASELINE configs[3] padding study).  One process, interleaved rounds.
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_ragged.hip -o tools/tune/build/tune_ragged
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
-#include "old_ragged.inc"
+#include "prev_ragged.inc"
 
 #include <algorithm>
 #include <cstring>
@@ -136,29 +136,41 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, false>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
                     }});
-      vs.push_back({"old (1 wave/group, nt) " + s.name, s.l.alg, [=] {
-                      hipLaunchKernelGGL((qfec::old_ragged_xor_kernel<false, true>),
+#define TV(NAME, U, W)                                                                      \
+  vs.push_back({NAME, s.l.alg, [=] {                                                        \
+                  hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, true, U, W>),            \
+                                     dim3((uint32_t)((G + W - 1) / W)), dim3(64 * W), 0, 0, a); \
+                }});
+      TV("flat U2 W4", 2, 4)
+      TV("flat U8 W4", 8, 4)
+      TV("flat U8 W8", 8, 8)
+      TV("flat U8 W2", 8, 2)
+      TV("flat U4 W1", 4, 1)
+      TV("flat U16 W4", 16, 4)
+#undef TV
+      vs.push_back({"prev (2 fixed windows/lane, nt) " + s.name, s.l.alg, [=] {
+                      hipLaunchKernelGGL((qfec::prev_ragged_xor_kernel<false, true>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
                     }});
-      vs.push_back({"old default-policy " + s.name, s.l.alg, [=] {
-                      hipLaunchKernelGGL((qfec::old_ragged_xor_kernel<false, false>),
+      vs.push_back({"prev default-policy " + s.name, s.l.alg, [=] {
+                      hipLaunchKernelGGL((qfec::prev_ragged_xor_kernel<false, false>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
                     }});
     }
   }
-  // correctness: product == old on the packed set
+  // correctness: product == prev on the packed set
   {
     auto a1 = args(sets[0], par);
     auto a2 = args(sets[0], par2);
     CK(hipMemset(par, 0, G * 1452));
     CK(hipMemset(par2, 0, G * 1452));
     CK(qfec::launch_ragged(a1, false, 0));
-    hipLaunchKernelGGL((qfec::old_ragged_xor_kernel<false, true>), dim3((uint32_t)((G + 3) / 4)),
+    hipLaunchKernelGGL((qfec::prev_ragged_xor_kernel<false, true>), dim3((uint32_t)((G + 3) / 4)),
                        dim3(256), 0, 0, a2);
     std::vector<uint8_t> h1(G * 1452), h2(G * 1452);
     CK(hipMemcpy(h1.data(), par, G * 1452, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h2.data(), par2, G * 1452, hipMemcpyDeviceToHost));
-    std::printf("product == old: %s\n", h1 == h2 ? "yes" : "NO");
+    std::printf("product == prev: %s\n", h1 == h2 ? "yes" : "NO");
     // host reference on a sample of groups
     const Layout& L0 = sets[0].l;
     std::vector<uint8_t> data(L0.bytes);
@@ -174,7 +186,7 @@ int main(int argc, char** argv) {
       badp += memcmp(ref, &h1[g * 1452], mx) != 0;
       bado += memcmp(ref, &h2[g * 1452], mx) != 0;
     }
-    std::printf("host check: product bad groups %d, old bad groups %d\n", badp, bado);
+    std::printf("host check: product bad groups %d, prev bad groups %d\n", badp, bado);
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
