@@ -276,34 +276,48 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 
 // The accumulator is only ever accessed as uint32_t (plain and atomic): one
 // type, so the compiler cannot reorder the plain initialisation / final reads
-// across the atomic XORs on type-based alias grounds.  The XOR is four
-// ds_xor_b32 per window by default: a 2 x ds_xor_b64 build (X64) produced
-// wrong accumulators in ~1% of recover groups for one unroll depth (U = 4;
-// U = 1, 2, 8 and every b32 build exact) — tools/debug/ragged_variants.hip.
-template <bool X64>
+// across the atomic XORs on type-based alias grounds.
+//   ACC = 0: window t's four dwords at 4t .. 4t+3 (ds_xor_b32 x4; lanes on
+//            consecutive windows hit every 4th bank: 4-way conflicts)
+//   ACC = 1: component-major, dword c of window t at c*kParWin + t (lanes on
+//            consecutive windows hit consecutive banks: conflict-free)
+//   ACC = 2: interleaved, 2 x ds_xor_b64 — wrong accumulators in ~1% of
+//            recover groups for one unroll depth (U = 4; every b32 build and
+//            U = 1, 2, 8 exact; tools/debug/ragged_variants.hip): not used.
+template <int ACC>
+__device__ __forceinline__ uint32_t acc_idx(uint32_t t, uint32_t c) {
+  return ACC == 1 ? c * (uint32_t)kParWin + t : 4u * t + c;
+}
+template <int ACC>
 __device__ __forceinline__ void lds_xor16(uint32_t* acc, uint32_t t, u32x4 v) {
-  if constexpr (X64) {
+  if constexpr (ACC == 2) {
     uint64_t* p = reinterpret_cast<uint64_t*>(acc + 4u * t);
     __hip_atomic_fetch_xor(p, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_xor(p + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
   } else {
-    uint32_t* p = acc + 4u * t;
-    __hip_atomic_fetch_xor(p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(p + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(p + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 0), v.x, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 1), v.y, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 2), v.z, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 3), v.w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
 }
+template <int ACC>
 __device__ __forceinline__ void lds_put16(uint32_t* acc, uint32_t t, u32x4 v) {
-  acc[4u * t] = v.x;
-  acc[4u * t + 1u] = v.y;
-  acc[4u * t + 2u] = v.z;
-  acc[4u * t + 3u] = v.w;
+  acc[acc_idx<ACC>(t, 0)] = v.x;
+  acc[acc_idx<ACC>(t, 1)] = v.y;
+  acc[acc_idx<ACC>(t, 2)] = v.z;
+  acc[acc_idx<ACC>(t, 3)] = v.w;
 }
+template <int ACC>
 __device__ __forceinline__ u32x4 lds_get16(const uint32_t* acc, uint32_t t) {
-  return u32x4{acc[4u * t], acc[4u * t + 1u], acc[4u * t + 2u], acc[4u * t + 3u]};
+  return u32x4{acc[acc_idx<ACC>(t, 0)], acc[acc_idx<ACC>(t, 1)], acc[acc_idx<ACC>(t, 2)],
+               acc[acc_idx<ACC>(t, 3)]};
 }
 
 // Bytes [16t, 16t+16) of a zero-padded packet (any len >= 1, 16t < len).
@@ -318,7 +332,7 @@ __device__ __forceinline__ u32x4 packet_window(const uint8_t* row, uint32_t len,
   return window16_small(row, len, 0u);  // t == 0 (rare: packets below 16 B)
 }
 
-template <bool RECOVER, bool NT, int U = 4, int WAVES = kFlatWaves, bool X64 = false>
+template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1>
 __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   __shared__ uint32_t s_par[WAVES][4 * kParWin];
   __shared__ uint64_t s_head[WAVES][kParWin];
@@ -354,9 +368,9 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
     // accumulator := the parity row (zero past plen)
     const uint8_t* prow = a.parity + a.parity_off[g];
     for (uint32_t t = lane; t < kParWin; t += 64u)
-      lds_put16(par, t, 16u * t < plen ? packet_window<NT>(prow, plen, t) : zero);
+      lds_put16<ACC>(par, t, 16u * t < plen ? packet_window<NT>(prow, plen, t) : zero);
   } else {
-    for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16(par, t, zero);
+    for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(par, t, zero);
   }
   const uint32_t kr = RECOVER ? k - 1u : k;  // received packets
   const uint32_t lim = RECOVER ? plen : kMaxPacket;
@@ -424,7 +438,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (tt[u] != 0xFFFFFFFFu) lds_xor16<X64>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+          if (tt[u] != 0xFFFFFFFFu) lds_xor16<ACC>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
       }
     } else {
       // Some packet below 16 B (rare): generic per-lane windows.
@@ -436,7 +450,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
         if (f < W) {
           const u32x4 md = meta[pi];
           const uint32_t t = f - md.w;
-          lds_xor16<X64>(par, t, packet_window<false>(a.bytes + (((uint64_t)md.y << 32) | md.x),
+          lds_xor16<ACC>(par, t, packet_window<false>(a.bytes + (((uint64_t)md.y << 32) | md.x),
                                                   md.z, t));
         }
       }
@@ -451,11 +465,11 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
     const uint32_t nw = (plen + 15u) >> 4;
     for (uint32_t t = lane; t < nw; t += 64u) {
       if (16u * t + 16u <= plen) {
-        st16t<NT>(dst + 16u * t, lds_get16(par, t));
+        st16t<NT>(dst + 16u * t, lds_get16<ACC>(par, t));
       } else {
         // tail: the 16 bytes ending at plen, from windows t-1 and t
         const uint32_t o = plen - 16u * t;  // 1..15
-        const u32x4 lo = lds_get16(par, t - 1u), hi = lds_get16(par, t);
+        const u32x4 lo = lds_get16<ACC>(par, t - 1u), hi = lds_get16<ACC>(par, t);
         const uint64_t a0 = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
         const uint64_t a1 = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
         const uint64_t a2 = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
@@ -470,7 +484,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
       }
     }
   } else if (lane < plen) {
-    dst[lane] = (uint8_t)(par[lane >> 2] >> (8u * (lane & 3u)));
+    dst[lane] = (uint8_t)(par[acc_idx<ACC>(0, lane >> 2)] >> (8u * (lane & 3u)));
   }
 }
 

@@ -114,18 +114,19 @@ int main(int argc, char** argv) {
   };
   using namespace qfec;
   const dim3 grid((uint32_t)((G + 3) / 4)), blk(256);
-#define QV(NAME, NT, U, X64)                                                                    \
+#define QV(NAME, NT, U, ACC)                                                                    \
   {NAME, [&](bool r) {                                                                          \
-     if (r) hipLaunchKernelGGL((ragged_xor_kernel<true, NT, U, 4, X64>), grid, blk, 0, 0, ar);  \
-     else hipLaunchKernelGGL((ragged_xor_kernel<false, NT, U, 4, X64>), grid, blk, 0, 0, ae);   \
+     if (r) hipLaunchKernelGGL((ragged_xor_kernel<true, NT, U, 4, ACC>), grid, blk, 0, 0, ar);  \
+     else hipLaunchKernelGGL((ragged_xor_kernel<false, NT, U, 4, ACC>), grid, blk, 0, 0, ae);   \
    }}
   std::vector<V> vs = {
       {"product", [&](bool r) { CK(launch_ragged(r ? ar : ae, r, 0)); }},
-      QV("nt U2 b32", true, 2, false),   QV("nt U4 b32", true, 4, false),
-      QV("nt U8 b32", true, 8, false),   QV("def U4 b32", false, 4, false),
-      QV("def U8 b32", false, 8, false), QV("nt U2 b64", true, 2, true),
-      QV("nt U4 b64", true, 4, true),    QV("nt U8 b64", true, 8, true),
-      QV("def U4 b64", false, 4, true),
+      QV("nt U2 b32", true, 2, 0),    QV("nt U4 b32", true, 4, 0),
+      QV("nt U8 b32", true, 8, 0),    QV("def U4 b32", false, 4, 0),
+      QV("nt U2 b32cm", true, 2, 1),  QV("nt U4 b32cm", true, 4, 1),
+      QV("def U2 b32cm", false, 2, 1), QV("nt U1 b32cm", true, 1, 1),
+      QV("nt U2 b64", true, 2, 2),    QV("nt U4 b64", true, 4, 2),
+      QV("nt U8 b64", true, 8, 2),    QV("def U4 b64", false, 4, 2),
   };
 #undef QV
   std::vector<uint8_t> h(G * 1452);

@@ -136,17 +136,19 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, false>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
                     }});
-#define TV(NAME, U, W)                                                                      \
+#define TV(NAME, U, W, ACC)                                                                 \
   vs.push_back({NAME, s.l.alg, [=] {                                                        \
-                  hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, true, U, W>),            \
+                  hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, true, U, W, ACC>),       \
                                      dim3((uint32_t)((G + W - 1) / W)), dim3(64 * W), 0, 0, a); \
                 }});
-      TV("flat U2 W4", 2, 4)
-      TV("flat U8 W4", 8, 4)
-      TV("flat U8 W8", 8, 8)
-      TV("flat U8 W2", 8, 2)
-      TV("flat U4 W1", 4, 1)
-      TV("flat U16 W4", 16, 4)
+      TV("flat U1 W4 cm", 1, 4, 1)
+      TV("flat U2 W4 cm", 2, 4, 1)
+      TV("flat U4 W4 cm", 4, 4, 1)
+      TV("flat U2 W4 il", 2, 4, 0)
+      TV("flat U4 W4 il", 4, 4, 0)
+      TV("flat U2 W2 cm", 2, 2, 1)
+      TV("flat U2 W8 cm", 2, 8, 1)
+      TV("flat U2 W1 cm", 2, 1, 1)
 #undef TV
       vs.push_back({"prev (2 fixed windows/lane, nt) " + s.name, s.l.alg, [=] {
                       hipLaunchKernelGGL((qfec::prev_ragged_xor_kernel<false, true>),
