@@ -147,6 +147,34 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
 /* out[j] ^= in[j] for j < n (QuicFecGroupInterface::XorBuffers). */
 int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, uint32_t flags);
 
+/* ---- packet protection around FEC (ENCRYPTION_NONE) -------------------- */
+/* The NULL packet protection libquic applies before the handshake completes:
+ * a 12-byte FNV-1a-128 tag of header || payload written in front of the
+ * payload.  Batched over a CSR layout (one lane per packet on the device):
+ * packet p's associated data (its packet header) is ad_len[p] bytes at
+ * bytes + ad_off[p]; its payload in_len[p] bytes at bytes + in_off[p].
+ *
+ * qfec_null_encrypt_batch replaces NullEncrypter::EncryptPacket
+ *   (src/net/quic/core/crypto/null_encrypter.cc:28-47), called per packet by
+ *   QuicPacketCreator::SerializePacket -> EncryptInPlace
+ *   (quic_packet_creator.cc:549): out + out_off[p] receives in_len[p] + 12
+ *   bytes, tag first.  out + out_off[p] may equal bytes + in_off[p] (in place,
+ *   as EncryptInPlace does) or must not overlap any input.
+ * qfec_null_decrypt_batch replaces NullDecrypter::DecryptPacket
+ *   (crypto/null_decrypter.cc:38-64), called by QuicFramer::DecryptPayload
+ *   (quic_framer.cc:1884): ok[p] = 1 and in_len[p] - 12 payload bytes at
+ *   out + out_off[p] when the tag verifies; ok[p] = 0 and the output untouched
+ *   when it does not (or in_len[p] < 12).  Output must not overlap the input.
+ * flags: QFEC_PTR_DEVICE / QFEC_PTR_HOST as above. */
+int qfec_null_encrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
+                            const uint16_t* ad_len, const uint64_t* in_off,
+                            const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                            const uint64_t* out_off, uint32_t flags);
+int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
+                            const uint16_t* ad_len, const uint64_t* in_off,
+                            const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                            const uint64_t* out_off, uint8_t* ok, uint32_t flags);
+
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of
  * splitmix64(seed ^ ((g*256 + i) << 32) ^ (j/8)) — generated on the device so

@@ -16,7 +16,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqfec.so")
 ARCH = os.environ.get("QFEC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["qfec_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc", "quic_fec_wire.cc"]
+SOURCES = ["qfec_kernels.hip", "qpp_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc",
+           "quic_fec_wire.cc"]
 HEADERS = ["qfec_internal.h", "quic_fec_group.h", "quic_fec_wire.h"]
 
 
@@ -53,7 +54,13 @@ def build_lib(force: bool = False, extra_flags=()) -> str:
                       "-I", os.path.join(ROOT, "include"), *extra_flags, "-c", s, "-o", o])
             objs.append(o)
         tmp = LIB + ".tmp"
-        _run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+        # export the C-ABI (qfec_*) and the C++ host mirror (net::*) only
+        vs = os.path.join(CSRC, "build", "exports.map")
+        with open(vs, "w") as f:
+            f.write('{\n  global:\n    qfec_*;\n    extern "C++" { net::*; };\n'
+                    '  local: *;\n};\n')
+        _run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", f"-Wl,--version-script={vs}",
+              "-o", tmp, *objs])
         os.replace(tmp, LIB)
     return LIB
 

@@ -634,6 +634,106 @@ int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, ui
   return QFEC_OK;
 }
 
+// ---- packet protection -----------------------------------------------------
+namespace {
+
+// Host-pointer path: stage the byte span the batch touches, its index arrays
+// and the output span through device allocations.
+int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64_t* ad_off,
+                 const uint16_t* ad_len, const uint64_t* in_off, const uint16_t* in_len,
+                 uint64_t n, uint8_t* out, const uint64_t* out_off, uint8_t* ok) {
+  uint64_t lo = UINT64_MAX, hi = 0, olo = UINT64_MAX, ohi = 0;
+  for (uint64_t p = 0; p < n; ++p) {
+    lo = std::min({lo, ad_off[p], in_off[p]});
+    hi = std::max({hi, ad_off[p] + ad_len[p], in_off[p] + in_len[p]});
+    const uint64_t olen = decrypt ? (in_len[p] >= 12 ? in_len[p] - 12u : 0u) : in_len[p] + 12u;
+    olo = std::min(olo, out_off[p]);
+    ohi = std::max(ohi, out_off[p] + olen);
+  }
+  std::vector<uint64_t> aoff(n), ioff(n), ooff(n);
+  for (uint64_t p = 0; p < n; ++p) {
+    aoff[p] = ad_off[p] - lo;
+    ioff[p] = in_off[p] - lo;
+    ooff[p] = out_off[p] - olo;
+  }
+  hipStream_t st = ctx->stream;
+  DevBuf d_bytes, d_aoff, d_alen, d_ioff, d_ilen, d_out, d_ooff, d_ok;
+  QFEC_HIP(ctx, hipMalloc(&d_bytes.p, std::max<uint64_t>(hi - lo, 1)));
+  QFEC_HIP(ctx, hipMalloc(&d_aoff.p, n * 8));
+  QFEC_HIP(ctx, hipMalloc(&d_alen.p, n * 2));
+  QFEC_HIP(ctx, hipMalloc(&d_ioff.p, n * 8));
+  QFEC_HIP(ctx, hipMalloc(&d_ilen.p, n * 2));
+  QFEC_HIP(ctx, hipMalloc(&d_out.p, std::max<uint64_t>(ohi - olo, 1)));
+  QFEC_HIP(ctx, hipMalloc(&d_ooff.p, n * 8));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_bytes.p, bytes + lo, hi - lo, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_aoff.p, aoff.data(), n * 8, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_alen.p, ad_len, n * 2, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_ioff.p, ioff.data(), n * 8, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_ilen.p, in_len, n * 2, hipMemcpyHostToDevice, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(d_ooff.p, ooff.data(), n * 8, hipMemcpyHostToDevice, st));
+  // seed the output span with the caller's bytes (gaps and failed packets stay)
+  QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, out + olo, ohi - olo, hipMemcpyHostToDevice, st));
+  if (decrypt) QFEC_HIP(ctx, hipMalloc(&d_ok.p, n));
+  qfec::ProtectArgs a{};
+  a.bytes = static_cast<const uint8_t*>(d_bytes.p);
+  a.ad_off = static_cast<const uint64_t*>(d_aoff.p);
+  a.ad_len = static_cast<const uint16_t*>(d_alen.p);
+  a.in_off = static_cast<const uint64_t*>(d_ioff.p);
+  a.in_len = static_cast<const uint16_t*>(d_ilen.p);
+  a.out = static_cast<uint8_t*>(d_out.p);
+  a.out_off = static_cast<const uint64_t*>(d_ooff.p);
+  a.ok = static_cast<uint8_t*>(d_ok.p);
+  a.n = n;
+  QFEC_HIP(ctx, qfec::launch_null_protect(a, decrypt, st));
+  QFEC_HIP(ctx, hipMemcpyAsync(out + olo, d_out.p, ohi - olo, hipMemcpyDeviceToHost, st));
+  if (decrypt) QFEC_HIP(ctx, hipMemcpyAsync(ok, d_ok.p, n, hipMemcpyDeviceToHost, st));
+  QFEC_HIP(ctx, hipStreamSynchronize(st));
+  return QFEC_OK;
+}
+
+int null_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64_t* ad_off,
+                 const uint16_t* ad_len, const uint64_t* in_off, const uint16_t* in_len,
+                 uint64_t n, uint8_t* out, const uint64_t* out_off, uint8_t* ok,
+                 uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n == 0) return QFEC_OK;
+  if (!bytes || !ad_off || !ad_len || !in_off || !in_len || !out || !out_off || (decrypt && !ok))
+    return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST)
+    return protect_host(ctx, decrypt, bytes, ad_off, ad_len, in_off, in_len, n, out, out_off, ok);
+  qfec::ProtectArgs a{};
+  a.bytes = bytes;
+  a.ad_off = ad_off;
+  a.ad_len = ad_len;
+  a.in_off = in_off;
+  a.in_len = in_len;
+  a.out = out;
+  a.out_off = out_off;
+  a.ok = ok;
+  a.n = n;
+  QFEC_HIP(ctx, qfec::launch_null_protect(a, decrypt, ctx->stream));
+  return QFEC_OK;
+}
+
+}  // namespace
+
+int qfec_null_encrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
+                            const uint16_t* ad_len, const uint64_t* in_off,
+                            const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                            const uint64_t* out_off, uint32_t flags) {
+  return null_protect(ctx, false, bytes, ad_off, ad_len, in_off, in_len, n_packets, out, out_off,
+                      nullptr, flags);
+}
+
+int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
+                            const uint16_t* ad_len, const uint64_t* in_off,
+                            const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                            const uint64_t* out_off, uint8_t* ok, uint32_t flags) {
+  return null_protect(ctx, true, bytes, ad_off, ad_len, in_off, in_len, n_packets, out, out_off,
+                      ok, flags);
+}
+
 int qfec_synth_fixed(qfec_ctx* ctx, uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
                      uint64_t group_stride, uint64_t g0, uint64_t n_groups, uint64_t seed) {
   int rc = bind(ctx);

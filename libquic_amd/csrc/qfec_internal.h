@@ -47,6 +47,23 @@ struct RaggedArgs {
   uint32_t* err;
 };
 
+// Packet protection batch (qpp_kernels.hip): packet p's associated data (the
+// packet header) is ad_len[p] bytes at bytes + ad_off[p], its input payload
+// in_len[p] bytes at bytes + in_off[p], its output at out + out_off[p].
+struct ProtectArgs {
+  const uint8_t* bytes;
+  const uint64_t* ad_off;
+  const uint16_t* ad_len;
+  const uint64_t* in_off;
+  const uint16_t* in_len;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint8_t* ok;  // decrypt: 1 = tag verified and payload written
+  uint64_t n;
+};
+
+hipError_t launch_null_protect(const ProtectArgs& a, bool decrypt, hipStream_t s);
+
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);

@@ -53,6 +53,10 @@ SIGNATURES = [
     ("qfec_recover_ragged", C.c_int,
      [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _vp, _u8p, _u8p, _vp, C.c_uint32]),
     ("qfec_xor_into", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_null_encrypt_batch", C.c_int,
+     [_vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, C.c_uint32]),
+    ("qfec_null_decrypt_batch", C.c_int,
+     [_vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p, C.c_uint32]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -207,6 +211,18 @@ class Context:
     def xor_into(self, src, n, dst, *, host=False):
         return self._check(self.lib.qfec_xor_into(self.ctx, _ptr(src), n, _ptr(dst),
                                                   QFEC_PTR_HOST if host else 0))
+
+    # -- packet protection (ENCRYPTION_NONE) --------------------------------
+    def null_encrypt(self, data, ad_off, ad_len, in_off, in_len, n, out, out_off, *, host=False):
+        return self._check(self.lib.qfec_null_encrypt_batch(
+            self.ctx, _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
+            _ptr(out), _ptr(out_off), QFEC_PTR_HOST if host else 0))
+
+    def null_decrypt(self, data, ad_off, ad_len, in_off, in_len, n, out, out_off, ok, *,
+                     host=False):
+        return self._check(self.lib.qfec_null_decrypt_batch(
+            self.ctx, _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
+            _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
 
     # -- synthetic inputs ----------------------------------------------------
     def synth_fixed(self, rows, k, L, g0, n_groups, seed, *, row_stride=None, group_stride=None):

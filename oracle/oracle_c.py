@@ -70,6 +70,23 @@ def lib():
         L.qo_fixed_digests.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
                                        C.c_uint32, C.c_int, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)]
+        # packet protection (qpp_oracle.h)
+        L.qo_fnv1a128_two.restype = None
+        L.qo_fnv1a128_two.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        for fn in (L.qo_null_encrypt, L.qo_null_decrypt):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
+                           C.c_size_t, C.POINTER(C.c_size_t)]
+        L.qo_null_encrypt_batch.restype = None
+        L.qo_null_encrypt_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
+                                                               C.c_void_p]
+        L.qo_null_decrypt_batch.restype = None
+        L.qo_null_decrypt_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
+                                                               C.c_void_p, C.c_void_p]
+        L.qo_null_encrypt_batch_mt.restype = None
+        L.qo_null_encrypt_batch_mt.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
+                                                                  C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -147,3 +164,58 @@ def fixed_digests(seed, drop_seed, g0, n, k, L, threads=None):
     a, b = C.c_uint64(0), C.c_uint64(0)
     lib().qo_fixed_digests(seed, drop_seed, g0, n, k, L, threads, C.byref(a), C.byref(b))
     return int(a.value), int(b.value)
+
+
+# ---- packet protection (qpp_oracle.h) -------------------------------------
+NULL_TAG = 12  # kHashSizeShort, null_encrypter.cc:15
+
+
+def _buf(b):
+    a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def fnv1a128_two(d1, d2=None):
+    a = _buf(d1)
+    lo, hi = C.c_uint64(0), C.c_uint64(0)
+    if d2 is None:
+        lib().qo_fnv1a128_two(_p(a), a.size, None, 0, C.byref(lo), C.byref(hi))
+    else:
+        b = _buf(d2)
+        lib().qo_fnv1a128_two(_p(a), a.size, _p(b), b.size, C.byref(lo), C.byref(hi))
+    return int(hi.value) << 64 | int(lo.value)
+
+
+def null_encrypt(ad, pt):
+    a, p = _buf(ad), _buf(pt)
+    out = np.zeros(p.size + NULL_TAG, np.uint8)
+    n = C.c_size_t(0)
+    ok = lib().qo_null_encrypt(_p(a), a.size, _p(p), p.size, _p(out), out.size, C.byref(n))
+    return bool(ok), out[:n.value]
+
+
+def null_decrypt(ad, ct):
+    a, c = _buf(ad), _buf(ct)
+    out = np.zeros(max(c.size - NULL_TAG, 0) + 1, np.uint8)
+    n = C.c_size_t(0)
+    ok = lib().qo_null_decrypt(_p(a), a.size, _p(c), c.size, _p(out), out.size, C.byref(n))
+    return bool(ok), out[:n.value]
+
+
+def null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, out_size, threads=1):
+    out = np.zeros(out_size, np.uint8)
+    args = [_p(data), _p(ad_off), _p(ad_len), _p(pt_off), _p(pt_len), pt_len.size, _p(out),
+            _p(out_off)]
+    if threads > 1:
+        lib().qo_null_encrypt_batch_mt(*args, threads)
+    else:
+        lib().qo_null_encrypt_batch(*args)
+    return out
+
+
+def null_decrypt_batch(data, ad_off, ad_len, ct_off, ct_len, out_off, out_size):
+    out = np.zeros(out_size, np.uint8)
+    ok = np.zeros(ct_len.size, np.uint8)
+    lib().qo_null_decrypt_batch(_p(data), _p(ad_off), _p(ad_len), _p(ct_off), _p(ct_len),
+                                ct_len.size, _p(out), _p(out_off), _p(ok))
+    return out, ok

@@ -1,0 +1,43 @@
+// ref_quic_shim.cc — C entry points into the REFERENCE's own packet
+// protection code, compiled from /root/reference by oracle/ref/Makefile into
+// oracle/_ref/libref_quic.so.  Test infrastructure only: it pins the
+// restatement in oracle/qpp_oracle.c (tests/test_oracle_protect.py) and
+// generates tests/golden/null_protect.npz (tests/golden/make_golden_protect.py).
+// No reference source is copied: this file only calls the reference classes.
+#include <stddef.h>
+#include <stdint.h>
+
+#include "net/base/int128.h"
+#include "net/quic/core/crypto/null_decrypter.h"
+#include "net/quic/core/crypto/null_encrypter.h"
+#include "net/quic/core/quic_utils.h"
+
+#define REF_API extern "C" __attribute__((visibility("default")))
+
+// QuicUtils::FNV1a_128_Hash_Two (quic_utils.cc:110)
+REF_API void ref_fnv1a128_two(const char* d1, int n1, const char* d2, int n2, uint64_t* lo,
+                              uint64_t* hi) {
+  const net::uint128 h = net::QuicUtils::FNV1a_128_Hash_Two(d1, n1, d2, n2);
+  *lo = net::Uint128Low64(h);
+  *hi = net::Uint128High64(h);
+}
+
+// NullEncrypter::EncryptPacket (crypto/null_encrypter.cc:28)
+REF_API int ref_null_encrypt(const char* ad, size_t ad_len, const char* pt, size_t pt_len,
+                             char* out, size_t cap, size_t* out_len) {
+  net::NullEncrypter e;
+  return e.EncryptPacket(net::kDefaultPathId, 1, base::StringPiece(ad, ad_len),
+                         base::StringPiece(pt, pt_len), out, out_len, cap)
+             ? 1
+             : 0;
+}
+
+// NullDecrypter::DecryptPacket (crypto/null_decrypter.cc:38)
+REF_API int ref_null_decrypt(const char* ad, size_t ad_len, const char* ct, size_t ct_len,
+                             char* out, size_t cap, size_t* out_len) {
+  net::NullDecrypter d;
+  return d.DecryptPacket(net::kDefaultPathId, 1, base::StringPiece(ad, ad_len),
+                         base::StringPiece(ct, ct_len), out, out_len, cap)
+             ? 1
+             : 0;
+}

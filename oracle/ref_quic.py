@@ -1,0 +1,89 @@
+"""ctypes loader for oracle/_ref/libref_quic.so — the REFERENCE's own
+NullEncrypter / NullDecrypter / QuicUtils::FNV1a_128_Hash_Two compiled from
+/root/reference by oracle/ref/Makefile.
+
+TEST INFRASTRUCTURE ONLY: used to pin oracle/qpp_oracle.c
+(tests/test_oracle_protect.py) and to generate tests/golden/null_protect.npz.
+Absent on a box without the reference build; callers skip then.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(_HERE, "_ref", "libref_quic.so")
+REF = "/root/reference"
+_lib = None
+
+
+def build() -> bool:
+    """Build from /root/reference when it exists (this container only)."""
+    if os.path.isdir(REF):
+        subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "ref"), f"REF={REF}"], check=True)
+    return os.path.exists(SO)
+
+
+def available() -> bool:
+    return os.path.exists(SO)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = C.CDLL(SO)
+        L.ref_fnv1a128_two.restype = None
+        L.ref_fnv1a128_two.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        for fn in (L.ref_null_encrypt, L.ref_null_decrypt):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
+                           C.c_size_t, C.POINTER(C.c_size_t)]
+        _lib = L
+    return _lib
+
+
+def _b(x):
+    a = np.frombuffer(bytes(x), dtype=np.uint8) if not isinstance(x, np.ndarray) else x
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a.size else None
+
+
+def fnv1a128_two(d1, d2=None):
+    a = _b(d1)
+    lo, hi = C.c_uint64(0), C.c_uint64(0)
+    if d2 is None:
+        lib().ref_fnv1a128_two(_ptr(a), a.size, None, 0, C.byref(lo), C.byref(hi))
+    else:
+        b = _b(d2)
+        # a non-null pointer even for an empty second part (the reference
+        # distinguishes nullptr, quic_utils.cc:121)
+        pb = b.ctypes.data_as(C.c_void_p) if b.size else C.cast(C.create_string_buffer(1), C.c_void_p)
+        lib().ref_fnv1a128_two(_ptr(a), a.size, pb, b.size, C.byref(lo), C.byref(hi))
+    return int(hi.value) << 64 | int(lo.value)
+
+
+def null_encrypt(ad, pt, cap=None):
+    a, p = _b(ad), _b(pt)
+    cap = p.size + 12 if cap is None else cap
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = C.c_size_t(0)
+    ok = lib().ref_null_encrypt(_ptr(a), a.size, _ptr(p), p.size, out.ctypes.data_as(C.c_void_p),
+                                cap, C.byref(n))
+    return bool(ok), out[:n.value].copy()
+
+
+def null_decrypt(ad, ct, cap=None):
+    a, c = _b(ad), _b(ct)
+    cap = max(c.size - 12, 0) if cap is None else cap
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = C.c_size_t(0)
+    ok = lib().ref_null_decrypt(_ptr(a), a.size, _ptr(c), c.size, out.ctypes.data_as(C.c_void_p),
+                                cap, C.byref(n))
+    return bool(ok), out[:n.value].copy()
