@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-ragged", action="store_true")
+    p.add_argument("--no-protect", action="store_true")
+    p.add_argument("--no-ceilings", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--profile-only", action="store_true",
@@ -276,11 +278,16 @@ def main():
     line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
                        work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified)
 
+    if not args.profile_only and rank == 0 and world == 1 and not args.no_ceilings:
+        line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
     if not args.profile_only and rank == 0 and world == 1:
         work.release()
         ctx, stream = work.ctx, work.stream
         if not args.no_ragged:
             line["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
+        if not args.no_protect:
+            line["protect"] = bench_protect(ctx, torch, dev, stream, G, k, L,
+                                            cpu=not args.no_cpu_baseline)
         if not args.no_e2e:
             line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
         if not args.no_cpu_baseline:
@@ -355,6 +362,116 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
             "recover_frac": round(b_rec / rec / 1e9 / HBM_PEAK_GBS, 4),
             "encode_us": round(enc * 1e6, 1), "recover_us": round(rec * 1e6, 1),
             "verified": bool(ok)}
+
+
+def _time_on(torch, stream, fn, reps):
+    """Mean ms of fn() over reps, HIP events on `stream` (the kernels' stream)."""
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def bench_ceilings(ctx, torch, buf, stream, reps=5):
+    """Measured streaming ceilings on this GPU: nt read of the
+    whole rows buffer and an nt copy of half of it into the other half."""
+    n = buf.numel()
+    half = (n // 2) & ~15
+    ms_r = _time_on(torch, stream, lambda: ctx.stream_probe(buf, n, buf, copy=False), reps)
+    ms_c = _time_on(torch, stream, lambda: ctx.stream_probe(buf, half, buf[half:], copy=True),
+                    reps)
+    return {"read_GBps": round(n / ms_r / 1e6, 1), "copy_GBps": round(2 * half / ms_c / 1e6, 1),
+            "read_frac_of_peak": round(n / ms_r / 1e6 / HBM_PEAK_GBS, 4),
+            "note": "nt 16-B streaming kernels (qfec_stream_probe), bytes moved / time"}
+
+
+def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
+    """Packet protection around FEC (ENCRYPTION_NONE, FNV-1a-128 tag): every
+    data packet of the headline workload (G x k packets of L bytes, a
+    `hdr`-byte header each) encrypted and decrypted in one batch each."""
+    n = G * k
+    rec = hdr + L
+    data = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+    # payload bytes from the counter-based generator (k rows of L at stride rec)
+    ctx.synth_fixed(data[hdr:], k, L, 0, G, SEED_FIXED, row_stride=rec, group_stride=k * rec)
+    ar = torch.arange(n, dtype=torch.int64, device=dev)
+    # header of packet p = the hdr bytes in front of its payload (the synth
+    # generator left them untouched: fill them with a pattern)
+    data.view(n, rec)[:, :hdr] = (ar.view(n, 1) * 131 + torch.arange(hdr, device=dev)).to(torch.uint8)
+    ad_off = ar * rec
+    pt_off = ad_off + hdr
+    ad_len = torch.full((n,), hdr, dtype=torch.int16, device=dev)
+    pt_len = torch.full((n,), L, dtype=torch.int16, device=dev)
+    out = torch.empty(n * (L + 12), dtype=torch.uint8, device=dev)
+    out_off = ar * (L + 12)
+    ms_e = _time_on(torch, stream, lambda: ctx.null_encrypt(data, ad_off, ad_len, pt_off, pt_len, n,
+                                                            out, out_off), reps)
+    # decrypt: [header | ciphertext] records
+    crec = hdr + L + 12
+    cat = torch.empty(n * crec, dtype=torch.uint8, device=dev)
+    cv = cat.view(n, crec)
+    cv[:, :hdr] = data.view(n, rec)[:, :hdr]
+    cv[:, hdr:] = out.view(n, L + 12)
+    del out
+    ct_len = torch.full((n,), L + 12, dtype=torch.int16, device=dev)
+    dout = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    c_ad_off, c_ct_off, d_out_off = ar * crec, ar * crec + hdr, ar * L
+    ms_d = _time_on(torch, stream, lambda: ctx.null_decrypt(cat, c_ad_off, ad_len, c_ct_off,
+                                                            ct_len, n, dout, d_out_off, ok), reps)
+    ctx.sync()
+    verified = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
+    b_enc = n * (hdr + L + L + 12)  # read header + payload, write tag + payload
+    b_dec = n * (hdr + L + 12 + L)
+    res = {"packets": n, "header": hdr, "payload": L,
+           "encrypt_GiBps": round(b_enc / (ms_e / 1e3) / 2**30, 2),
+           "decrypt_GiBps": round(b_dec / (ms_d / 1e3) / 2**30, 2),
+           "encrypt_hashed_GBps": round(n * (hdr + L) / (ms_e / 1e3) / 1e9, 1),
+           "encrypt_hbm_frac": round(b_enc / (ms_e / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+           "encrypt_us": round(ms_e * 1e3, 1), "decrypt_us": round(ms_d * 1e3, 1),
+           "bound": "valu (byte-serial FNV-1a-128 per packet, ~10 VALU instr / byte / lane)",
+           "verified": verified}
+    del cat, dout, data
+    torch.cuda.empty_cache()
+    if cpu:
+        res["cpu_baseline"] = cpu_protect_baseline(hdr, L)
+    return res
+
+
+def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
+    """Oracle (reference-pinned C restatement) NULL encrypt on the host cores."""
+    from oracle import oracle_c as OC
+    threads = min(16, os.cpu_count() or 1)
+    rec = hdr + L
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 256, n * rec, dtype=np.uint8)
+    ar = np.arange(n, dtype=np.uint64)
+    ad_off, pt_off = ar * np.uint64(rec), ar * np.uint64(rec) + np.uint64(hdr)
+    ad_len = np.full(n, hdr, np.uint16)
+    pt_len = np.full(n, L, np.uint16)
+    out_off = ar * np.uint64(L + 12)
+
+    def run(th):
+        t0, reps = time.perf_counter(), 0
+        while True:
+            OC.null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, n * (L + 12),
+                                  threads=th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                return reps * n * (hdr + L + L + 12) / el / 2**30, reps
+    mt, reps_mt = run(threads)
+    st, _ = run(1)
+    return {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_core_value": round(st, 3),
+            "sample": f"oracle NULL encrypt of {n} packets ({hdr}+{L} B), {reps_mt} passes on "
+                      f"{threads} threads (restatement pinned against the reference build)"}
 
 
 def bench_e2e(ctx, torch, k, L, G=1 << 18):

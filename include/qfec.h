@@ -175,6 +175,13 @@ int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t*
                             const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
                             const uint64_t* out_off, uint8_t* ok, uint32_t flags);
 
+/* ---- measurement support (bench.py, device pointers) ------------------- */
+/* Streaming bandwidth probe over n bytes of src (n rounded down to 16):
+ * mode 0 = read only (nt loads, XOR-folded; dst receives at most 16 bytes),
+ * mode 1 = copy src -> dst (nt loads + nt stores).  The measured ceilings the
+ * FEC kernels' rates are compared with. */
+int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* dst, int mode);
+
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of
  * splitmix64(seed ^ ((g*256 + i) << 32) ^ (j/8)) — generated on the device so

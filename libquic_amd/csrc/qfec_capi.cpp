@@ -734,6 +734,15 @@ int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t*
                       ok, flags);
 }
 
+int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* dst, int mode) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!src || !dst) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (mode != 0 && mode != 1) return fail(ctx, QFEC_ERR_INTERNAL, "probe mode %d", mode);
+  QFEC_HIP(ctx, qfec::launch_stream_probe(src, n, dst, mode == 1, ctx->stream));
+  return QFEC_OK;
+}
+
 int qfec_synth_fixed(qfec_ctx* ctx, uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
                      uint64_t group_stride, uint64_t g0, uint64_t n_groups, uint64_t seed) {
   int rc = bind(ctx);

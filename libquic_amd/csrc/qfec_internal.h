@@ -67,6 +67,8 @@ hipError_t launch_null_protect(const ProtectArgs& a, bool decrypt, hipStream_t s
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);
+hipError_t launch_stream_probe(const uint8_t* src, uint64_t n, uint8_t* dst, bool copy,
+                               hipStream_t s);
 hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_synth_fixed(uint8_t* rows, uint32_t k, uint32_t L, uint64_t row_stride,
                               uint64_t group_stride, uint64_t g0, uint64_t n, uint64_t seed,

@@ -505,6 +505,39 @@ __global__ __launch_bounds__(kBlock) void xor_into_kernel(const uint8_t* in, uin
 }
 
 // ---------------------------------------------------------------------------
+// Bandwidth probes (bench.py's measured ceilings): streaming
+// read (nt 16-B loads, 8 in flight per lane, XOR-folded) and copy (nt load +
+// nt store), grid-stride over n bytes (n a multiple of 16).
+// ---------------------------------------------------------------------------
+template <bool COPY>
+__global__ __launch_bounds__(kBlock) void stream_probe_kernel(const uint8_t* src, uint64_t n,
+                                                              uint8_t* dst) {
+  constexpr uint32_t U = 8;
+  const uint64_t nwin = n / 16u;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; w + (U - 1) * stride < nwin; w += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) v[u] = ld16t<true>(src + 16u * (w + u * stride));
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if constexpr (COPY) st16t<true>(dst + 16u * (w + u * stride), v[u]);
+      else acc ^= v[u];
+    }
+  }
+  for (; w < nwin; w += stride) {
+    const u32x4 v = ld16t<true>(src + 16u * w);
+    if constexpr (COPY) st16t<true>(dst + 16u * w, v);
+    else acc ^= v;
+  }
+  if constexpr (!COPY) {
+    if ((acc.x & acc.y & acc.z & acc.w) == 0xFFFFFFFFu) st16(dst, acc);  // keeps the loads
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic inputs (counter-based splitmix64).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -670,6 +703,17 @@ hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStrea
   if (blocks < 1) blocks = 1;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(xor_into_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, s, in, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_probe(const uint8_t* src, uint64_t n, uint8_t* dst, bool copy,
+                               hipStream_t s) {
+  if (n < 16) return hipSuccess;
+  const dim3 grid(8192), blk(kBlock);
+  if (copy)
+    hipLaunchKernelGGL(stream_probe_kernel<true>, grid, blk, 0, s, src, n & ~15ull, dst);
+  else
+    hipLaunchKernelGGL(stream_probe_kernel<false>, grid, blk, 0, s, src, n & ~15ull, dst);
   return hipGetLastError();
 }
 

@@ -15,14 +15,13 @@
 //     x ^= octet;  x = x*315 + (x << 88)            (mod 2^128)
 // = four v_mad_u64_u32 (the x*315 carry chain, with x0*2^24 folded into the
 // third limb's addend) + one v_mul_lo_u32 + a shift/add for the top limb.
-// The kernel is VALU-bound (≈10 instructions per byte per lane) with one
-// streaming pass over HBM; a lane reads its packet in 16-byte chunks (one
-// cache line serves four consecutive chunk loads of the lane).
+// The byte step is ≈10 VALU instructions per lane; a lane reads its packet in
+// batches of eight 16-byte chunks issued back to back (see kBatch).
 //
 // In-place encryption (QuicPacketCreator::EncryptInPlace: output == payload,
 // payload shifted right by the tag) is supported: the lane loads the payload's
-// last 16 bytes and chunk c+1 before it stores chunk c, and writes the tag
-// last.  Decrypt verifies first and copies the payload only when the tag
+// last 16 bytes first, never stores a chunk before the chunk after it is
+// loaded, and writes the tag last.  Decrypt verifies first and copies the payload only when the tag
 // matches (output untouched otherwise, as the reference's memcpy-after-check).
 #include "qfec_internal.h"
 
@@ -105,17 +104,26 @@ __device__ __forceinline__ void fnv_tail(Fnv128& h, u32x4 v, uint32_t len) {
   for (uint32_t i = first; i < first + rem; ++i) fnv_step(h, byte_of(v, i));
 }
 
+// A lane reads its packet in batches of kBatch 16-byte chunks (128 bytes, one
+// L2 line's worth) issued back to back, then hashes them: the line is consumed
+// while it is still in L2.  Loading chunk by chunk instead (load, hash ~170
+// instructions, load the next) lets 64 lanes x 8 waves x 256 CUs of
+// half-used lines fall out of L2 between a lane's consecutive chunks: 7x less
+// throughput measured (tools/tune/tune_protect.hip).
+constexpr uint32_t kBatch = 8;
+
 // Hash a span (no copy).
 __device__ __forceinline__ void fnv_span(Fnv128& h, const uint8_t* p, uint32_t len) {
   const uint32_t nfull = len >> 4;
   const u32x4 tail = load_tail(p, len);
-  uint32_t c = 0;
-  for (; c + 2u <= nfull; c += 2u) {  // two chunks in flight
-    const u32x4 a = ld16(p + 16u * c), b = ld16(p + 16u * c + 16u);
-    fnv_chunk(h, a);
-    fnv_chunk(h, b);
+  for (uint32_t c = 0; c < nfull; c += kBatch) {
+    u32x4 v[kBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u) v[u] = ld16(p + 16u * min(c + u, nfull - 1u));
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u)
+      if (c + u < nfull) fnv_chunk(h, v[u]);
   }
-  if (c < nfull) fnv_chunk(h, ld16(p + 16u * c));
   fnv_tail(h, tail, len);
 }
 
@@ -129,19 +137,51 @@ __device__ __forceinline__ void store_tail(uint8_t* d, u32x4 v, uint32_t len) {
   for (uint32_t i = 0; i < len; ++i) d[i] = (uint8_t)byte_of(v, i);
 }
 
-// Hash a span and copy it to d (d may equal p + 12: in-place encryption).
+// Hash a span and copy it to d.  d may equal p + 12 (in-place encryption):
+// the tail is loaded before any store, and the last chunk of a batch is
+// stored only after the next batch is loaded (its store reaches 12 bytes
+// into the next chunk).
 __device__ __forceinline__ void fnv_span_copy(Fnv128& h, const uint8_t* p, uint32_t len,
                                               uint8_t* d) {
   const uint32_t nfull = len >> 4;
-  const u32x4 tail = load_tail(p, len);  // before any store (in-place safety)
-  u32x4 next = nfull ? ld16(p) : u32x4{0u, 0u, 0u, 0u};
-  for (uint32_t c = 0; c < nfull; ++c) {
-    const u32x4 cur = next;
-    if (c + 1u < nfull) next = ld16(p + 16u * (c + 1u));  // before storing chunk c
-    fnv_chunk(h, cur);
-    st16(d + 16u * c, cur);
+  const u32x4 tail = load_tail(p, len);
+  u32x4 pend = {0u, 0u, 0u, 0u};
+  uint32_t pend_c = 0xFFFFFFFFu;  // chunk index of the deferred store
+  for (uint32_t c = 0; c < nfull; c += kBatch) {
+    u32x4 v[kBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u) v[u] = ld16(p + 16u * min(c + u, nfull - 1u));
+    if (pend_c != 0xFFFFFFFFu) st16(d + 16u * pend_c, pend);
+    const uint32_t nb = min(kBatch, nfull - c);
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u) {
+      if (u < nb) {
+        fnv_chunk(h, v[u]);
+        if (u + 1u < nb) st16(d + 16u * (c + u), v[u]);
+      }
+    }
+    pend = v[0];
+#pragma unroll
+    for (uint32_t u = 1; u < kBatch; ++u) pend = (u + 1u == nb) ? v[u] : pend;
+    pend_c = c + nb - 1u;
   }
+  if (pend_c != 0xFFFFFFFFu) st16(d + 16u * pend_c, pend);
   fnv_tail(h, tail, len);
+  store_tail(d, tail, len);
+}
+
+// Plain copy of a span, batched like the hash loops (decrypt's second pass).
+__device__ __forceinline__ void copy_span(const uint8_t* p, uint32_t len, uint8_t* d) {
+  const uint32_t nfull = len >> 4;
+  const u32x4 tail = load_tail(p, len);
+  for (uint32_t c = 0; c < nfull; c += kBatch) {
+    u32x4 v[kBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u) v[u] = ld16(p + 16u * min(c + u, nfull - 1u));
+#pragma unroll
+    for (uint32_t u = 0; u < kBatch; ++u)
+      if (c + u < nfull) st16(d + 16u * (c + u), v[u]);
+  }
   store_tail(d, tail, len);
 }
 
@@ -181,12 +221,7 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_kernel(ProtectArgs a) {
   a.ok[p] = ok ? 1 : 0;
   if (!ok) return;
   // copy after the check (null_decrypter.cc:60-62); the payload is in L2 now
-  uint8_t* o = a.out + a.out_off[p];
-  const uint8_t* src = ct + kTag;
-  const uint32_t nfull = plen >> 4;
-  const u32x4 tail = load_tail(src, plen);
-  for (uint32_t c = 0; c < nfull; ++c) st16(o + 16u * c, ld16(src + 16u * c));
-  store_tail(o, tail, plen);
+  copy_span(ct + kTag, plen, a.out + a.out_off[p]);
 }
 
 }  // namespace

@@ -57,6 +57,7 @@ SIGNATURES = [
      [_vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, C.c_uint32]),
     ("qfec_null_decrypt_batch", C.c_int,
      [_vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p, C.c_uint32]),
+    ("qfec_stream_probe", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -223,6 +224,10 @@ class Context:
         return self._check(self.lib.qfec_null_decrypt_batch(
             self.ctx, _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
             _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+
+    def stream_probe(self, src, n, dst, copy=False):
+        return self._check(self.lib.qfec_stream_probe(self.ctx, _ptr(src), n, _ptr(dst),
+                                                      1 if copy else 0))
 
     # -- synthetic inputs ----------------------------------------------------
     def synth_fixed(self, rows, k, L, g0, n_groups, seed, *, row_stride=None, group_stride=None):
