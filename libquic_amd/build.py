@@ -17,8 +17,8 @@ LIB = os.path.join(HERE, "libqfec.so")
 ARCH = os.environ.get("QFEC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["qfec_kernels.hip", "qpp_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc",
-           "quic_fec_wire.cc"]
-HEADERS = ["qfec_internal.h", "quic_fec_group.h", "quic_fec_wire.h"]
+           "quic_fec_wire.cc", "quic_fec_connection.cc"]
+HEADERS = ["qfec_internal.h", "quic_fec_group.h", "quic_fec_wire.h", "quic_fec_connection.h"]
 
 
 def hipcc() -> str:
@@ -65,24 +65,31 @@ def build_lib(force: bool = False, extra_flags=()) -> str:
     return LIB
 
 
-def build_cpp_tests(force: bool = False) -> str:
-    """tests/cpp/test_quic_fec_group: C++ host-mirror tests (run on the GPU box)."""
-    src = os.path.join(ROOT, "tests", "cpp", "test_quic_fec_group.cc")
-    out = os.path.join(ROOT, "tests", "cpp", "build", "test_quic_fec_group")
-    if not os.path.exists(src):
-        return ""
-    deps = [src, LIB, os.path.join(CSRC, "quic_fec_group.h"), os.path.join(CSRC, "quic_fec_wire.h"),
-            os.path.join(ROOT, "oracle", "qfec_oracle.c")]
-    if force or _stale(out, deps):
-        os.makedirs(os.path.dirname(out), exist_ok=True)
-        oobj = os.path.join(os.path.dirname(out), "qfec_oracle.o")
-        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-c", os.path.join(ROOT, "oracle", "qfec_oracle.c"),
-              "-o", oobj])
-        _run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
-              "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), src, oobj,
-              "-L", HERE, "-lqfec", "-Wl,-rpath,$ORIGIN/../../../libquic_amd",
-              "-Wl,-rpath-link,/opt/rocm/lib", "-lpthread", "-o", out])
-    return out
+CPP_TESTS = ["test_quic_fec_group", "test_quic_fec_connection"]
+
+
+def build_cpp_tests(force: bool = False) -> list:
+    """tests/cpp/<name>: C++ host-mirror tests linked against libqfec.so."""
+    outs = []
+    bdir = os.path.join(ROOT, "tests", "cpp", "build")
+    oracle_c = os.path.join(ROOT, "oracle", "qfec_oracle.c")
+    oobj = os.path.join(bdir, "qfec_oracle.o")
+    for name in CPP_TESTS:
+        src = os.path.join(ROOT, "tests", "cpp", name + ".cc")
+        out = os.path.join(bdir, name)
+        if not os.path.exists(src):
+            continue
+        deps = [src, LIB, oracle_c] + [os.path.join(CSRC, h) for h in HEADERS]
+        if force or _stale(out, deps):
+            os.makedirs(bdir, exist_ok=True)
+            if force or _stale(oobj, [oracle_c]):
+                _run(["gcc", "-O2", "-std=c11", "-fPIC", "-c", oracle_c, "-o", oobj])
+            _run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+                  "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), src, oobj,
+                  "-L", HERE, "-lqfec", "-Wl,-rpath,$ORIGIN/../../../libquic_amd",
+                  "-Wl,-rpath-link,/opt/rocm/lib", "-lpthread", "-o", out])
+        outs.append(out)
+    return outs
 
 
 if __name__ == "__main__":

@@ -1,0 +1,213 @@
+// quic_fec_connection.cc — see quic_fec_connection.h.
+#include "quic_fec_connection.h"
+
+#include <algorithm>
+
+namespace net {
+
+// ---------------------------------------------------------------------------
+// QuicFecSender
+// ---------------------------------------------------------------------------
+QuicFecSender::QuicFecSender(size_t max_packets_per_fec_group) {
+  set_max_packets_per_fec_group(max_packets_per_fec_group);
+}
+
+QuicFecSender::~QuicFecSender() = default;
+
+void QuicFecSender::set_max_packets_per_fec_group(size_t n) {
+  max_packets_per_fec_group_ = std::min<size_t>(std::max<size_t>(n, 1), QFEC_MAX_GROUP_PACKETS);
+}
+
+bool QuicFecSender::OnDataPacket(QuicPacketNumber packet_number, StringPiece payload,
+                                 bool entropy_flag, FecHeaderFields* fields) {
+  if (last_packet_number_ != kInvalidPacketNumber && packet_number <= last_packet_number_) {
+    detailed_error_ = "packet number does not increase: " + std::to_string(packet_number);
+    return false;
+  }
+  if (payload.size() > kMaxPacketSize) {
+    detailed_error_ = "Illegal payload size: " + std::to_string(payload.size());
+    return false;
+  }
+  FecHeaderFields f;
+  f.entropy_flag = entropy_flag;
+  if (fec_protect_) {
+    if (!group_) group_.reset(new QuicFecGroup(packet_number));
+    const QuicPacketNumber offset = packet_number - group_->FecGroupNumber();
+    if (offset > 0xFF) {  // uint8 first_fec_protected_packet_offset
+      detailed_error_ = "packet beyond the FEC group's uint8 offset range";
+      return false;
+    }
+    QuicPacketHeader h;
+    h.packet_number = packet_number;
+    h.entropy_flag = entropy_flag;
+    h.is_in_fec_group = IN_FEC_GROUP;
+    h.fec_group = group_->FecGroupNumber();
+    if (!group_->Update(ENCRYPTION_FORWARD_SECURE, h, payload)) {
+      detailed_error_ = group_->detailed_error();
+      return false;
+    }
+    f.in_fec_group = true;
+    f.fec_group_offset = static_cast<uint8_t>(offset);
+  }
+  last_packet_number_ = packet_number;
+  if (fields) *fields = f;
+  return true;
+}
+
+bool QuicFecSender::ShouldSendFec(bool force_close) const {
+  if (!group_) return false;
+  const size_t n = group_->NumReceivedPackets();
+  return n >= max_packets_per_fec_group_ || (force_close && n > 0);
+}
+
+bool QuicFecSender::CloseFecGroup(QuicPacketNumber fec_packet_number, QuicFecEncodeBatch* batch,
+                                  void* tag) {
+  if (!group_ || !batch) return false;
+  if (fec_packet_number <= last_packet_number_ ||
+      fec_packet_number - group_->FecGroupNumber() > 0xFF) {
+    detailed_error_ = "FEC packet number outside the group's offset range";
+    return false;
+  }
+  QuicFecEncodeBatch::Entry e;
+  e.tag = tag;
+  e.fec_packet_number = fec_packet_number;
+  e.fec_group = group_->FecGroupNumber();
+  e.group = std::move(group_);
+  batch->Add(std::move(e));
+  last_packet_number_ = fec_packet_number;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// QuicFecEncodeBatch
+// ---------------------------------------------------------------------------
+int QuicFecEncodeBatch::Flush(qfec_ctx* ctx) {
+  std::vector<QuicFecGroup*> groups;
+  groups.reserve(entries_.size());
+  for (Entry& e : entries_) groups.push_back(e.group.get());
+  const int rc = QuicFecGroup::ComputeAll(ctx, groups);  // one launch
+  if (rc != QFEC_OK) return rc;
+  for (Entry& e : entries_) {
+    const StringPiece red = e.group->PayloadParity();
+    e.fec_packet_body.resize(2 + red.size());
+    const size_t n = SerializeFecPacketBody(e.fec_packet_number, e.fec_group, e.entropy_flag, red,
+                                            e.fec_packet_body.data(), e.fec_packet_body.size());
+    if (n == 0) return QFEC_ERR_INVALID_FEC_DATA;
+    e.fec_packet_body.resize(n);
+  }
+  return QFEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// QuicFecReceiver
+// ---------------------------------------------------------------------------
+QuicFecReceiver::QuicFecReceiver(size_t max_fec_groups)
+    : max_fec_groups_(std::max<size_t>(max_fec_groups, 1)) {}
+
+QuicFecReceiver::~QuicFecReceiver() = default;
+
+QuicFecGroup* QuicFecReceiver::GetFecGroup(QuicFecGroupNumber n) {
+  auto it = group_map_.find(n);
+  if (it != group_map_.end()) return it->second.get();
+  if (closed_.count(n) != 0) return nullptr;  // finished / revived / closed: not recreated
+  if (group_map_.size() >= max_fec_groups_) {
+    // Too many groups: a group older than all kept ones was dropped before
+    // and is not recreated; otherwise the lowest group is dropped.
+    if (n < group_map_.begin()->first) return nullptr;
+    MarkClosed(group_map_.begin()->first);
+    group_map_.erase(group_map_.begin());
+  }
+  QuicFecGroup* g = new QuicFecGroup(n);
+  group_map_[n].reset(g);
+  return g;
+}
+
+bool QuicFecReceiver::OnPacket(EncryptionLevel level, const QuicPacketHeader& header,
+                               StringPiece payload) {
+  if (header.is_in_fec_group != IN_FEC_GROUP || header.fec_group == 0) {
+    detailed_error_ = "packet is not in an FEC group";
+    return false;
+  }
+  QuicFecGroup* g = GetFecGroup(header.fec_group);
+  if (!g) {
+    detailed_error_ = "FEC group already closed";
+    return false;
+  }
+  const bool ok = header.fec_flag ? g->UpdateFec(level, header, payload)
+                                  : g->Update(level, header, payload);
+  if (!ok) {
+    detailed_error_ = g->detailed_error();
+    return false;
+  }
+  if (g->IsFinished()) {  // nothing lost: no revival needed, stop tracking
+    MarkClosed(header.fec_group);
+    group_map_.erase(header.fec_group);
+  }
+  return true;
+}
+
+void QuicFecReceiver::MarkClosed(QuicFecGroupNumber n) {
+  closed_.insert(n);
+  while (closed_.size() > kClosedGroupMemory) closed_.erase(closed_.begin());
+}
+
+void QuicFecReceiver::CloseFecGroupsBefore(QuicPacketNumber packet_number) {
+  // groups that start below the threshold can never be useful again
+  closed_.erase(closed_.begin(), closed_.lower_bound(packet_number));
+  for (auto it = group_map_.begin(); it != group_map_.end();) {
+    if (it->second->IsWaitingForPacketBefore(packet_number)) {
+      MarkClosed(it->first);
+      it = group_map_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+size_t QuicFecReceiver::CollectRevivable(QuicFecReviveBatch* batch, void* tag) {
+  size_t n = 0;
+  for (auto it = group_map_.begin(); it != group_map_.end();) {
+    if (it->second->CanRevive()) {
+      MarkClosed(it->first);
+      batch->Add(tag, std::move(it->second));
+      it = group_map_.erase(it);
+      ++n;
+    } else {
+      ++it;
+    }
+  }
+  return n;
+}
+
+const QuicFecGroup* QuicFecReceiver::GetGroup(QuicFecGroupNumber n) const {
+  auto it = group_map_.find(n);
+  return it == group_map_.end() ? nullptr : it->second.get();
+}
+
+// ---------------------------------------------------------------------------
+// QuicFecReviveBatch
+// ---------------------------------------------------------------------------
+void QuicFecReviveBatch::Add(void* tag, std::unique_ptr<QuicFecGroup> group) {
+  groups_.emplace_back(tag, std::move(group));
+}
+
+int QuicFecReviveBatch::Flush(qfec_ctx* ctx, std::vector<Revived>* revived) {
+  std::vector<QuicFecGroup*> gs;
+  gs.reserve(groups_.size());
+  for (auto& g : groups_) gs.push_back(g.second.get());
+  const int rc = QuicFecGroup::ComputeAll(ctx, gs);  // one launch
+  if (rc != QFEC_OK) return rc;
+  char buf[kMaxPacketSize];
+  for (auto& g : groups_) {
+    Revived r;
+    r.tag = g.first;
+    const size_t n = g.second->Revive(&r.header, buf, sizeof(buf));
+    if (n == 0) continue;  // cannot happen for a CanRevive() group
+    r.payload.assign(buf, n);
+    if (revived) revived->push_back(std::move(r));
+  }
+  groups_.clear();
+  return QFEC_OK;
+}
+
+}  // namespace net

@@ -1,0 +1,186 @@
+// quic_fec_connection.h — connection-level FEC on top of the GPU-backed
+// QuicFecGroup: the send-side group state of the historical QuicPacketCreator
+// and the receive-side group map of the historical QuicConnection, with the
+// XOR work of many connections batched into ONE ragged kernel launch
+// (SURVEY.md §8(f) rank 2).
+//
+// The reference snapshot no longer has this code (FEC was removed at
+// QUIC_VERSION_32, src/net/quic/core/quic_protocol.h:373); what remains are
+// the two hook sites and the v<=31 wire vestiges:
+//   send:    QuicPacketCreator::SerializePacket (quic_packet_creator.cc:517-563)
+//            between BuildDataPacket (:530) and EncryptInPlace (:549) —
+//            QuicFecSender::OnDataPacket takes the plaintext after the header;
+//            when ShouldSendFec() the creator closes the group and serializes an
+//            FEC packet whose body comes from QuicFecEncodeBatch::Flush.
+//   receive: QuicConnection::ProcessValidatedPacket (quic_connection.cc:1388-1392,
+//            today "Drop any FEC packet") — QuicFecReceiver::OnPacket takes the
+//            decrypted payload of a packet in a group (or the redundancy of an
+//            FEC packet); revivable groups go to a QuicFecReviveBatch whose
+//            Flush returns the revived packets for QuicFramer's revived-packet
+//            path (the v<=31 ack frame lists them, quic_fec_wire.h).
+// Member names and semantics follow the historical classes [no in-container
+// source]: max_packets_per_fec_group (<= 255: uint8 offset,
+// quic_framer.cc:1126-1136), ShouldSendFec(force_close), IsFecGroupOpen,
+// kMaxFecGroups = 2 groups kept on receive with the lowest evicted,
+// CloseFecGroupsBefore(packet_number).
+//
+// Threading: like QuicConnection (quic_connection.h:14), not thread-safe; a
+// batch may collect from many connections of one thread.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <map>
+#include <set>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "quic_fec_group.h"
+#include "quic_fec_wire.h"
+
+namespace net {
+
+const size_t kMaxFecGroups = 2;                   // receive-side groups kept open
+const size_t kDefaultMaxPacketsPerFecGroup = 10;  // send-side group size
+
+class QuicFecEncodeBatch;
+class QuicFecReviveBatch;
+
+// ---------------------------------------------------------------------------
+// Send side (one per connection).
+// ---------------------------------------------------------------------------
+class QuicFecSender {
+ public:
+  explicit QuicFecSender(size_t max_packets_per_fec_group = kDefaultMaxPacketsPerFecGroup);
+  ~QuicFecSender();
+
+  // Clamped to [1, 255] (uint8 group offset).  Takes effect for the next group.
+  void set_max_packets_per_fec_group(size_t n);
+  size_t max_packets_per_fec_group() const { return max_packets_per_fec_group_; }
+
+  // FEC protection on/off for subsequent data packets (historical
+  // StartFecProtection / StopFecProtection); stopping does not close an open
+  // group — the caller sends its FEC packet first (ShouldSendFec(true)).
+  void StartFecProtection() { fec_protect_ = true; }
+  void StopFecProtection() { fec_protect_ = false; }
+  bool fec_protection() const { return fec_protect_; }
+
+  // A data packet was built (plaintext payload after the header).  When
+  // protection is on it joins the open group (opening one at this packet
+  // number if none is open); the return value holds the FEC header fields
+  // to write in front of it (in_fec_group + offset; WriteFecPrivateHeader).
+  // Fails (returns false) on a payload above kMaxPacketSize or a packet number
+  // that does not increase; *fields is then unchanged.
+  bool OnDataPacket(QuicPacketNumber packet_number, StringPiece payload, bool entropy_flag,
+                    FecHeaderFields* fields);
+
+  bool IsFecGroupOpen() const { return group_ != nullptr; }
+  size_t NumPacketsInGroup() const { return group_ ? group_->NumReceivedPackets() : 0; }
+  // The open group is full, or force_close and it holds at least one packet.
+  bool ShouldSendFec(bool force_close) const;
+
+  // Close the open group; its FEC packet will be packet `fec_packet_number`
+  // (> every packet of the group, at most 255 above the group's first).  The
+  // group moves into `batch`; its redundancy and serialized FEC packet body
+  // come from the batch's Flush.  `tag` identifies the connection there.
+  bool CloseFecGroup(QuicPacketNumber fec_packet_number, QuicFecEncodeBatch* batch,
+                     void* tag = nullptr);
+
+  const std::string& detailed_error() const { return detailed_error_; }
+
+ private:
+  size_t max_packets_per_fec_group_;
+  bool fec_protect_ = true;
+  std::unique_ptr<QuicFecGroup> group_;
+  QuicPacketNumber last_packet_number_ = kInvalidPacketNumber;
+  std::string detailed_error_;
+};
+
+// Closed send-side groups of any number of connections.
+class QuicFecEncodeBatch {
+ public:
+  struct Entry {
+    void* tag = nullptr;
+    QuicPacketNumber fec_packet_number = kInvalidPacketNumber;
+    QuicFecGroupNumber fec_group = 0;
+    bool entropy_flag = false;
+    std::unique_ptr<QuicFecGroup> group;
+    std::vector<uint8_t> fec_packet_body;  // private header + redundancy (after Flush)
+  };
+
+  // ONE ragged encode launch for every entry (QuicFecGroup::ComputeAll), then
+  // each entry's FEC packet body (SerializeFecPacketBody).  Returns a qfec_*
+  // code; on failure no body is filled.
+  int Flush(qfec_ctx* ctx);
+  std::vector<Entry>& entries() { return entries_; }
+  size_t size() const { return entries_.size(); }
+  void Clear() { entries_.clear(); }
+  void Add(Entry e) { entries_.push_back(std::move(e)); }
+
+ private:
+  std::vector<Entry> entries_;
+};
+
+// ---------------------------------------------------------------------------
+// Receive side (one per connection): the group map.
+// ---------------------------------------------------------------------------
+class QuicFecReceiver {
+ public:
+  explicit QuicFecReceiver(size_t max_fec_groups = kMaxFecGroups);
+  ~QuicFecReceiver();
+
+  // A decrypted packet that belongs to an FEC group: a data packet
+  // (header.is_in_fec_group, payload = plaintext after the header) or an FEC
+  // packet (header.fec_flag, payload = redundancy).  Returns false if it was
+  // not taken: not in a group, its group was already evicted, or the group
+  // refused it (duplicate, outside the protected range, oversize).
+  bool OnPacket(EncryptionLevel level, const QuicPacketHeader& header, StringPiece payload);
+
+  // Drop every group still waiting for a packet below `packet_number` (the
+  // peer stopped waiting for them: STOP_WAITING / least unacked).
+  void CloseFecGroupsBefore(QuicPacketNumber packet_number);
+
+  // Move every group that can revive now into `batch` (they leave the map;
+  // later packets of a revived group are ignored as finished).
+  size_t CollectRevivable(QuicFecReviveBatch* batch, void* tag = nullptr);
+
+  size_t NumGroups() const { return group_map_.size(); }
+  const QuicFecGroup* GetGroup(QuicFecGroupNumber n) const;
+  const std::string& detailed_error() const { return detailed_error_; }
+
+ private:
+  QuicFecGroup* GetFecGroup(QuicFecGroupNumber n);
+  void MarkClosed(QuicFecGroupNumber n);
+
+  // Recently finished / revived / evicted groups, so a late packet does not
+  // reopen them (bounded; CloseFecGroupsBefore prunes below its threshold).
+  static const size_t kClosedGroupMemory = 256;
+
+  size_t max_fec_groups_;
+  std::map<QuicFecGroupNumber, std::unique_ptr<QuicFecGroup>> group_map_;
+  std::set<QuicFecGroupNumber> closed_;
+  std::string detailed_error_;
+};
+
+// Revivable groups of any number of connections.
+class QuicFecReviveBatch {
+ public:
+  struct Revived {
+    void* tag = nullptr;
+    QuicPacketHeader header;  // packet_number of the lost packet, fec_group set
+    std::string payload;      // redundancy length, zero padded (PADDING frames)
+  };
+
+  void Add(void* tag, std::unique_ptr<QuicFecGroup> group);
+  size_t size() const { return groups_.size(); }
+  // ONE ragged launch for every collected group, then each group's revived
+  // packet, in collection order.  Returns a qfec_* code.
+  int Flush(qfec_ctx* ctx, std::vector<Revived>* revived);
+
+ private:
+  std::vector<std::pair<void*, std::unique_ptr<QuicFecGroup>>> groups_;
+};
+
+}  // namespace net
