@@ -87,6 +87,26 @@ def lib():
         L.qo_null_encrypt_batch_mt.restype = None
         L.qo_null_encrypt_batch_mt.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
                                                                   C.c_void_p, C.c_int]
+        # ChaCha20-Poly1305 (qaead_oracle.h)
+        L.qo_chacha20.restype = None
+        L.qo_chacha20.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                  C.c_uint32]
+        L.qo_poly1305.restype = None
+        L.qo_poly1305.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        for fn in (L.qo_c20p1305_seal, L.qo_c20p1305_open):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                           C.c_void_p, C.c_size_t, C.c_size_t]
+        for fn in (L.qo_quic_c20p1305_encrypt, L.qo_quic_c20p1305_decrypt):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint8, C.c_uint64,
+                           C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.qo_quic_c20p1305_encrypt_batch.restype = None
+        L.qo_quic_c20p1305_encrypt_batch.argtypes = [C.c_void_p] * 10 + [C.c_uint64, C.c_void_p,
+                                                                        C.c_void_p, C.c_int]
+        L.qo_quic_c20p1305_decrypt_batch.restype = None
+        L.qo_quic_c20p1305_decrypt_batch.argtypes = [C.c_void_p] * 10 + [C.c_uint64, C.c_void_p,
+                                                                        C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -218,4 +238,77 @@ def null_decrypt_batch(data, ad_off, ad_len, ct_off, ct_len, out_off, out_size):
     ok = np.zeros(ct_len.size, np.uint8)
     lib().qo_null_decrypt_batch(_p(data), _p(ad_off), _p(ad_len), _p(ct_off), _p(ct_len),
                                 ct_len.size, _p(out), _p(out_off), _p(ok))
+    return out, ok
+
+
+# ---- ChaCha20-Poly1305 (qaead_oracle.h) -----------------------------------
+AEAD_TAG = 12  # kAuthTagSize, chacha20_poly1305_encrypter.h
+
+
+def _pn(a):
+    return _p(a) if a.size else None
+
+
+def chacha20(key, nonce, data, counter=0):
+    k, n, d = _buf(key), _buf(nonce), _buf(data)
+    out = np.zeros(max(d.size, 1), np.uint8)
+    lib().qo_chacha20(_p(out), _pn(d), d.size, _p(k), _p(n), counter)
+    return out[:d.size]
+
+
+def poly1305(key, msg):
+    k, m = _buf(key), _buf(msg)
+    tag = np.zeros(16, np.uint8)
+    lib().qo_poly1305(_p(tag), _pn(m), m.size, _p(k))
+    return tag
+
+
+def c20p1305_seal(key, nonce, pt, ad, tag_len=16):
+    k, n, p, a = _buf(key), _buf(nonce), _buf(pt), _buf(ad)
+    out = np.zeros(p.size + tag_len, np.uint8)
+    lib().qo_c20p1305_seal(_p(out), _p(k), _p(n), _pn(p), p.size, _pn(a), a.size, tag_len)
+    return out
+
+
+def c20p1305_open(key, nonce, ct, ad, tag_len=16):
+    k, n, c, a = _buf(key), _buf(nonce), _buf(ct), _buf(ad)
+    out = np.zeros(max(c.size - tag_len, 0) + 1, np.uint8)
+    ok = lib().qo_c20p1305_open(_p(out), _p(k), _p(n), _pn(c), c.size, _pn(a), a.size, tag_len)
+    return bool(ok), out[:max(c.size - tag_len, 0)]
+
+
+def quic_c20p1305_encrypt(key, prefix, packet_number, ad, pt, path_id=0):
+    k, x, a, p = _buf(key), _buf(prefix), _buf(ad), _buf(pt)
+    out = np.zeros(p.size + AEAD_TAG, np.uint8)
+    lib().qo_quic_c20p1305_encrypt(_p(out), _p(k), _p(x), path_id, packet_number, _pn(a), a.size,
+                                   _pn(p), p.size)
+    return out
+
+
+def quic_c20p1305_decrypt(key, prefix, packet_number, ad, ct, path_id=0):
+    k, x, a, c = _buf(key), _buf(prefix), _buf(ad), _buf(ct)
+    out = np.zeros(max(c.size - AEAD_TAG, 0) + 1, np.uint8)
+    ok = lib().qo_quic_c20p1305_decrypt(_p(out), _p(k), _p(x), path_id, packet_number, _pn(a),
+                                        a.size, _pn(c), c.size)
+    return bool(ok), out[:max(c.size - AEAD_TAG, 0)]
+
+
+def quic_c20p1305_encrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                                ad_len, pt_off, pt_len, out_off, out_size, threads=1):
+    out = np.zeros(out_size, np.uint8)
+    lib().qo_quic_c20p1305_encrypt_batch(
+        _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
+        None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(pt_off),
+        _p(pt_len), pt_len.size, _p(out), _p(out_off), threads)
+    return out
+
+
+def quic_c20p1305_decrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                                ad_len, ct_off, ct_len, out_off, out_size):
+    out = np.zeros(out_size, np.uint8)
+    ok = np.zeros(ct_len.size, np.uint8)
+    lib().qo_quic_c20p1305_decrypt_batch(
+        _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
+        None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(ct_off),
+        _p(ct_len), ct_len.size, _p(out), _p(out_off), _p(ok))
     return out, ok

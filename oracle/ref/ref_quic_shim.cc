@@ -12,6 +12,11 @@
 #include "net/quic/core/crypto/null_encrypter.h"
 #include "net/quic/core/quic_utils.h"
 
+extern "C" {
+#include <openssl/chacha.h>
+#include <openssl/poly1305.h>
+}
+
 #define REF_API extern "C" __attribute__((visibility("default")))
 
 // QuicUtils::FNV1a_128_Hash_Two (quic_utils.cc:110)
@@ -40,4 +45,22 @@ REF_API int ref_null_decrypt(const char* ad, size_t ad_len, const char* ct, size
                          base::StringPiece(ct, ct_len), out, out_len, cap)
              ? 1
              : 0;
+}
+
+// BoringSSL CRYPTO_chacha_20 (boringssl/crypto/chacha/chacha.c:118)
+REF_API void ref_chacha20(uint8_t* out, const uint8_t* in, size_t len, const uint8_t* key,
+                          const uint8_t* nonce, uint32_t counter) {
+  CRYPTO_chacha_20(out, in, len, key, nonce, counter);
+}
+
+// BoringSSL CRYPTO_poly1305_* (boringssl/crypto/poly1305/poly1305_vec.c), one
+// message fed in `nsplit` arbitrary pieces to exercise the update buffering.
+REF_API void ref_poly1305(uint8_t* tag, const uint8_t* msg, size_t len, const uint8_t* key,
+                          size_t split) {
+  poly1305_state st;
+  CRYPTO_poly1305_init(&st, key);
+  if (split == 0 || split > len) split = len;
+  CRYPTO_poly1305_update(&st, msg, split);
+  CRYPTO_poly1305_update(&st, msg + split, len - split);
+  CRYPTO_poly1305_finish(&st, tag);
 }

@@ -42,6 +42,11 @@ def lib():
             fn.restype = C.c_int
             fn.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
                            C.c_size_t, C.POINTER(C.c_size_t)]
+        L.ref_chacha20.restype = None
+        L.ref_chacha20.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                   C.c_uint32]
+        L.ref_poly1305.restype = None
+        L.ref_poly1305.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         _lib = L
     return _lib
 
@@ -87,3 +92,19 @@ def null_decrypt(ad, ct, cap=None):
     ok = lib().ref_null_decrypt(_ptr(a), a.size, _ptr(c), c.size, out.ctypes.data_as(C.c_void_p),
                                 cap, C.byref(n))
     return bool(ok), out[:n.value].copy()
+
+
+def chacha20(key, nonce, data, counter=0):
+    """BoringSSL CRYPTO_chacha_20 (the reference's C implementation)."""
+    k, n, d = _b(key), _b(nonce), _b(data)
+    out = np.zeros(max(d.size, 1), np.uint8)
+    lib().ref_chacha20(out.ctypes.data_as(C.c_void_p), _ptr(d), d.size, _ptr(k), _ptr(n), counter)
+    return out[:d.size].copy()
+
+
+def poly1305(key, msg, split=0):
+    """BoringSSL CRYPTO_poly1305_{init,update,finish} (poly1305_vec.c)."""
+    k, m = _b(key), _b(msg)
+    tag = np.zeros(16, np.uint8)
+    lib().ref_poly1305(tag.ctypes.data_as(C.c_void_p), _ptr(m), m.size, _ptr(k), split)
+    return tag

@@ -1,0 +1,95 @@
+"""CPU tests of the ChaCha20-Poly1305 oracle (oracle/qaead_oracle.c): pinned by
+BoringSSL's own test vectors from the reference tree
+(tests/golden/chacha20_poly1305.npz, made by tests/golden/make_golden_aead.py
+from boringssl/crypto/cipher/test/chacha20_poly1305_tests.txt) and, for the
+primitives, by the reference's chacha.c / poly1305_vec.c compiled into
+oracle/_ref (skipped where that build is absent)."""
+import numpy as np
+import pytest
+
+from oracle import oracle_c as OC
+from oracle import ref_quic as R
+
+from conftest import load_npz
+
+
+@pytest.fixture(scope="module")
+def vec():
+    z = load_npz("chacha20_poly1305.npz")
+
+    def get(f, i):
+        o, l = int(z[f + "_off"][i]), int(z[f + "_len"][i])
+        return z[f][o:o + l]
+    return z, get
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not R.available() and not R.build():
+        pytest.skip("reference build oracle/_ref absent (no /root/reference here)")
+    return R
+
+
+def test_boringssl_vectors_seal_open(vec):
+    z, get = vec
+    n = z["key_len"].size
+    assert n == 81
+    for i in range(n):
+        key, nonce, pt, ad, ct, tag = (get(f, i) for f in ("key", "nonce", "in", "ad", "ct", "tag"))
+        out = OC.c20p1305_seal(key, nonce, pt, ad, tag_len=tag.size)
+        assert np.array_equal(out[:pt.size], ct), i
+        assert np.array_equal(out[pt.size:], tag), i
+        ok, dec = OC.c20p1305_open(key, nonce, out, ad, tag_len=tag.size)
+        assert ok and np.array_equal(dec, pt), i
+        bad = out.copy()
+        bad[-1] ^= 1
+        assert not OC.c20p1305_open(key, nonce, bad, ad, tag_len=tag.size)[0], i
+
+
+def test_rfc7539_keystream_kat():
+    # RFC 7539 §2.4.2: key 00..1f, nonce 000000000000004a00000000, counter 1
+    key = bytes(range(32))
+    nonce = bytes.fromhex("000000000000004a00000000")
+    pt = (b"Ladies and Gentlemen of the class of '99: If I could offer you only one tip "
+          b"for the future, sunscreen would be it.")
+    ct = OC.chacha20(key, nonce, pt, counter=1)
+    assert bytes(ct[:16]).hex() == "6e2e359a2568f98041ba0728dd0d6981"
+
+
+def test_rfc7539_poly1305_kat():
+    # RFC 7539 §2.5.2
+    key = bytes.fromhex("85d6be7857556d337f4452fe42d506a80103808afb0db2fd4abff6af4149f51b")
+    tag = OC.poly1305(key, b"Cryptographic Forum Research Group")
+    assert bytes(tag).hex() == "a8061dc1305136c6c22b8baf0c0127a9"
+
+
+def test_primitives_vs_reference_random(ref):
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        key = rng.integers(0, 256, 32, dtype=np.uint8)
+        nonce = rng.integers(0, 256, 12, dtype=np.uint8)
+        data = rng.integers(0, 256, int(rng.integers(0, 1500)), dtype=np.uint8)
+        ctr = int(rng.integers(0, 2**32 - 64))
+        assert np.array_equal(OC.chacha20(key, nonce, data, ctr), ref.chacha20(key, nonce, data, ctr))
+        split = int(rng.integers(0, data.size + 1))
+        assert np.array_equal(OC.poly1305(key, data), ref.poly1305(key, data, split))
+
+
+def test_quic_packet_form():
+    rng = np.random.default_rng(9)
+    key = rng.integers(0, 256, 32, dtype=np.uint8)
+    prefix = rng.integers(0, 256, 4, dtype=np.uint8)
+    ad = rng.integers(0, 256, 21, dtype=np.uint8)
+    pt = rng.integers(0, 256, 1350, dtype=np.uint8)
+    pn = 0x0000123456789ABC
+    ct = OC.quic_c20p1305_encrypt(key, prefix, pn, ad, pt)
+    # == RFC AEAD with nonce prefix || LE64(packet number), tag truncated to 12
+    nonce = np.concatenate([prefix, np.frombuffer(pn.to_bytes(8, "little"), np.uint8)])
+    assert np.array_equal(ct, OC.c20p1305_seal(key, nonce, pt, ad, tag_len=12))
+    ok, back = OC.quic_c20p1305_decrypt(key, prefix, pn, ad, ct)
+    assert ok and np.array_equal(back, pt)
+    assert not OC.quic_c20p1305_decrypt(key, prefix, pn + 1, ad, ct)[0]
+    # path id occupies the top byte of the packed packet number
+    ct7 = OC.quic_c20p1305_encrypt(key, prefix, pn, ad, pt, path_id=7)
+    nonce7 = np.concatenate([prefix, np.frombuffer(((7 << 56) | pn).to_bytes(8, "little"), np.uint8)])
+    assert np.array_equal(ct7, OC.c20p1305_seal(key, nonce7, pt, ad, tag_len=12))
