@@ -175,6 +175,35 @@ int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t*
                             const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
                             const uint64_t* out_off, uint8_t* ok, uint32_t flags);
 
+/* ChaCha20-Poly1305 packet protection (the AEAD libquic negotiates, 12-byte
+ * tags), batched like the NULL forms above.  Packet p is protected under key
+ * key_idx[p]: keys holds 32 bytes per key, prefixes the 4-byte nonce prefix
+ * per key; the 12-byte nonce is prefix || LE64(path_id[p] << 56 |
+ * packet_number[p]) (path_id may be NULL: all 0).
+ * qfec_chacha20poly1305_seal_batch replaces ChaCha20Poly1305Encrypter::
+ *   EncryptPacket (AeadBaseEncrypter::EncryptPacket,
+ *   src/net/quic/core/crypto/aead_base_encrypter.cc:107-134 -> BoringSSL
+ *   EVP_aead_chacha20_poly1305): out + out_off[p] receives in_len[p] + 12
+ *   bytes, ciphertext then tag; it may equal bytes + in_off[p] (in place).
+ * qfec_chacha20poly1305_open_batch replaces ChaCha20Poly1305Decrypter::
+ *   DecryptPacket (aead_base_decrypter.cc): ok[p] = 1 and in_len[p] - 12
+ *   plaintext bytes at out + out_off[p] when the tag verifies; ok[p] = 0 and
+ *   the output untouched otherwise.  Output must not overlap the input. */
+int qfec_chacha20poly1305_seal_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len,
+                                     uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
+                                     uint32_t flags);
+int qfec_chacha20poly1305_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len,
+                                     uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
+                                     uint8_t* ok, uint32_t flags);
+
 /* ---- measurement support (bench.py, device pointers) ------------------- */
 /* Streaming bandwidth probe over n bytes of src (n rounded down to 16):
  * mode 0 = read only (nt loads, XOR-folded; dst receives at most 16 bytes),

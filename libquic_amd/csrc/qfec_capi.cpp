@@ -639,9 +639,20 @@ namespace {
 
 // Host-pointer path: stage the byte span the batch touches, its index arrays
 // and the output span through device allocations.
+// aead == nullptr: NULL protection; otherwise its key table / per-packet
+// arrays (host pointers) are staged too and the ChaCha20-Poly1305 kernels run.
+struct AeadHost {
+  const uint8_t* keys;
+  const uint8_t* prefixes;
+  const uint32_t* key_idx;
+  const uint64_t* packet_number;
+  const uint8_t* path_id;
+};
+
 int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64_t* ad_off,
                  const uint16_t* ad_len, const uint64_t* in_off, const uint16_t* in_len,
-                 uint64_t n, uint8_t* out, const uint64_t* out_off, uint8_t* ok) {
+                 uint64_t n, uint8_t* out, const uint64_t* out_off, uint8_t* ok,
+                 const AeadHost* aead = nullptr) {
   uint64_t lo = UINT64_MAX, hi = 0, olo = UINT64_MAX, ohi = 0;
   for (uint64_t p = 0; p < n; ++p) {
     lo = std::min({lo, ad_off[p], in_off[p]});
@@ -684,6 +695,35 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
   a.out_off = static_cast<const uint64_t*>(d_ooff.p);
   a.ok = static_cast<uint8_t*>(d_ok.p);
   a.n = n;
+  if (aead) {
+    uint32_t nkeys = 0;
+    for (uint64_t p = 0; p < n; ++p) nkeys = std::max(nkeys, aead->key_idx[p] + 1u);
+    DevBuf d_keys, d_pre, d_kidx, d_pn, d_path;
+    QFEC_HIP(ctx, hipMalloc(&d_keys.p, 32ull * nkeys));
+    QFEC_HIP(ctx, hipMalloc(&d_pre.p, 4ull * nkeys));
+    QFEC_HIP(ctx, hipMalloc(&d_kidx.p, n * 4));
+    QFEC_HIP(ctx, hipMalloc(&d_pn.p, n * 8));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_keys.p, aead->keys, 32ull * nkeys, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_pre.p, aead->prefixes, 4ull * nkeys, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_kidx.p, aead->key_idx, n * 4, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_pn.p, aead->packet_number, n * 8, hipMemcpyHostToDevice, st));
+    if (aead->path_id) {
+      QFEC_HIP(ctx, hipMalloc(&d_path.p, n));
+      QFEC_HIP(ctx, hipMemcpyAsync(d_path.p, aead->path_id, n, hipMemcpyHostToDevice, st));
+    }
+    qfec::AeadArgs aa{};
+    aa.io = a;
+    aa.keys = static_cast<const uint8_t*>(d_keys.p);
+    aa.prefixes = static_cast<const uint8_t*>(d_pre.p);
+    aa.key_idx = static_cast<const uint32_t*>(d_kidx.p);
+    aa.packet_number = static_cast<const uint64_t*>(d_pn.p);
+    aa.path_id = static_cast<const uint8_t*>(d_path.p);
+    QFEC_HIP(ctx, qfec::launch_chacha20poly1305(aa, decrypt, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(out + olo, d_out.p, ohi - olo, hipMemcpyDeviceToHost, st));
+    if (decrypt) QFEC_HIP(ctx, hipMemcpyAsync(ok, d_ok.p, n, hipMemcpyDeviceToHost, st));
+    QFEC_HIP(ctx, hipStreamSynchronize(st));
+    return QFEC_OK;
+  }
   QFEC_HIP(ctx, qfec::launch_null_protect(a, decrypt, st));
   QFEC_HIP(ctx, hipMemcpyAsync(out + olo, d_out.p, ohi - olo, hipMemcpyDeviceToHost, st));
   if (decrypt) QFEC_HIP(ctx, hipMemcpyAsync(ok, d_ok.p, n, hipMemcpyDeviceToHost, st));
@@ -718,6 +758,41 @@ int null_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
 
 }  // namespace
 
+int chacha_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* keys, const uint8_t* prefixes,
+                   const uint32_t* key_idx, const uint64_t* packet_number, const uint8_t* path_id,
+                   const uint8_t* bytes, const uint64_t* ad_off, const uint16_t* ad_len,
+                   const uint64_t* in_off, const uint16_t* in_len, uint64_t n, uint8_t* out,
+                   const uint64_t* out_off, uint8_t* ok, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n == 0) return QFEC_OK;
+  if (!keys || !prefixes || !key_idx || !packet_number || !bytes || !ad_off || !ad_len ||
+      !in_off || !in_len || !out || !out_off || (decrypt && !ok))
+    return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & QFEC_PTR_HOST) {
+    const AeadHost h{keys, prefixes, key_idx, packet_number, path_id};
+    return protect_host(ctx, decrypt, bytes, ad_off, ad_len, in_off, in_len, n, out, out_off, ok,
+                        &h);
+  }
+  qfec::AeadArgs a{};
+  a.io.bytes = bytes;
+  a.io.ad_off = ad_off;
+  a.io.ad_len = ad_len;
+  a.io.in_off = in_off;
+  a.io.in_len = in_len;
+  a.io.out = out;
+  a.io.out_off = out_off;
+  a.io.ok = ok;
+  a.io.n = n;
+  a.keys = keys;
+  a.prefixes = prefixes;
+  a.key_idx = key_idx;
+  a.packet_number = packet_number;
+  a.path_id = path_id;
+  QFEC_HIP(ctx, qfec::launch_chacha20poly1305(a, decrypt, ctx->stream));
+  return QFEC_OK;
+}
+
 int qfec_null_encrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
                             const uint16_t* ad_len, const uint64_t* in_off,
                             const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
@@ -732,6 +807,28 @@ int qfec_null_decrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t*
                             const uint64_t* out_off, uint8_t* ok, uint32_t flags) {
   return null_protect(ctx, true, bytes, ad_off, ad_len, in_off, in_len, n_packets, out, out_off,
                       ok, flags);
+}
+
+int qfec_chacha20poly1305_seal_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len,
+                                     uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
+                                     uint32_t flags) {
+  return chacha_protect(ctx, false, keys, prefixes, key_idx, packet_number, path_id, bytes,
+                        ad_off, ad_len, in_off, in_len, n_packets, out, out_off, nullptr, flags);
+}
+
+int qfec_chacha20poly1305_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len,
+                                     uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
+                                     uint8_t* ok, uint32_t flags) {
+  return chacha_protect(ctx, true, keys, prefixes, key_idx, packet_number, path_id, bytes,
+                        ad_off, ad_len, in_off, in_len, n_packets, out, out_off, ok, flags);
 }
 
 int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* dst, int mode) {

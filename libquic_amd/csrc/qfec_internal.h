@@ -64,6 +64,20 @@ struct ProtectArgs {
 
 hipError_t launch_null_protect(const ProtectArgs& a, bool decrypt, hipStream_t s);
 
+// ChaCha20-Poly1305 (QUIC: 12-byte tag, nonce = prefix || LE64(path<<56|pn)).
+// Packet p is protected with key key_idx[p] (keys: 32 B each, prefixes: 4 B
+// each), packet number packet_number[p], path id path_id[p] (nullptr: 0).
+struct AeadArgs {
+  ProtectArgs io;
+  const uint8_t* keys;
+  const uint8_t* prefixes;
+  const uint32_t* key_idx;
+  const uint64_t* packet_number;
+  const uint8_t* path_id;
+};
+
+hipError_t launch_chacha20poly1305(const AeadArgs& a, bool decrypt, hipStream_t s);
+
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);

@@ -305,6 +305,358 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   if (ok) store_tail(o, tail, plen);
 }
 
+// ===========================================================================
+// ChaCha20-Poly1305 (RFC 7539 AEAD; QUIC: 12-byte tag)
+//   seal  AeadBaseEncrypter::EncryptPacket  crypto/aead_base_encrypter.cc:107-134
+//         -> EVP_aead_chacha20_poly1305 seal_impl,
+//            boringssl/crypto/cipher/e_chacha20poly1305.c:106-140
+//   open  AeadBaseDecrypter::DecryptPacket  -> open_impl (:142-176)
+// One lane per packet again (Poly1305 is a serial MAC over the packet): the
+// lane generates its packet's keystream block by block (ChaCha20, counter 1..)
+// while the payload moves through the same LDS-staged slabs as above; the
+// ciphertext goes back into the lane's LDS row and leaves by coalesced stores.
+// Poly1305 runs in five 26-bit limbs (25 v_mad_u64_u32 per 16-byte block).
+// ===========================================================================
+__device__ __forceinline__ uint32_t rotl32(uint32_t v, uint32_t n) {
+  return __builtin_amdgcn_alignbit(v, v, 32u - n);
+}
+
+#define QPP_QR(a, b, c, d)   \
+  a += b; d = rotl32(d ^ a, 16); \
+  c += d; b = rotl32(b ^ c, 12); \
+  a += b; d = rotl32(d ^ a, 8);  \
+  c += d; b = rotl32(b ^ c, 7);
+
+struct ChachaKey {
+  uint32_t k[8];
+  uint32_t n[3];
+};
+
+// One 64-byte keystream block (chacha.c:80-116) into ks[16].
+__device__ __forceinline__ void chacha_block(const ChachaKey& key, uint32_t counter,
+                                             uint32_t (&ks)[16]) {
+  uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    key.k[0], key.k[1], key.k[2], key.k[3],
+                    key.k[4], key.k[5], key.k[6], key.k[7],
+                    counter, key.n[0], key.n[1], key.n[2]};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    QPP_QR(x[0], x[4], x[8], x[12]) QPP_QR(x[1], x[5], x[9], x[13])
+    QPP_QR(x[2], x[6], x[10], x[14]) QPP_QR(x[3], x[7], x[11], x[15])
+    QPP_QR(x[0], x[5], x[10], x[15]) QPP_QR(x[1], x[6], x[11], x[12])
+    QPP_QR(x[2], x[7], x[8], x[13]) QPP_QR(x[3], x[4], x[9], x[14])
+  }
+  const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                           key.k[0], key.k[1], key.k[2], key.k[3],
+                           key.k[4], key.k[5], key.k[6], key.k[7],
+                           counter, key.n[0], key.n[1], key.n[2]};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ks[i] = x[i] + in[i];
+}
+#undef QPP_QR
+
+struct Poly1305 {
+  uint32_t r0, r1, r2, r3, r4;
+  uint32_t h0, h1, h2, h3, h4;
+  uint32_t pad[4];
+};
+
+__device__ __forceinline__ void poly_init(Poly1305& p, const uint32_t (&k)[16]) {
+  // r clamp (RFC 7539 §2.5) in 26-bit limbs
+  p.r0 = k[0] & 0x3ffffffu;
+  p.r1 = ((k[0] >> 26) | (k[1] << 6)) & 0x3ffff03u;
+  p.r2 = ((k[1] >> 20) | (k[2] << 12)) & 0x3ffc0ffu;
+  p.r3 = ((k[2] >> 14) | (k[3] << 18)) & 0x3f03fffu;
+  p.r4 = (k[3] >> 8) & 0x00fffffu;
+  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
+  p.pad[0] = k[4];
+  p.pad[1] = k[5];
+  p.pad[2] = k[6];
+  p.pad[3] = k[7];
+}
+
+// h = (h + m + 2^128) * r mod 2^130 - 5 for one full 16-byte block.
+__device__ __forceinline__ void poly_block(Poly1305& p, u32x4 m) {
+  uint64_t h0 = p.h0 + (m.x & 0x3ffffffu);
+  uint64_t h1 = p.h1 + (((m.x >> 26) | (m.y << 6)) & 0x3ffffffu);
+  uint64_t h2 = p.h2 + (((m.y >> 20) | (m.z << 12)) & 0x3ffffffu);
+  uint64_t h3 = p.h3 + (((m.z >> 14) | (m.w << 18)) & 0x3ffffffu);
+  uint64_t h4 = p.h4 + ((m.w >> 8) | (1u << 24));
+  const uint32_t s1 = p.r1 * 5u, s2 = p.r2 * 5u, s3 = p.r3 * 5u, s4 = p.r4 * 5u;
+  const uint32_t a0 = (uint32_t)h0, a1 = (uint32_t)h1, a2 = (uint32_t)h2, a3 = (uint32_t)h3,
+                 a4 = (uint32_t)h4;
+  uint64_t d0 = (uint64_t)a0 * p.r0 + (uint64_t)a1 * s4 + (uint64_t)a2 * s3 +
+                (uint64_t)a3 * s2 + (uint64_t)a4 * s1;
+  uint64_t d1 = (uint64_t)a0 * p.r1 + (uint64_t)a1 * p.r0 + (uint64_t)a2 * s4 +
+                (uint64_t)a3 * s3 + (uint64_t)a4 * s2;
+  uint64_t d2 = (uint64_t)a0 * p.r2 + (uint64_t)a1 * p.r1 + (uint64_t)a2 * p.r0 +
+                (uint64_t)a3 * s4 + (uint64_t)a4 * s3;
+  uint64_t d3 = (uint64_t)a0 * p.r3 + (uint64_t)a1 * p.r2 + (uint64_t)a2 * p.r1 +
+                (uint64_t)a3 * p.r0 + (uint64_t)a4 * s4;
+  uint64_t d4 = (uint64_t)a0 * p.r4 + (uint64_t)a1 * p.r3 + (uint64_t)a2 * p.r2 +
+                (uint64_t)a3 * p.r1 + (uint64_t)a4 * p.r0;
+  d1 += d0 >> 26;
+  d2 += d1 >> 26;
+  d3 += d2 >> 26;
+  d4 += d3 >> 26;
+  uint32_t c = (uint32_t)(d4 >> 26);
+  h0 = (d0 & 0x3ffffffu) + (uint64_t)c * 5u;
+  p.h1 = (uint32_t)(d1 & 0x3ffffffu) + (uint32_t)(h0 >> 26);
+  p.h0 = (uint32_t)(h0 & 0x3ffffffu);
+  p.h2 = (uint32_t)(d2 & 0x3ffffffu);
+  p.h3 = (uint32_t)(d3 & 0x3ffffffu);
+  p.h4 = (uint32_t)(d4 & 0x3ffffffu);
+}
+
+// Final reduction + pad; returns the first 12 tag bytes as three words.
+__device__ __forceinline__ void poly_finish(const Poly1305& p, uint32_t (&tag)[3]) {
+  uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
+  c = h1 >> 26; h1 &= 0x3ffffffu;
+  h2 += c; c = h2 >> 26; h2 &= 0x3ffffffu;
+  h3 += c; c = h3 >> 26; h3 &= 0x3ffffffu;
+  h4 += c; c = h4 >> 26; h4 &= 0x3ffffffu;
+  h0 += c * 5u; c = h0 >> 26; h0 &= 0x3ffffffu;
+  h1 += c;
+  // g = h + 5 - 2^130: select g when h >= p
+  uint32_t g0 = h0 + 5u; c = g0 >> 26; g0 &= 0x3ffffffu;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffffu;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffffu;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffffu;
+  uint32_t g4 = h4 + c - (1u << 26);
+  const uint32_t mask = (g4 >> 31) - 1u;  // all ones if h >= p
+  h0 = (h0 & ~mask) | (g0 & mask);
+  h1 = (h1 & ~mask) | (g1 & mask);
+  h2 = (h2 & ~mask) | (g2 & mask);
+  h3 = (h3 & ~mask) | (g3 & mask);
+  h4 = (h4 & ~mask) | (g4 & mask);
+  // to 4 x 32 bits, + pad mod 2^128
+  // (the top word, (h3 >> 18) | (h4 << 8), only feeds tag bytes 12..15: not kept)
+  const uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14);
+  uint64_t f = (uint64_t)w0 + p.pad[0];
+  tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + p.pad[1] + (f >> 32);
+  tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + p.pad[2] + (f >> 32);
+  tag[2] = (uint32_t)f;
+}
+
+// Poly1305 over a per-lane span padded with zeros to 16 (the AD; short).
+__device__ __forceinline__ void poly_span_padded(Poly1305& p, const uint8_t* d, uint32_t len) {
+  const uint32_t nfull = len >> 4;
+  for (uint32_t c = 0; c < nfull; ++c) poly_block(p, ld16(d + 16u * c));
+  const uint32_t rem = len & 15u;
+  if (rem) {
+    uint8_t b[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; ++i) b[i] = i < rem ? d[16u * nfull + i] : (uint8_t)0;
+    u32x4 v;
+    __builtin_memcpy(&v, b, 16);
+    poly_block(p, v);
+  }
+}
+
+// Keep only the `rem` bytes of the tail chunk that load_tail put at its top
+// (len >= 16) or bottom (len < 16), moved to bytes [0, rem), zero above.
+__device__ __forceinline__ u32x4 tail_bytes(u32x4 t, uint32_t len) {
+  const uint32_t rem = len & 15u;
+  uint8_t b[16];
+  __builtin_memcpy(b, &t, 16);
+  const uint32_t first = len >= 16u ? 16u - rem : 0u;
+  uint8_t o[16];
+#pragma unroll
+  for (uint32_t i = 0; i < 16u; ++i) o[i] = i < rem ? b[(first + i) & 15u] : (uint8_t)0;
+  u32x4 v;
+  __builtin_memcpy(&v, o, 16);
+  return v;
+}
+
+__device__ __forceinline__ u32x4 ks_chunk(const uint32_t (&ks)[16], uint32_t j) {
+  return j == 0 ? u32x4{ks[0], ks[1], ks[2], ks[3]}
+         : j == 1 ? u32x4{ks[4], ks[5], ks[6], ks[7]}
+         : j == 2 ? u32x4{ks[8], ks[9], ks[10], ks[11]}
+                  : u32x4{ks[12], ks[13], ks[14], ks[15]};
+}
+
+// Transposed read back of the wave's LDS rows into the loading-lane layout.
+template <uint32_t SC>
+__device__ __forceinline__ void stage_from_lds(const u32x4* rows, uint32_t lane, u32x4 (&v)[SC]) {
+  const uint32_t i = lane / SC, m = lane % SC;
+#pragma unroll
+  for (uint32_t I = 0; I < SC; ++I) v[I] = rows[((64u / SC) * I + i) * (SC + 1u) + m];
+}
+
+__device__ __forceinline__ ChachaKey load_key(const AeadArgs& a, uint64_t p) {
+  ChachaKey key;
+  const uint32_t ki = a.key_idx[p];
+  const uint8_t* kp = a.keys + 32ull * ki;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t w;
+    __builtin_memcpy(&w, kp + 4 * i, 4);
+    key.k[i] = w;
+  }
+  uint32_t pre;
+  __builtin_memcpy(&pre, a.prefixes + 4ull * ki, 4);
+  const uint64_t pn = ((uint64_t)(a.path_id ? a.path_id[p] : 0u) << 56) | a.packet_number[p];
+  key.n[0] = pre;  // nonce = prefix || LE64(path_id << 56 | packet_number)
+  key.n[1] = (uint32_t)pn;
+  key.n[2] = (uint32_t)(pn >> 32);
+  return key;
+}
+
+// Payload pass over the wave's packets: XOR the keystream (XOR = true) and/or
+// MAC (MAC_IN: the MAC covers the input chunks; MAC_OUT: the output chunks)
+// every full chunk; the transformed chunks leave through LDS by coalesced
+// stores when meta[].dst is set.
+template <uint32_t SC, bool XOR, bool MAC_IN, bool MAC_OUT>
+__device__ __forceinline__ void aead_pass(const ChachaKey& key, Poly1305& poly,
+                                          const StageMeta* meta, u32x4* rows, uint32_t lane,
+                                          uint32_t my_nfull, bool store) {
+  const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
+  u32x4 buf[SC];
+  if (nslab) stage_load<SC>(meta, lane, 0, buf);
+  for (uint32_t sl = 0; sl < nslab; ++sl) {
+    stage_to_lds<SC>(rows, lane, buf);
+    if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, buf);  // regs free again
+#pragma unroll
+    for (uint32_t b = 0; b < SC / 4u; ++b) {
+      const uint32_t c0 = sl * SC + 4u * b;
+      if (c0 >= my_nfull) break;
+      uint32_t ks[16];
+      if constexpr (XOR) chacha_block(key, 1u + c0 / 4u, ks);
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        if (c0 + j < my_nfull) {
+          u32x4& slot = rows[lane * (SC + 1u) + 4u * b + j];
+          u32x4 v = slot;
+          if constexpr (MAC_IN) poly_block(poly, v);
+          if constexpr (XOR) {
+            v ^= ks_chunk(ks, j);
+            slot = v;
+          }
+          if constexpr (MAC_OUT) poly_block(poly, v);
+        }
+      }
+    }
+    if (store) {
+      u32x4 out[SC];
+      stage_from_lds<SC>(rows, lane, out);
+      stage_store<SC>(meta, lane, sl, out);
+    }
+  }
+}
+
+__device__ __forceinline__ void poly_lengths(Poly1305& p, uint32_t ad_len, uint32_t ct_len) {
+  poly_block(p, u32x4{ad_len, 0u, ct_len, 0u});  // LE64(ad_len) || LE64(ct_len)
+}
+
+template <uint32_t SC>
+__global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
+  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
+  __shared__ StageMeta s_meta[kWaves][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = p < a.io.n;
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = nullptr;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  ChachaKey key = {};
+  Poly1305 poly = {};
+  u32x4 tail = {0u, 0u, 0u, 0u};
+  if (valid) {
+    ad = a.io.bytes + a.io.ad_off[p];
+    pt = a.io.bytes + a.io.in_off[p];
+    alen = a.io.ad_len[p];
+    plen = a.io.in_len[p];
+    o = a.io.out + a.io.out_off[p];
+    key = load_key(a, p);
+    uint32_t k0[16];
+    chacha_block(key, 0u, k0);  // one-time Poly1305 key (e_chacha20poly1305.c:97-99)
+    poly_init(poly, k0);
+    poly_span_padded(poly, ad, alen);
+    tail = tail_bytes(load_tail(pt, plen), plen);  // before any store (in place)
+  }
+  s_meta[wv][lane] = StageMeta{pt, o, plen >> 4};
+  aead_pass<SC, true, false, true>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
+  if (!valid) return;
+  const uint32_t rem = plen & 15u;
+  if (rem) {
+    const uint32_t c = plen >> 4;
+    uint32_t ks[16];
+    chacha_block(key, 1u + c / 4u, ks);
+    u32x4 ct = tail ^ ks_chunk(ks, c & 3u);
+    uint8_t b[16];
+    __builtin_memcpy(b, &ct, 16);
+    for (uint32_t i = rem; i < 16u; ++i) b[i] = 0;  // zero pad for the MAC
+    __builtin_memcpy(&ct, b, 16);
+    poly_block(poly, ct);
+    for (uint32_t i = 0; i < rem; ++i) o[16u * c + i] = b[i];
+  }
+  poly_lengths(poly, alen, plen);
+  uint32_t tag[3];
+  poly_finish(poly, tag);
+  __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
+}
+
+template <uint32_t SC>
+__global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
+  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
+  __shared__ StageMeta s_meta[kWaves][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t clen = p < a.io.n ? a.io.in_len[p] : 0u;
+  const bool valid = p < a.io.n && clen >= kTag;
+  if (p < a.io.n && !valid) a.io.ok[p] = 0;  // open_impl: in_len < tag_len
+  const uint8_t* ad = nullptr;
+  const uint8_t* ct = nullptr;
+  uint32_t alen = 0, plen = 0;
+  ChachaKey key = {};
+  Poly1305 poly = {};
+  u32x4 tail = {0u, 0u, 0u, 0u};
+  uint32_t want[3] = {0u, 0u, 0u};
+  if (valid) {
+    ad = a.io.bytes + a.io.ad_off[p];
+    ct = a.io.bytes + a.io.in_off[p];
+    alen = a.io.ad_len[p];
+    plen = clen - kTag;
+    __builtin_memcpy(want, ct + plen, kTag);
+    key = load_key(a, p);
+    uint32_t k0[16];
+    chacha_block(key, 0u, k0);
+    poly_init(poly, k0);
+    poly_span_padded(poly, ad, alen);
+    tail = tail_bytes(load_tail(ct, plen), plen);
+  }
+  // pass 1: MAC over the ciphertext (no output)
+  s_meta[wv][lane] = StageMeta{ct, nullptr, plen >> 4};
+  aead_pass<SC, false, true, false>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, false);
+  bool ok = false;
+  if (valid) {
+    if (plen & 15u) poly_block(poly, tail);  // zero padded
+    poly_lengths(poly, alen, plen);
+    uint32_t tag[3];
+    poly_finish(poly, tag);
+    ok = ((tag[0] ^ want[0]) | (tag[1] ^ want[1]) | (tag[2] ^ want[2])) == 0u;
+    a.io.ok[p] = ok ? 1 : 0;
+  }
+  // pass 2 (verified packets only): decrypt into the output
+  uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
+  s_meta[wv][lane] = StageMeta{ct, o, ok ? plen >> 4 : 0u};
+  aead_pass<SC, true, false, false>(key, poly, s_meta[wv], s_rows[wv], lane, ok ? plen >> 4 : 0u,
+                                    true);
+  const uint32_t rem = plen & 15u;
+  if (ok && rem) {
+    const uint32_t c = plen >> 4;
+    uint32_t ks[16];
+    chacha_block(key, 1u + c / 4u, ks);
+    const u32x4 pt = tail ^ ks_chunk(ks, c & 3u);
+    uint8_t b[16];
+    __builtin_memcpy(b, &pt, 16);
+    for (uint32_t i = 0; i < rem; ++i) o[16u * c + i] = b[i];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t s) {
@@ -323,6 +675,38 @@ hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t 
       hipLaunchKernelGGL(null_decrypt_staged_kernel<kSlabChunks>, dim3(blocks), dim3(kBlock), 0, s, a);
     else
       hipLaunchKernelGGL(null_encrypt_staged_kernel<kSlabChunks>, dim3(blocks), dim3(kBlock), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace qfec
+
+namespace qfec {
+
+// AEAD slab: 128 B (8 chunks = 2 ChaCha blocks) per packet per slab — the
+// keystream and MAC state take the registers a 256-B slab buffer would need.
+hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t s) {
+  constexpr uint32_t SC = 8;
+  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
+  for (uint64_t p = 0; p < a0.io.n; p += chunk) {
+    AeadArgs a = a0;
+    a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;
+    a.io.ad_off += p;
+    a.io.ad_len += p;
+    a.io.in_off += p;
+    a.io.in_len += p;
+    a.io.out_off += p;
+    if (decrypt) a.io.ok += p;
+    a.key_idx += p;
+    a.packet_number += p;
+    if (a.path_id) a.path_id += p;
+    const uint32_t blocks = (uint32_t)((a.io.n + kBlock - 1) / kBlock);
+    if (decrypt)
+      hipLaunchKernelGGL(c20p1305_open_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL(c20p1305_seal_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
