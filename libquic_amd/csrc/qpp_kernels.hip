@@ -685,10 +685,11 @@ hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t 
 
 namespace qfec {
 
-// AEAD slab: 128 B (8 chunks = 2 ChaCha blocks) per packet per slab — the
-// keystream and MAC state take the registers a 256-B slab buffer would need.
+// AEAD slab: 256 B (16 chunks = 4 ChaCha blocks) per packet per slab: seal
+// +10%, open +16% over 128-B slabs; 64-B slabs 0.82x
+// (profiles/round1/tune_protect_a4.txt).
 hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t s) {
-  constexpr uint32_t SC = 8;
+  constexpr uint32_t SC = 16;
   const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;

@@ -95,6 +95,40 @@ int main(int argc, char** argv) {
     std::printf("decrypt(encrypt) verified: %llu / %llu\n", (unsigned long long)good,
                 (unsigned long long)n);
   }
+  // ChaCha20-Poly1305: one key, packet numbers 1..n; seal out = ct || tag
+  std::vector<uint8_t> key(32), pre(4);
+  for (int i = 0; i < 32; ++i) key[i] = (uint8_t)(i * 7 + 1);
+  for (int i = 0; i < 4; ++i) pre[i] = (uint8_t)(0xA0 + i);
+  std::vector<uint32_t> kidx(n, 0);
+  std::vector<uint64_t> pns(n);
+  for (uint64_t p = 0; p < n; ++p) pns[p] = p + 1;
+  qfec::AeadArgs as{};
+  as.io = e;
+  as.keys = up(key);
+  as.prefixes = up(pre);
+  as.key_idx = up(kidx);
+  as.packet_number = up(pns);
+  as.path_id = nullptr;
+  CK(qfec::launch_chacha20poly1305(as, false, 0));
+  CK(hipDeviceSynchronize());
+  // open input: [header | ct || tag] records in a buffer of their own
+  uint8_t* d_cat2;
+  CK(hipMalloc(&d_cat2, n * (H + L + 12)));
+  CK(hipMemcpy2D(d_cat2, H + L + 12, d_in, H + L, H, n, hipMemcpyDeviceToDevice));
+  CK(hipMemcpy2D(d_cat2 + H, H + L + 12, d_out, L + 12, L + 12, n, hipMemcpyDeviceToDevice));
+  qfec::AeadArgs ao = as;
+  ao.io = d;
+  ao.io.bytes = d_cat2;
+  CK(qfec::launch_chacha20poly1305(ao, true, 0));
+  CK(hipDeviceSynchronize());
+  {
+    std::vector<uint8_t> ok(n);
+    CK(hipMemcpy(ok.data(), d_ok, n, hipMemcpyDeviceToHost));
+    uint64_t good = 0;
+    for (auto v : ok) good += v;
+    std::printf("chacha20poly1305 open(seal) verified: %llu / %llu\n", (unsigned long long)good,
+                (unsigned long long)n);
+  }
   uint32_t* sink;
   CK(hipMalloc(&sink, 4));
   struct V {
@@ -109,6 +143,14 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"null encrypt staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(e, false, 0)); }},
       {"null decrypt staged (product)", dec_b, hashed, [&] { CK(qfec::launch_null_protect(d, true, 0)); }},
+      {"chacha20poly1305 seal (product)", enc_b, hashed, [&] { CK(qfec::launch_chacha20poly1305(as, false, 0)); }},
+      {"chacha20poly1305 open (product)", dec_b, hashed, [&] { CK(qfec::launch_chacha20poly1305(ao, true, 0)); }},
+      {"chacha20poly1305 seal SC=16", enc_b, hashed, [&] {
+         hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<16>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
+      {"chacha20poly1305 open SC=16", dec_b, hashed, [&] {
+         hipLaunchKernelGGL(qfec::c20p1305_open_kernel<16>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, ao); }},
+      {"chacha20poly1305 seal SC=4", enc_b, hashed, [&] {
+         hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<4>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
       {"null encrypt staged SC=4", enc_b, hashed, [&] {
          hipLaunchKernelGGL(qfec::null_encrypt_staged_kernel<4>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
       {"null encrypt staged SC=8", enc_b, hashed, [&] {
