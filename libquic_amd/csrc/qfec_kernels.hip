@@ -332,31 +332,69 @@ __device__ __forceinline__ u32x4 packet_window(const uint8_t* row, uint32_t len,
   return window16_small(row, len, 0u);  // t == 0 (rare: packets below 16 B)
 }
 
-template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1>
-__global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
-  __shared__ uint32_t s_par[WAVES][4 * kParWin];
-  __shared__ uint64_t s_head[WAVES][kParWin];
-  __shared__ u32x4 s_meta[WAVES][64];
-  const uint32_t lane = lane_id();
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
-  if (g >= a.n_groups) return;
-  uint32_t* par = s_par[wv];
-  uint64_t* head = s_head[wv];
-  u32x4* meta = s_meta[wv];
+// Per-group inputs a wave can fetch one group ahead: the group scalars and,
+// for the first 64 received packets, lane r's packet length / offset (and for
+// recover the parity row's two windows per lane).
+struct GroupPrefetch {
+  uint32_t p0, k, m, plen;       // wave-uniform
+  uint64_t dst_off;              // parity_off (encode) / out_off (recover)
+  uint32_t len, offlo, offhi;    // lane r = received packet r (r < 64)
+  u32x4 pw0, pw1;                // recover: parity windows lane, lane + 64
+};
 
-  const uint32_t p0 = a.grp_ptr[g];
-  const uint32_t p1 = a.grp_ptr[g + 1];
-  const uint32_t k = p1 - p0;
-  if (p1 < p0 || k == 0u || k > 255u) {
+template <bool RECOVER>
+__device__ __forceinline__ void group_scalars(const RaggedArgs& a, uint64_t g, GroupPrefetch& f) {
+  f.p0 = a.grp_ptr[g];
+  f.k = a.grp_ptr[g + 1] - f.p0;
+  f.m = 0xFFFFFFFFu;
+  f.plen = 0;
+  if constexpr (RECOVER) {
+    f.m = a.missing[g];
+    f.plen = a.parity_len[g];
+    f.dst_off = a.out_off[g];
+  } else {
+    f.dst_off = a.parity_off[g];
+  }
+}
+
+// Vector part (needs the scalars).  Invalid groups load nothing.
+template <bool RECOVER, bool NT>
+__device__ __forceinline__ void group_vectors(const RaggedArgs& a, uint64_t g, uint32_t lane,
+                                              GroupPrefetch& f) {
+  f.len = f.offlo = f.offhi = 0;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  f.pw0 = f.pw1 = zero;
+  const bool ok = f.k >= 1u && f.k <= 255u && (!RECOVER || (f.m < f.k && f.plen >= 1u &&
+                                                             f.plen <= kMaxPacket));
+  if (!ok) return;
+  const uint32_t kr = RECOVER ? f.k - 1u : f.k;
+  if (lane < kr) {
+    const uint32_t p = f.p0 + lane + (lane >= f.m ? 1u : 0u);
+    f.len = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    f.offlo = (uint32_t)o;
+    f.offhi = (uint32_t)(o >> 32);
+  }
+  if constexpr (RECOVER) {
+    const uint8_t* prow = a.parity + a.parity_off[g];
+    if (16u * lane < f.plen) f.pw0 = packet_window<NT>(prow, f.plen, lane);
+    if (16u * (lane + 64u) < f.plen) f.pw1 = packet_window<NT>(prow, f.plen, lane + 64u);
+  }
+}
+
+// One group, one wave (see the flat-window description above).
+template <bool RECOVER, bool NT, int U, int ACC>
+__device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
+                                             const GroupPrefetch& f, uint32_t* par,
+                                             uint64_t* head, u32x4* meta) {
+  const uint32_t p0 = f.p0, k = f.k, m = f.m;
+  uint32_t plen = f.plen;
+  if (k == 0u || k > 255u) {  // grp_ptr not monotone shows up as k > 255 too
     if (lane == 0) atomicOr(a.err, kErrGroupSize);
     return;
   }
-  uint32_t m = 0xFFFFFFFFu, plen = 0;
   const u32x4 zero = {0u, 0u, 0u, 0u};
   if constexpr (RECOVER) {
-    m = a.missing[g];
-    plen = a.parity_len[g];
     if (m >= k) {
       if (lane == 0) atomicOr(a.err, kErrMissingIndex);
       return;
@@ -365,10 +403,9 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
       if (lane == 0) atomicOr(a.err, kErrParityLength);
       return;
     }
-    // accumulator := the parity row (zero past plen)
-    const uint8_t* prow = a.parity + a.parity_off[g];
-    for (uint32_t t = lane; t < kParWin; t += 64u)
-      lds_put16<ACC>(par, t, 16u * t < plen ? packet_window<NT>(prow, plen, t) : zero);
+    // accumulator := the parity row (zero past plen), prefetched windows
+    lds_put16<ACC>(par, lane, f.pw0);
+    if (lane + 64u < kParWin) lds_put16<ACC>(par, lane + 64u, f.pw1);
   } else {
     for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(par, t, zero);
   }
@@ -378,13 +415,16 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   for (uint32_t c = 0; c < kr; c += 64u) {
     // packet table of this chunk: lane j = received packet c + j
     const uint32_t r = c + lane;
-    uint32_t len = 0, offlo = 0, offhi = 0;
-    if (r < kr) {
-      const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
-      len = a.pkt_len[p];
-      const uint64_t o = a.pkt_off[p];
-      offlo = (uint32_t)o;
-      offhi = (uint32_t)(o >> 32);
+    uint32_t len = f.len, offlo = f.offlo, offhi = f.offhi;
+    if (c > 0) {  // groups of more than 64 received packets: load inline
+      len = offlo = offhi = 0;
+      if (r < kr) {
+        const uint32_t p = p0 + r + (r >= m ? 1u : 0u);
+        len = a.pkt_len[p];
+        const uint64_t o = a.pkt_off[p];
+        offlo = (uint32_t)o;
+        offhi = (uint32_t)(o >> 32);
+      }
     }
     const bool bad = r < kr && (len == 0u || len > lim);
     if (wave_any(bad)) {
@@ -428,13 +468,13 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
         uint32_t tt[U], sh[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t f = 64u * (it + u) + lane;
-          const uint32_t win = 16u * (f - md[u].w);
+          const uint32_t fl = 64u * (it + u) + lane;
+          const uint32_t win = 16u * (fl - md[u].w);
           const bool full = win + 16u <= md[u].z;
           v[u] = ld16t<NT>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) +
                            (full ? win : md[u].z - 16u));
           sh[u] = full ? 0u : min(win + 16u - md[u].z, 15u);
-          tt[u] = f < W ? f - md[u].w : 0xFFFFFFFFu;
+          tt[u] = fl < W ? fl - md[u].w : 0xFFFFFFFFu;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -444,12 +484,12 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
       // Some packet below 16 B (rare): generic per-lane windows.
       for (uint32_t it = 0; it < nit; ++it) {
         const uint64_t M = head[it];
-        const uint32_t f = 64u * it + lane;
+        const uint32_t fl = 64u * it + lane;
         const uint32_t pi = min(before + (uint32_t)__popcll(M & below) - 1u, last);
         before += (uint32_t)__popcll(M);
-        if (f < W) {
+        if (fl < W) {
           const u32x4 md = meta[pi];
-          const uint32_t t = f - md.w;
+          const uint32_t t = fl - md.w;
           lds_xor16<ACC>(par, t, packet_window<false>(a.bytes + (((uint64_t)md.y << 32) | md.x),
                                                   md.z, t));
         }
@@ -460,7 +500,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
     plen = wave_max11(mx);
     if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
   }
-  uint8_t* dst = a.out + (RECOVER ? a.out_off[g] : a.parity_off[g]);
+  uint8_t* dst = a.out + f.dst_off;
   if (plen >= 16u) {
     const uint32_t nw = (plen + 15u) >> 4;
     for (uint32_t t = lane; t < nw; t += 64u) {
@@ -486,6 +526,22 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   } else if (lane < plen) {
     dst[lane] = (uint8_t)(par[acc_idx<ACC>(0, lane >> 2)] >> (8u * (lane & 3u)));
   }
+}
+
+// One short-lived wave per group.
+template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1>
+__global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[WAVES][4 * kParWin];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
+  if (g >= a.n_groups) return;
+  GroupPrefetch f;
+  group_scalars<RECOVER>(a, g, f);
+  group_vectors<RECOVER, NT>(a, g, lane, f);
+  ragged_group<RECOVER, NT, U, ACC>(a, g, lane, f, s_par[wv], s_head[wv], s_meta[wv]);
 }
 
 // ---------------------------------------------------------------------------

@@ -6,6 +6,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_ragged.hip -o tools/tune/build/tune_ragged
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
 #include "prev_ragged.inc"
+#include "pipe_ragged.inc"
 
 #include <algorithm>
 #include <cstring>
@@ -136,20 +137,17 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, false>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
                     }});
-#define TV(NAME, U, W, ACC)                                                                 \
+#define TP(NAME, GRID)                                                                      \
   vs.push_back({NAME, s.l.alg, [=] {                                                        \
-                  hipLaunchKernelGGL((qfec::ragged_xor_kernel<false, true, U, W, ACC>),       \
-                                     dim3((uint32_t)((G + W - 1) / W)), dim3(64 * W), 0, 0, a); \
+                  hipLaunchKernelGGL((qfec::ragged_pipe_kernel<false, true>), dim3(GRID),     \
+                                     dim3(256), 0, 0, a);                                    \
                 }});
-      TV("flat U1 W4 cm", 1, 4, 1)
-      TV("flat U2 W4 cm", 2, 4, 1)
-      TV("flat U4 W4 cm", 4, 4, 1)
-      TV("flat U2 W4 il", 2, 4, 0)
-      TV("flat U4 W4 il", 4, 4, 0)
-      TV("flat U2 W2 cm", 2, 2, 1)
-      TV("flat U2 W8 cm", 2, 8, 1)
-      TV("flat U2 W1 cm", 2, 1, 1)
-#undef TV
+      TP("pipe grid 1024", 1024)
+      TP("pipe grid 2048", 2048)
+      TP("pipe grid 4096", 4096)
+      TP("pipe grid 8192", 8192)
+      TP("pipe grid 16384", 16384)
+#undef TP
       vs.push_back({"prev (2 fixed windows/lane, nt) " + s.name, s.l.alg, [=] {
                       hipLaunchKernelGGL((qfec::prev_ragged_xor_kernel<false, true>),
                                          dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
