@@ -107,6 +107,21 @@ def lib():
         L.qo_quic_c20p1305_decrypt_batch.restype = None
         L.qo_quic_c20p1305_decrypt_batch.argtypes = [C.c_void_p] * 10 + [C.c_uint64, C.c_void_p,
                                                                         C.c_void_p, C.c_void_p]
+        # AES-128-GCM
+        L.qo_aes128_expand.restype = None
+        L.qo_aes128_expand.argtypes = [C.c_void_p, C.c_void_p]
+        L.qo_aes128_encrypt.restype = None
+        L.qo_aes128_encrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        for fn in (L.qo_aes128gcm_seal, L.qo_aes128gcm_open):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                           C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t]
+        L.qo_quic_aes128gcm_encrypt_batch.restype = None
+        L.qo_quic_aes128gcm_encrypt_batch.argtypes = [C.c_void_p] * 10 + [
+            C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.qo_quic_aes128gcm_decrypt_batch.restype = None
+        L.qo_quic_aes128gcm_decrypt_batch.argtypes = [C.c_void_p] * 10 + [
+            C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -308,6 +323,52 @@ def quic_c20p1305_decrypt_batch(keys, prefixes, key_idx, packet_number, path_id,
     out = np.zeros(out_size, np.uint8)
     ok = np.zeros(ct_len.size, np.uint8)
     lib().qo_quic_c20p1305_decrypt_batch(
+        _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
+        None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(ct_off),
+        _p(ct_len), ct_len.size, _p(out), _p(out_off), _p(ok))
+    return out, ok
+
+
+# ---- AES-128-GCM (qaead_oracle.h) ------------------------------------------
+def aes128_encrypt(key, block):
+    k, b = _buf(key), _buf(block)
+    rk = np.zeros(44, np.uint32)
+    lib().qo_aes128_expand(_p(rk), _p(k))
+    out = np.zeros(16, np.uint8)
+    lib().qo_aes128_encrypt(_p(out), _p(b), _p(rk))
+    return out
+
+
+def aes128gcm_seal(key, iv, pt, ad, tag_len=16):
+    k, n, p, a = _buf(key), _buf(iv), _buf(pt), _buf(ad)
+    out = np.zeros(p.size + tag_len, np.uint8)
+    lib().qo_aes128gcm_seal(_p(out), _p(k), _p(n), n.size, _pn(p), p.size, _pn(a), a.size, tag_len)
+    return out
+
+
+def aes128gcm_open(key, iv, ct, ad, tag_len=16):
+    k, n, c, a = _buf(key), _buf(iv), _buf(ct), _buf(ad)
+    out = np.zeros(max(c.size - tag_len, 0) + 1, np.uint8)
+    ok = lib().qo_aes128gcm_open(_p(out), _p(k), _p(n), n.size, _pn(c), c.size, _pn(a), a.size,
+                                 tag_len)
+    return bool(ok), out[:max(c.size - tag_len, 0)]
+
+
+def quic_aes128gcm_encrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                                 ad_len, pt_off, pt_len, out_off, out_size, threads=1):
+    out = np.zeros(out_size, np.uint8)
+    lib().qo_quic_aes128gcm_encrypt_batch(
+        _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
+        None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(pt_off),
+        _p(pt_len), pt_len.size, _p(out), _p(out_off), threads)
+    return out
+
+
+def quic_aes128gcm_decrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                                 ad_len, ct_off, ct_len, out_off, out_size):
+    out = np.zeros(out_size, np.uint8)
+    ok = np.zeros(ct_len.size, np.uint8)
+    lib().qo_quic_aes128gcm_decrypt_batch(
         _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
         None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(ct_off),
         _p(ct_len), ct_len.size, _p(out), _p(out_off), _p(ok))

@@ -264,3 +264,244 @@ void qo_quic_c20p1305_decrypt_batch(const uint8_t* keys, const uint8_t* prefixes
                                               bytes + in_off[p], in_len[p]);
   }
 }
+
+/* ======================================================================== */
+/* AES-128 (FIPS-197 §5.1-5.2), byte-oriented                                */
+/* ======================================================================== */
+static uint8_t g_sbox[256];
+static int g_sbox_ready = 0;
+
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return r;
+}
+
+/* S-box from its definition: multiplicative inverse in GF(2^8) + affine map */
+static void sbox_init(void) {
+  if (g_sbox_ready) return;
+  for (int x = 0; x < 256; ++x) {
+    uint8_t inv = 0;
+    for (int y = 1; y < 256 && x; ++y)
+      if (gf_mul((uint8_t)x, (uint8_t)y) == 1) { inv = (uint8_t)y; break; }
+    uint8_t s = inv;
+    for (int i = 1; i < 5; ++i) s ^= (uint8_t)((inv << i) | (inv >> (8 - i)));
+    g_sbox[x] = (uint8_t)(s ^ 0x63);
+  }
+  g_sbox_ready = 1;
+}
+
+void qo_aes128_expand(uint32_t rk[44], const uint8_t key[16]) {
+  sbox_init();
+  /* words big-endian as FIPS-197 (w[i] = key[4i..4i+3]) */
+  for (int i = 0; i < 4; ++i)
+    rk[i] = (uint32_t)key[4 * i] << 24 | (uint32_t)key[4 * i + 1] << 16 |
+            (uint32_t)key[4 * i + 2] << 8 | key[4 * i + 3];
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; ++i) {
+    uint32_t t = rk[i - 1];
+    if (i % 4 == 0) {
+      t = (t << 8) | (t >> 24); /* RotWord */
+      t = (uint32_t)g_sbox[t >> 24] << 24 | (uint32_t)g_sbox[(t >> 16) & 0xff] << 16 |
+          (uint32_t)g_sbox[(t >> 8) & 0xff] << 8 | g_sbox[t & 0xff];
+      t ^= (uint32_t)rcon << 24;
+      rcon = gf_mul(rcon, 2);
+    }
+    rk[i] = rk[i - 4] ^ t;
+  }
+}
+
+void qo_aes128_encrypt(uint8_t out[16], const uint8_t in[16], const uint32_t rk[44]) {
+  sbox_init();
+  uint8_t s[16];
+  for (int i = 0; i < 16; ++i) s[i] = in[i] ^ (uint8_t)(rk[i / 4] >> (24 - 8 * (i % 4)));
+  for (int r = 1; r <= 10; ++r) {
+    uint8_t t[16];
+    for (int i = 0; i < 16; ++i) t[i] = g_sbox[s[i]];             /* SubBytes */
+    for (int c = 0; c < 4; ++c)                                       /* ShiftRows */
+      for (int rr = 0; rr < 4; ++rr) s[4 * c + rr] = t[4 * ((c + rr) % 4) + rr];
+    if (r != 10) {                                                    /* MixColumns */
+      for (int c = 0; c < 4; ++c) {
+        const uint8_t a0 = s[4 * c], a1 = s[4 * c + 1], a2 = s[4 * c + 2], a3 = s[4 * c + 3];
+        s[4 * c] = gf_mul(a0, 2) ^ gf_mul(a1, 3) ^ a2 ^ a3;
+        s[4 * c + 1] = a0 ^ gf_mul(a1, 2) ^ gf_mul(a2, 3) ^ a3;
+        s[4 * c + 2] = a0 ^ a1 ^ gf_mul(a2, 2) ^ gf_mul(a3, 3);
+        s[4 * c + 3] = gf_mul(a0, 3) ^ a1 ^ a2 ^ gf_mul(a3, 2);
+      }
+    }
+    for (int i = 0; i < 16; ++i) s[i] ^= (uint8_t)(rk[4 * r + i / 4] >> (24 - 8 * (i % 4)));
+  }
+  memcpy(out, s, 16);
+}
+
+/* ======================================================================== */
+/* GCM (SP 800-38D §6.3-7): bitwise GF(2^128) multiply, Algorithm 1          */
+/* ======================================================================== */
+static void gf128_mul(uint8_t x[16], const uint8_t h[16]) {
+  uint8_t z[16] = {0}, v[16];
+  memcpy(v, h, 16);
+  for (int i = 0; i < 128; ++i) {
+    if (x[i / 8] & (0x80 >> (i % 8)))
+      for (int j = 0; j < 16; ++j) z[j] ^= v[j];
+    const int lsb = v[15] & 1;
+    for (int j = 15; j > 0; --j) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
+    v[0] >>= 1;
+    if (lsb) v[0] ^= 0xe1;
+  }
+  memcpy(x, z, 16);
+}
+
+static void ghash_update(uint8_t y[16], const uint8_t h[16], const uint8_t* d, size_t len) {
+  for (; len > 0;) {
+    const size_t n = len < 16 ? len : 16;
+    for (size_t i = 0; i < n; ++i) y[i] ^= d[i]; /* zero padded block */
+    gf128_mul(y, h);
+    d += n; len -= n;
+  }
+}
+
+static void inc32(uint8_t ctr[16]) {
+  for (int i = 15; i >= 12; --i)
+    if (++ctr[i]) break;
+}
+
+static void gcm_core(uint8_t tag[16], uint8_t* out, const uint8_t key[16], const uint8_t* iv,
+                     size_t iv_len, const uint8_t* in, size_t in_len, const uint8_t* ad,
+                     size_t ad_len, int decrypt) {
+  uint32_t rk[44];
+  qo_aes128_expand(rk, key);
+  uint8_t h[16] = {0}, j0[16] = {0}, y[16] = {0};
+  qo_aes128_encrypt(h, h, rk);
+  if (iv_len == 12) {
+    memcpy(j0, iv, 12);
+    j0[15] = 1;
+  } else {
+    ghash_update(j0, h, iv, iv_len);
+    uint8_t lb[16] = {0};
+    st64(lb + 8, 0);
+    const uint64_t bits = (uint64_t)iv_len * 8;
+    for (int i = 0; i < 8; ++i) lb[15 - i] = (uint8_t)(bits >> (8 * i));
+    ghash_update(j0, h, lb, 16);
+  }
+  ghash_update(y, h, ad, ad_len);
+  /* GCTR from inc32(J0); MAC over the ciphertext */
+  uint8_t ctr[16], ks[16];
+  memcpy(ctr, j0, 16);
+  const uint8_t* src = in;
+  for (size_t off = 0; off < in_len; off += 16) {
+    inc32(ctr);
+    qo_aes128_encrypt(ks, ctr, rk);
+    const size_t n = in_len - off < 16 ? in_len - off : 16;
+    if (out)
+      for (size_t i = 0; i < n; ++i) out[off + i] = src[off + i] ^ ks[i];
+  }
+  ghash_update(y, h, decrypt ? in : out, in_len);
+  uint8_t lens[16];
+  const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)in_len * 8;
+  for (int i = 0; i < 8; ++i) {
+    lens[7 - i] = (uint8_t)(ab >> (8 * i));
+    lens[15 - i] = (uint8_t)(cb >> (8 * i));
+  }
+  ghash_update(y, h, lens, 16);
+  qo_aes128_encrypt(ks, j0, rk);
+  for (int i = 0; i < 16; ++i) tag[i] = y[i] ^ ks[i];
+}
+
+int qo_aes128gcm_seal(uint8_t* out, const uint8_t key[16], const uint8_t* iv, size_t iv_len,
+                      const uint8_t* in, size_t in_len, const uint8_t* ad, size_t ad_len,
+                      size_t tag_len) {
+  uint8_t tag[16];
+  gcm_core(tag, out, key, iv, iv_len, in, in_len, ad, ad_len, 0);
+  memcpy(out + in_len, tag, tag_len);
+  return 1;
+}
+
+int qo_aes128gcm_open(uint8_t* out, const uint8_t key[16], const uint8_t* iv, size_t iv_len,
+                      const uint8_t* in, size_t in_len, const uint8_t* ad, size_t ad_len,
+                      size_t tag_len) {
+  if (in_len < tag_len) return 0;
+  const size_t pt_len = in_len - tag_len;
+  uint8_t tag[16];
+  gcm_core(tag, NULL, key, iv, iv_len, in, pt_len, ad, ad_len, 1); /* MAC only */
+  uint8_t diff = 0;
+  for (size_t i = 0; i < tag_len; ++i) diff |= (uint8_t)(tag[i] ^ in[pt_len + i]);
+  if (diff) return 0;
+  gcm_core(tag, out, key, iv, iv_len, in, pt_len, ad, ad_len, 1);
+  return 1;
+}
+
+struct gcm_job {
+  const uint8_t *keys, *prefixes, *path_id, *bytes;
+  const uint32_t* key_idx;
+  const uint64_t *packet_number, *ad_off, *in_off, *out_off;
+  const uint16_t *ad_len, *in_len;
+  uint8_t* out;
+  uint8_t* ok;
+  uint64_t p0, p1;
+};
+
+static void* gcm_worker(void* arg) {
+  const struct gcm_job* j = (const struct gcm_job*)arg;
+  for (uint64_t p = j->p0; p < j->p1; ++p) {
+    const uint32_t k = j->key_idx[p];
+    uint8_t nonce[12];
+    quic_nonce(nonce, j->prefixes + 4ull * k, j->path_id ? j->path_id[p] : 0,
+               j->packet_number[p]);
+    if (j->ok)
+      j->ok[p] = (uint8_t)qo_aes128gcm_open(j->out + j->out_off[p], j->keys + 16ull * k, nonce,
+                                            12, j->bytes + j->in_off[p], j->in_len[p],
+                                            j->bytes + j->ad_off[p], j->ad_len[p],
+                                            QO_QUIC_AEAD_TAG);
+    else
+      qo_aes128gcm_seal(j->out + j->out_off[p], j->keys + 16ull * k, nonce, 12,
+                        j->bytes + j->in_off[p], j->in_len[p], j->bytes + j->ad_off[p],
+                        j->ad_len[p], QO_QUIC_AEAD_TAG);
+  }
+  return NULL;
+}
+
+static void gcm_batch(const uint8_t* keys, const uint8_t* prefixes, const uint32_t* key_idx,
+                      const uint64_t* packet_number, const uint8_t* path_id,
+                      const uint8_t* bytes, const uint64_t* ad_off, const uint16_t* ad_len,
+                      const uint64_t* in_off, const uint16_t* in_len, uint64_t n, uint8_t* out,
+                      const uint64_t* out_off, uint8_t* ok, int threads) {
+  sbox_init();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  struct gcm_job jobs[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (struct gcm_job){keys, prefixes, path_id, bytes, key_idx, packet_number, ad_off,
+                               in_off, out_off, ad_len, in_len, out, ok,
+                               n * (uint64_t)t / (uint64_t)threads,
+                               n * (uint64_t)(t + 1) / (uint64_t)threads};
+    if (threads == 1) gcm_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, gcm_worker, &jobs[t]);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+}
+
+void qo_quic_aes128gcm_encrypt_batch(const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len, uint64_t n,
+                                     uint8_t* out, const uint64_t* out_off, int threads) {
+  gcm_batch(keys, prefixes, key_idx, packet_number, path_id, bytes, ad_off, ad_len, in_off,
+            in_len, n, out, out_off, NULL, threads);
+}
+
+void qo_quic_aes128gcm_decrypt_batch(const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len, uint64_t n,
+                                     uint8_t* out, const uint64_t* out_off, uint8_t* ok) {
+  gcm_batch(keys, prefixes, key_idx, packet_number, path_id, bytes, ad_off, ad_len, in_off,
+            in_len, n, out, out_off, ok, 1);
+}

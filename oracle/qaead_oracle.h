@@ -25,10 +25,20 @@
  *                         nonce = prefix(4) || LE64(path_id << 56 | packet_number)
  *                         (QuicUtils::PackPathIdAndPacketNumber quic_utils.cc:465-475)
  *
+ *   qo_aes128_*           AES-128 (FIPS-197) as AES_set_encrypt_key / AES_encrypt,
+ *                         boringssl/crypto/aes/aes.c (C build)
+ *   qo_aes128gcm_seal/open  aead_aes_gcm_seal / _open,
+ *                         boringssl/crypto/cipher/e_aes.c:1050-1140 over
+ *                         CRYPTO_gcm128_* (boringssl/crypto/modes/gcm.c):
+ *                         SP 800-38D GCM, any IV length, tag truncated to tag_len
+ *   qo_quic_aes128gcm_*   Aes128Gcm12Encrypter / Decrypter
+ *                         (crypto/aes_128_gcm_12_encrypter.cc: 16-byte key, 4-byte
+ *                         nonce prefix, kAuthTagSize = 12) via AeadBaseEncrypter
+ *
  * PINNED by BoringSSL's own test vectors in the reference tree
- * (boringssl/crypto/cipher/test/chacha20_poly1305_tests.txt ->
- * tests/golden/chacha20_poly1305.npz, tests/golden/make_golden_aead.py) and,
- * for the primitives, by the reference's chacha.c / poly1305_vec.c compiled
+ * (boringssl/crypto/cipher/test/{chacha20_poly1305,aes_128_gcm}_tests.txt ->
+ * tests/golden/{chacha20_poly1305,aes_128_gcm}.npz, tests/golden/make_golden_aead.py)
+ * and by the reference's chacha.c / poly1305_vec.c / aes.c / gcm.c compiled
  * into oracle/_ref/libref_quic.so (oracle/ref/Makefile).  The AEAD glue
  * (e_chacha20poly1305.c) and AeadBaseEncrypter link BoringSSL's generated
  * err_data.c, which needs Go: not buildable here, restated.
@@ -83,6 +93,30 @@ void qo_quic_c20p1305_decrypt_batch(const uint8_t* keys, const uint8_t* prefixes
                                     const uint64_t* ad_off, const uint16_t* ad_len,
                                     const uint64_t* in_off, const uint16_t* in_len, uint64_t n,
                                     uint8_t* out, const uint64_t* out_off, uint8_t* ok);
+
+/* ---- AES-128-GCM ---- */
+#define QO_AES128_KEY 16u
+void qo_aes128_expand(uint32_t rk[44], const uint8_t key[16]);
+void qo_aes128_encrypt(uint8_t out[16], const uint8_t in[16], const uint32_t rk[44]);
+int qo_aes128gcm_seal(uint8_t* out, const uint8_t key[16], const uint8_t* iv, size_t iv_len,
+                      const uint8_t* in, size_t in_len, const uint8_t* ad, size_t ad_len,
+                      size_t tag_len);
+int qo_aes128gcm_open(uint8_t* out, const uint8_t key[16], const uint8_t* iv, size_t iv_len,
+                      const uint8_t* in, size_t in_len, const uint8_t* ad, size_t ad_len,
+                      size_t tag_len);
+/* Batches (keys: 16 B each, prefixes: 4 B each; as the ChaCha20 forms). */
+void qo_quic_aes128gcm_encrypt_batch(const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len, uint64_t n,
+                                     uint8_t* out, const uint64_t* out_off, int threads);
+void qo_quic_aes128gcm_decrypt_batch(const uint8_t* keys, const uint8_t* prefixes,
+                                     const uint32_t* key_idx, const uint64_t* packet_number,
+                                     const uint8_t* path_id, const uint8_t* bytes,
+                                     const uint64_t* ad_off, const uint16_t* ad_len,
+                                     const uint64_t* in_off, const uint16_t* in_len, uint64_t n,
+                                     uint8_t* out, const uint64_t* out_off, uint8_t* ok);
 
 #ifdef __cplusplus
 }

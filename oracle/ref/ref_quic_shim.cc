@@ -13,8 +13,10 @@
 #include "net/quic/core/quic_utils.h"
 
 extern "C" {
+#include <openssl/aes.h>
 #include <openssl/chacha.h>
 #include <openssl/poly1305.h>
+#include "modes/internal.h"  // CRYPTO_gcm128_* (boringssl/crypto/modes)
 }
 
 #define REF_API extern "C" __attribute__((visibility("default")))
@@ -63,4 +65,28 @@ REF_API void ref_poly1305(uint8_t* tag, const uint8_t* msg, size_t len, const ui
   CRYPTO_poly1305_update(&st, msg, split);
   CRYPTO_poly1305_update(&st, msg + split, len - split);
   CRYPTO_poly1305_finish(&st, tag);
+}
+
+// BoringSSL AES_set_encrypt_key + AES_encrypt (boringssl/crypto/aes/aes.c)
+REF_API void ref_aes128_encrypt(uint8_t* out, const uint8_t* in, const uint8_t* key) {
+  AES_KEY ks;
+  AES_set_encrypt_key(key, 128, &ks);
+  AES_encrypt(in, out, &ks);
+}
+
+// What aead_aes_gcm_seal (boringssl/crypto/cipher/e_aes.c:1050-1091) does,
+// over the reference's own GCM mode functions (crypto/modes/gcm.c):
+// setiv, aad, encrypt, tag(tag_len).  Returns 1.
+REF_API int ref_aes128gcm_seal(uint8_t* out, const uint8_t* key, const uint8_t* iv, size_t iv_len,
+                               const uint8_t* in, size_t in_len, const uint8_t* ad,
+                               size_t ad_len, size_t tag_len) {
+  AES_KEY ks;
+  AES_set_encrypt_key(key, 128, &ks);
+  GCM128_CONTEXT gcm;
+  CRYPTO_gcm128_init(&gcm, &ks, (block128_f)AES_encrypt);
+  CRYPTO_gcm128_setiv(&gcm, &ks, iv, iv_len);
+  if (ad_len > 0 && !CRYPTO_gcm128_aad(&gcm, ad, ad_len)) return 0;
+  if (!CRYPTO_gcm128_encrypt(&gcm, &ks, in, out, in_len)) return 0;
+  CRYPTO_gcm128_tag(&gcm, out + in_len, tag_len);
+  return 1;
 }

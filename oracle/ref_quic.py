@@ -47,6 +47,12 @@ def lib():
                                    C.c_uint32]
         L.ref_poly1305.restype = None
         L.ref_poly1305.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.ref_aes128_encrypt.restype = None
+        L.ref_aes128_encrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ref_aes128gcm_seal.restype = C.c_int
+        L.ref_aes128gcm_seal.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                         C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                         C.c_size_t]
         _lib = L
     return _lib
 
@@ -108,3 +114,21 @@ def poly1305(key, msg, split=0):
     tag = np.zeros(16, np.uint8)
     lib().ref_poly1305(tag.ctypes.data_as(C.c_void_p), _ptr(m), m.size, _ptr(k), split)
     return tag
+
+
+def aes128_encrypt(key, block):
+    """BoringSSL AES_set_encrypt_key + AES_encrypt (aes.c)."""
+    k, b = _b(key), _b(block)
+    out = np.zeros(16, np.uint8)
+    lib().ref_aes128_encrypt(out.ctypes.data_as(C.c_void_p), _ptr(b), _ptr(k))
+    return out
+
+
+def aes128gcm_seal(key, iv, pt, ad, tag_len=16):
+    """aead_aes_gcm_seal's sequence over BoringSSL's CRYPTO_gcm128_* (gcm.c)."""
+    k, n, p, a = _b(key), _b(iv), _b(pt), _b(ad)
+    out = np.zeros(p.size + tag_len, np.uint8)
+    ok = lib().ref_aes128gcm_seal(out.ctypes.data_as(C.c_void_p), _ptr(k), _ptr(n), n.size, _ptr(p),
+                                  p.size, _ptr(a), a.size, tag_len)
+    assert ok
+    return out

@@ -1,7 +1,8 @@
-"""Convert BoringSSL's ChaCha20-Poly1305 test vectors — data files in the
-reference tree (/root/reference/boringssl/crypto/cipher/test/
-chacha20_poly1305_tests.txt: RFC 7539 §2.8.2 and A.5 plus BoringSSL's own
-cases, tags truncated to 1..16 bytes) — into tests/golden/chacha20_poly1305.npz.
+"""Convert BoringSSL's AEAD test vectors — data files in the reference tree
+(/root/reference/boringssl/crypto/cipher/test/chacha20_poly1305_tests.txt:
+RFC 7539 §2.8.2 and A.5 plus BoringSSL's own cases, tags truncated to 1..16
+bytes; aes_128_gcm_tests.txt: the GCM spec / NIST cases, 8..64-byte IVs) —
+into tests/golden/{chacha20_poly1305,aes_128_gcm}.npz.
 Run in the container that has /root/reference:
     python tests/golden/make_golden_aead.py
 """
@@ -10,8 +11,10 @@ import sys
 
 import numpy as np
 
-SRC = "/root/reference/boringssl/crypto/cipher/test/chacha20_poly1305_tests.txt"
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "chacha20_poly1305.npz")
+TESTS = "/root/reference/boringssl/crypto/cipher/test/"
+HERE = os.path.dirname(os.path.abspath(__file__))
+FILES = {"chacha20_poly1305_tests.txt": "chacha20_poly1305.npz",
+         "aes_128_gcm_tests.txt": "aes_128_gcm.npz"}
 
 
 def value(v):
@@ -45,14 +48,16 @@ def pack(vals):
 
 
 def main():
-    cases = parse(sys.argv[1] if len(sys.argv) > 1 else SRC)
-    assert all(set(c) == {"KEY", "NONCE", "IN", "AD", "CT", "TAG"} for c in cases)
-    d = {}
-    for f in ("KEY", "NONCE", "IN", "AD", "CT", "TAG"):
-        b, o, l = pack([c[f] for c in cases])
-        d[f.lower()], d[f.lower() + "_off"], d[f.lower() + "_len"] = b, o, l
-    np.savez_compressed(OUT, **d)
-    print(f"{len(cases)} vectors -> {OUT}")
+    for src, dst in FILES.items():
+        cases = parse(os.path.join(TESTS, src))
+        assert all(set(c) == {"KEY", "NONCE", "IN", "AD", "CT", "TAG"} for c in cases)
+        d = {}
+        for f in ("KEY", "NONCE", "IN", "AD", "CT", "TAG"):
+            b, o, l = pack([c[f] for c in cases])
+            d[f.lower()], d[f.lower() + "_off"], d[f.lower() + "_len"] = b, o, l
+        out = os.path.join(HERE, dst)
+        np.savez_compressed(out, **d)
+        print(f"{len(cases)} vectors -> {out}")
 
 
 if __name__ == "__main__":

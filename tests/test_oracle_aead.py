@@ -93,3 +93,52 @@ def test_quic_packet_form():
     ct7 = OC.quic_c20p1305_encrypt(key, prefix, pn, ad, pt, path_id=7)
     nonce7 = np.concatenate([prefix, np.frombuffer(((7 << 56) | pn).to_bytes(8, "little"), np.uint8)])
     assert np.array_equal(ct7, OC.c20p1305_seal(key, nonce7, pt, ad, tag_len=12))
+
+
+# ---- AES-128-GCM -------------------------------------------------------------
+@pytest.fixture(scope="module")
+def gvec():
+    z = load_npz("aes_128_gcm.npz")
+
+    def get(f, i):
+        o, l = int(z[f + "_off"][i]), int(z[f + "_len"][i])
+        return z[f][o:o + l]
+    return z, get
+
+
+def test_aes_fips197_kat():
+    # FIPS-197 Appendix C.1
+    key = bytes(range(16))
+    pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    assert bytes(OC.aes128_encrypt(key, pt)).hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"
+
+
+def test_boringssl_gcm_vectors(gvec):
+    z, get = gvec
+    n = z["key_len"].size
+    assert n == 74
+    for i in range(n):
+        key, iv, pt, ad, ct, tag = (get(f, i) for f in ("key", "nonce", "in", "ad", "ct", "tag"))
+        out = OC.aes128gcm_seal(key, iv, pt, ad, tag_len=tag.size)
+        assert np.array_equal(out[:pt.size], ct), i
+        assert np.array_equal(out[pt.size:], tag), i
+        ok, dec = OC.aes128gcm_open(key, iv, out, ad, tag_len=tag.size)
+        assert ok and np.array_equal(dec, pt), i
+        bad = out.copy()
+        bad[0 if out.size else 0] ^= 1
+        if bad.size:
+            assert not OC.aes128gcm_open(key, iv, bad, ad, tag_len=tag.size)[0], i
+
+
+def test_gcm_vs_reference_random(ref):
+    rng = np.random.default_rng(13)
+    for _ in range(150):
+        key = rng.integers(0, 256, 16, dtype=np.uint8)
+        blk = rng.integers(0, 256, 16, dtype=np.uint8)
+        assert np.array_equal(OC.aes128_encrypt(key, blk), ref.aes128_encrypt(key, blk))
+        iv = rng.integers(0, 256, 12 if rng.integers(0, 4) else int(rng.integers(1, 40)),
+                          dtype=np.uint8)
+        pt = rng.integers(0, 256, int(rng.integers(0, 1500)), dtype=np.uint8)
+        ad = rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8)
+        assert np.array_equal(OC.aes128gcm_seal(key, iv, pt, ad, 12),
+                              ref.aes128gcm_seal(key, iv, pt, ad, 12))
