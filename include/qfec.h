@@ -204,6 +204,26 @@ int qfec_chacha20poly1305_open_batch(qfec_ctx* ctx, const uint8_t* keys, const u
                                      uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
                                      uint8_t* ok, uint32_t flags);
 
+/* AES-128-GCM packet protection (12-byte tags), same batch form as the
+ * ChaCha20-Poly1305 calls above with 16-byte keys (keys holds 16 bytes per
+ * key).  Replaces Aes128Gcm12Encrypter::EncryptPacket / Aes128Gcm12Decrypter::
+ * DecryptPacket (crypto/aes_128_gcm_12_encrypter.cc -> AeadBaseEncrypter,
+ * BoringSSL EVP_aead_aes_128_gcm).  Throughput is best when runs of 64
+ * consecutive packets share a key (one GHASH table per wave); mixed-key runs
+ * are correct but take a bit-serial GHASH. */
+int qfec_aes128gcm_seal_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                              const uint32_t* key_idx, const uint64_t* packet_number,
+                              const uint8_t* path_id, const uint8_t* bytes, const uint64_t* ad_off,
+                              const uint16_t* ad_len, const uint64_t* in_off,
+                              const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                              const uint64_t* out_off, uint32_t flags);
+int qfec_aes128gcm_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                              const uint32_t* key_idx, const uint64_t* packet_number,
+                              const uint8_t* path_id, const uint8_t* bytes, const uint64_t* ad_off,
+                              const uint16_t* ad_len, const uint64_t* in_off,
+                              const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                              const uint64_t* out_off, uint8_t* ok, uint32_t flags);
+
 /* ---- measurement support (bench.py, device pointers) ------------------- */
 /* Streaming bandwidth probe over n bytes of src (n rounded down to 16):
  * mode 0 = read only (nt loads, XOR-folded; dst receives at most 16 bytes),

@@ -647,6 +647,7 @@ struct AeadHost {
   const uint32_t* key_idx;
   const uint64_t* packet_number;
   const uint8_t* path_id;
+  bool aes;  // AES-128-GCM (16-B keys) instead of ChaCha20-Poly1305 (32-B keys)
 };
 
 int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64_t* ad_off,
@@ -699,11 +700,12 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
     uint32_t nkeys = 0;
     for (uint64_t p = 0; p < n; ++p) nkeys = std::max(nkeys, aead->key_idx[p] + 1u);
     DevBuf d_keys, d_pre, d_kidx, d_pn, d_path;
-    QFEC_HIP(ctx, hipMalloc(&d_keys.p, 32ull * nkeys));
+    const uint64_t ksz = aead->aes ? 16ull : 32ull;
+    QFEC_HIP(ctx, hipMalloc(&d_keys.p, ksz * nkeys));
     QFEC_HIP(ctx, hipMalloc(&d_pre.p, 4ull * nkeys));
     QFEC_HIP(ctx, hipMalloc(&d_kidx.p, n * 4));
     QFEC_HIP(ctx, hipMalloc(&d_pn.p, n * 8));
-    QFEC_HIP(ctx, hipMemcpyAsync(d_keys.p, aead->keys, 32ull * nkeys, hipMemcpyHostToDevice, st));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_keys.p, aead->keys, ksz * nkeys, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_pre.p, aead->prefixes, 4ull * nkeys, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_kidx.p, aead->key_idx, n * 4, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_pn.p, aead->packet_number, n * 8, hipMemcpyHostToDevice, st));
@@ -718,7 +720,8 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
     aa.key_idx = static_cast<const uint32_t*>(d_kidx.p);
     aa.packet_number = static_cast<const uint64_t*>(d_pn.p);
     aa.path_id = static_cast<const uint8_t*>(d_path.p);
-    QFEC_HIP(ctx, qfec::launch_chacha20poly1305(aa, decrypt, st));
+    QFEC_HIP(ctx, aead->aes ? qfec::launch_aes128gcm(aa, decrypt, st)
+                            : qfec::launch_chacha20poly1305(aa, decrypt, st));
     QFEC_HIP(ctx, hipMemcpyAsync(out + olo, d_out.p, ohi - olo, hipMemcpyDeviceToHost, st));
     if (decrypt) QFEC_HIP(ctx, hipMemcpyAsync(ok, d_ok.p, n, hipMemcpyDeviceToHost, st));
     QFEC_HIP(ctx, hipStreamSynchronize(st));
@@ -758,7 +761,7 @@ int null_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
 
 }  // namespace
 
-int chacha_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* keys, const uint8_t* prefixes,
+int aead_protect(qfec_ctx* ctx, bool aes, bool decrypt, const uint8_t* keys, const uint8_t* prefixes,
                    const uint32_t* key_idx, const uint64_t* packet_number, const uint8_t* path_id,
                    const uint8_t* bytes, const uint64_t* ad_off, const uint16_t* ad_len,
                    const uint64_t* in_off, const uint16_t* in_len, uint64_t n, uint8_t* out,
@@ -770,7 +773,7 @@ int chacha_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* keys, const uint8
       !in_off || !in_len || !out || !out_off || (decrypt && !ok))
     return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
   if (flags & QFEC_PTR_HOST) {
-    const AeadHost h{keys, prefixes, key_idx, packet_number, path_id};
+    const AeadHost h{keys, prefixes, key_idx, packet_number, path_id, aes};
     return protect_host(ctx, decrypt, bytes, ad_off, ad_len, in_off, in_len, n, out, out_off, ok,
                         &h);
   }
@@ -789,7 +792,8 @@ int chacha_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* keys, const uint8
   a.key_idx = key_idx;
   a.packet_number = packet_number;
   a.path_id = path_id;
-  QFEC_HIP(ctx, qfec::launch_chacha20poly1305(a, decrypt, ctx->stream));
+  QFEC_HIP(ctx, aes ? qfec::launch_aes128gcm(a, decrypt, ctx->stream)
+                    : qfec::launch_chacha20poly1305(a, decrypt, ctx->stream));
   return QFEC_OK;
 }
 
@@ -816,7 +820,7 @@ int qfec_chacha20poly1305_seal_batch(qfec_ctx* ctx, const uint8_t* keys, const u
                                      const uint64_t* in_off, const uint16_t* in_len,
                                      uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
                                      uint32_t flags) {
-  return chacha_protect(ctx, false, keys, prefixes, key_idx, packet_number, path_id, bytes,
+  return aead_protect(ctx, false, false, keys, prefixes, key_idx, packet_number, path_id, bytes,
                         ad_off, ad_len, in_off, in_len, n_packets, out, out_off, nullptr, flags);
 }
 
@@ -827,8 +831,28 @@ int qfec_chacha20poly1305_open_batch(qfec_ctx* ctx, const uint8_t* keys, const u
                                      const uint64_t* in_off, const uint16_t* in_len,
                                      uint64_t n_packets, uint8_t* out, const uint64_t* out_off,
                                      uint8_t* ok, uint32_t flags) {
-  return chacha_protect(ctx, true, keys, prefixes, key_idx, packet_number, path_id, bytes,
+  return aead_protect(ctx, false, true, keys, prefixes, key_idx, packet_number, path_id, bytes,
                         ad_off, ad_len, in_off, in_len, n_packets, out, out_off, ok, flags);
+}
+
+int qfec_aes128gcm_seal_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                              const uint32_t* key_idx, const uint64_t* packet_number,
+                              const uint8_t* path_id, const uint8_t* bytes, const uint64_t* ad_off,
+                              const uint16_t* ad_len, const uint64_t* in_off,
+                              const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                              const uint64_t* out_off, uint32_t flags) {
+  return aead_protect(ctx, true, false, keys, prefixes, key_idx, packet_number, path_id, bytes,
+                      ad_off, ad_len, in_off, in_len, n_packets, out, out_off, nullptr, flags);
+}
+
+int qfec_aes128gcm_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t* prefixes,
+                              const uint32_t* key_idx, const uint64_t* packet_number,
+                              const uint8_t* path_id, const uint8_t* bytes, const uint64_t* ad_off,
+                              const uint16_t* ad_len, const uint64_t* in_off,
+                              const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
+                              const uint64_t* out_off, uint8_t* ok, uint32_t flags) {
+  return aead_protect(ctx, true, true, keys, prefixes, key_idx, packet_number, path_id, bytes,
+                      ad_off, ad_len, in_off, in_len, n_packets, out, out_off, ok, flags);
 }
 
 int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* dst, int mode) {

@@ -77,6 +77,8 @@ struct AeadArgs {
 };
 
 hipError_t launch_chacha20poly1305(const AeadArgs& a, bool decrypt, hipStream_t s);
+// AES-128-GCM (QUIC: 12-byte tag; keys are 16 B each).
+hipError_t launch_aes128gcm(const AeadArgs& a, bool decrypt, hipStream_t s);
 
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);

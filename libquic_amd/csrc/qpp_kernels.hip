@@ -657,6 +657,397 @@ __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
   }
 }
 
+// ===========================================================================
+// AES-128-GCM (QUIC: 12-byte tag)
+//   seal  Aes128Gcm12Encrypter::EncryptPacket = AeadBaseEncrypter::EncryptPacket
+//         -> EVP_aead_aes_128_gcm aead_aes_gcm_seal,
+//            boringssl/crypto/cipher/e_aes.c:1050-1091 over crypto/modes/gcm.c
+//   open  Aes128Gcm12Decrypter::DecryptPacket -> aead_aes_gcm_open (:1093-1140)
+// One lane per packet: its AES-128 round keys in registers (expanded per
+// lane), CTR keystream one AES block per 16-byte chunk, GHASH per chunk.
+// AES rounds use one T-table (Te0; Te1..3 are byte rotations of it) in LDS,
+// replicated 32x so lane l reads copy l % 32: any lookup pattern costs at
+// most 2 bank cycles.  GHASH uses Shoup's 4-bit tables (BoringSSL
+// gcm_init_4bit / gcm_gmult_4bit) from the wave's H in LDS (256 B, one bank
+// row: conflict-free) when every packet of the wave has the same key — the
+// batched-by-connection case — and a bit-serial multiply otherwise.
+// ===========================================================================
+__constant__ uint32_t kTe0[256] = {
+    0xa56363c6u, 0x847c7cf8u, 0x997777eeu, 0x8d7b7bf6u, 0x0df2f2ffu, 0xbd6b6bd6u, 0xb16f6fdeu, 0x54c5c591u,
+    0x50303060u, 0x03010102u, 0xa96767ceu, 0x7d2b2b56u, 0x19fefee7u, 0x62d7d7b5u, 0xe6abab4du, 0x9a7676ecu,
+    0x45caca8fu, 0x9d82821fu, 0x40c9c989u, 0x877d7dfau, 0x15fafaefu, 0xeb5959b2u, 0xc947478eu, 0x0bf0f0fbu,
+    0xecadad41u, 0x67d4d4b3u, 0xfda2a25fu, 0xeaafaf45u, 0xbf9c9c23u, 0xf7a4a453u, 0x967272e4u, 0x5bc0c09bu,
+    0xc2b7b775u, 0x1cfdfde1u, 0xae93933du, 0x6a26264cu, 0x5a36366cu, 0x413f3f7eu, 0x02f7f7f5u, 0x4fcccc83u,
+    0x5c343468u, 0xf4a5a551u, 0x34e5e5d1u, 0x08f1f1f9u, 0x937171e2u, 0x73d8d8abu, 0x53313162u, 0x3f15152au,
+    0x0c040408u, 0x52c7c795u, 0x65232346u, 0x5ec3c39du, 0x28181830u, 0xa1969637u, 0x0f05050au, 0xb59a9a2fu,
+    0x0907070eu, 0x36121224u, 0x9b80801bu, 0x3de2e2dfu, 0x26ebebcdu, 0x6927274eu, 0xcdb2b27fu, 0x9f7575eau,
+    0x1b090912u, 0x9e83831du, 0x742c2c58u, 0x2e1a1a34u, 0x2d1b1b36u, 0xb26e6edcu, 0xee5a5ab4u, 0xfba0a05bu,
+    0xf65252a4u, 0x4d3b3b76u, 0x61d6d6b7u, 0xceb3b37du, 0x7b292952u, 0x3ee3e3ddu, 0x712f2f5eu, 0x97848413u,
+    0xf55353a6u, 0x68d1d1b9u, 0x00000000u, 0x2cededc1u, 0x60202040u, 0x1ffcfce3u, 0xc8b1b179u, 0xed5b5bb6u,
+    0xbe6a6ad4u, 0x46cbcb8du, 0xd9bebe67u, 0x4b393972u, 0xde4a4a94u, 0xd44c4c98u, 0xe85858b0u, 0x4acfcf85u,
+    0x6bd0d0bbu, 0x2aefefc5u, 0xe5aaaa4fu, 0x16fbfbedu, 0xc5434386u, 0xd74d4d9au, 0x55333366u, 0x94858511u,
+    0xcf45458au, 0x10f9f9e9u, 0x06020204u, 0x817f7ffeu, 0xf05050a0u, 0x443c3c78u, 0xba9f9f25u, 0xe3a8a84bu,
+    0xf35151a2u, 0xfea3a35du, 0xc0404080u, 0x8a8f8f05u, 0xad92923fu, 0xbc9d9d21u, 0x48383870u, 0x04f5f5f1u,
+    0xdfbcbc63u, 0xc1b6b677u, 0x75dadaafu, 0x63212142u, 0x30101020u, 0x1affffe5u, 0x0ef3f3fdu, 0x6dd2d2bfu,
+    0x4ccdcd81u, 0x140c0c18u, 0x35131326u, 0x2fececc3u, 0xe15f5fbeu, 0xa2979735u, 0xcc444488u, 0x3917172eu,
+    0x57c4c493u, 0xf2a7a755u, 0x827e7efcu, 0x473d3d7au, 0xac6464c8u, 0xe75d5dbau, 0x2b191932u, 0x957373e6u,
+    0xa06060c0u, 0x98818119u, 0xd14f4f9eu, 0x7fdcdca3u, 0x66222244u, 0x7e2a2a54u, 0xab90903bu, 0x8388880bu,
+    0xca46468cu, 0x29eeeec7u, 0xd3b8b86bu, 0x3c141428u, 0x79dedea7u, 0xe25e5ebcu, 0x1d0b0b16u, 0x76dbdbadu,
+    0x3be0e0dbu, 0x56323264u, 0x4e3a3a74u, 0x1e0a0a14u, 0xdb494992u, 0x0a06060cu, 0x6c242448u, 0xe45c5cb8u,
+    0x5dc2c29fu, 0x6ed3d3bdu, 0xefacac43u, 0xa66262c4u, 0xa8919139u, 0xa4959531u, 0x37e4e4d3u, 0x8b7979f2u,
+    0x32e7e7d5u, 0x43c8c88bu, 0x5937376eu, 0xb76d6ddau, 0x8c8d8d01u, 0x64d5d5b1u, 0xd24e4e9cu, 0xe0a9a949u,
+    0xb46c6cd8u, 0xfa5656acu, 0x07f4f4f3u, 0x25eaeacfu, 0xaf6565cau, 0x8e7a7af4u, 0xe9aeae47u, 0x18080810u,
+    0xd5baba6fu, 0x887878f0u, 0x6f25254au, 0x722e2e5cu, 0x241c1c38u, 0xf1a6a657u, 0xc7b4b473u, 0x51c6c697u,
+    0x23e8e8cbu, 0x7cdddda1u, 0x9c7474e8u, 0x211f1f3eu, 0xdd4b4b96u, 0xdcbdbd61u, 0x868b8b0du, 0x858a8a0fu,
+    0x907070e0u, 0x423e3e7cu, 0xc4b5b571u, 0xaa6666ccu, 0xd8484890u, 0x05030306u, 0x01f6f6f7u, 0x120e0e1cu,
+    0xa36161c2u, 0x5f35356au, 0xf95757aeu, 0xd0b9b969u, 0x91868617u, 0x58c1c199u, 0x271d1d3au, 0xb99e9e27u,
+    0x38e1e1d9u, 0x13f8f8ebu, 0xb398982bu, 0x33111122u, 0xbb6969d2u, 0x70d9d9a9u, 0x898e8e07u, 0xa7949433u,
+    0xb69b9b2du, 0x221e1e3cu, 0x92878715u, 0x20e9e9c9u, 0x49cece87u, 0xff5555aau, 0x78282850u, 0x7adfdfa5u,
+    0x8f8c8c03u, 0xf8a1a159u, 0x80898909u, 0x170d0d1au, 0xdabfbf65u, 0x31e6e6d7u, 0xc6424284u, 0xb86868d0u,
+    0xc3414182u, 0xb0999929u, 0x772d2d5au, 0x110f0f1eu, 0xcbb0b07bu, 0xfc5454a8u, 0xd6bbbb6du, 0x3a16162cu,
+};
+
+// rem_4bit (gcm.c): reduction of the 4 bits shifted out, top 16 bits of hi
+__constant__ uint32_t kRem4[16] = {0x0000u, 0x1C20u, 0x3840u, 0x2460u, 0x7080u, 0x6CA0u,
+                                   0x48C0u, 0x54E0u, 0xE100u, 0xFD20u, 0xD940u, 0xC560u,
+                                   0x9180u, 0x8DA0u, 0xA9C0u, 0xB5E0u};
+
+constexpr uint32_t kTeCopies = 32;
+
+struct AesKey {
+  uint32_t rk[44];  // little-endian words of the FIPS-197 round-key bytes
+};
+
+__device__ __forceinline__ uint32_t te0(const uint32_t* te, uint32_t x, uint32_t copy) {
+  return te[x * kTeCopies + copy];
+}
+
+__device__ __forceinline__ uint32_t sbox_of(const uint32_t* te, uint32_t x, uint32_t copy) {
+  return (te0(te, x, copy) >> 8) & 0xFFu;  // Te0 byte 1 = S(x)
+}
+
+// FIPS-197 §5.2 key expansion in little-endian words.
+__device__ __forceinline__ void aes_expand(AesKey& k, const uint8_t* key, const uint32_t* te,
+                                           uint32_t copy) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __builtin_memcpy(&k.rk[i], key + 4 * i, 4);
+  uint32_t rcon = 1;
+#pragma unroll
+  for (int i = 4; i < 44; ++i) {
+    uint32_t t = k.rk[i - 1];
+    if (i % 4 == 0) {
+      t = (t >> 8) | (t << 24);  // RotWord (LE)
+      t = sbox_of(te, t & 0xFFu, copy) | (sbox_of(te, (t >> 8) & 0xFFu, copy) << 8) |
+          (sbox_of(te, (t >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, t >> 24, copy) << 24);
+      t ^= rcon;
+      rcon = ((rcon << 1) ^ ((rcon & 0x80u) ? 0x1Bu : 0u)) & 0xFFu;
+    }
+    k.rk[i] = k.rk[i - 4] ^ t;
+  }
+}
+
+__device__ __forceinline__ u32x4 aes_encrypt(const AesKey& k, u32x4 in, const uint32_t* te,
+                                             uint32_t copy) {
+  uint32_t s0 = in.x ^ k.rk[0], s1 = in.y ^ k.rk[1], s2 = in.z ^ k.rk[2], s3 = in.w ^ k.rk[3];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t t0 = te0(te, s0 & 0xFFu, copy) ^
+                        rotl32(te0(te, (s1 >> 8) & 0xFFu, copy), 8) ^
+                        rotl32(te0(te, (s2 >> 16) & 0xFFu, copy), 16) ^
+                        rotl32(te0(te, s3 >> 24, copy), 24) ^ k.rk[4 * r];
+    const uint32_t t1 = te0(te, s1 & 0xFFu, copy) ^
+                        rotl32(te0(te, (s2 >> 8) & 0xFFu, copy), 8) ^
+                        rotl32(te0(te, (s3 >> 16) & 0xFFu, copy), 16) ^
+                        rotl32(te0(te, s0 >> 24, copy), 24) ^ k.rk[4 * r + 1];
+    const uint32_t t2 = te0(te, s2 & 0xFFu, copy) ^
+                        rotl32(te0(te, (s3 >> 8) & 0xFFu, copy), 8) ^
+                        rotl32(te0(te, (s0 >> 16) & 0xFFu, copy), 16) ^
+                        rotl32(te0(te, s1 >> 24, copy), 24) ^ k.rk[4 * r + 2];
+    const uint32_t t3 = te0(te, s3 & 0xFFu, copy) ^
+                        rotl32(te0(te, (s0 >> 8) & 0xFFu, copy), 8) ^
+                        rotl32(te0(te, (s1 >> 16) & 0xFFu, copy), 16) ^
+                        rotl32(te0(te, s2 >> 24, copy), 24) ^ k.rk[4 * r + 3];
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+  }
+  u32x4 o;
+  o.x = (sbox_of(te, s0 & 0xFFu, copy) | (sbox_of(te, (s1 >> 8) & 0xFFu, copy) << 8) |
+         (sbox_of(te, (s2 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s3 >> 24, copy) << 24)) ^
+        k.rk[40];
+  o.y = (sbox_of(te, s1 & 0xFFu, copy) | (sbox_of(te, (s2 >> 8) & 0xFFu, copy) << 8) |
+         (sbox_of(te, (s3 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s0 >> 24, copy) << 24)) ^
+        k.rk[41];
+  o.z = (sbox_of(te, s2 & 0xFFu, copy) | (sbox_of(te, (s3 >> 8) & 0xFFu, copy) << 8) |
+         (sbox_of(te, (s0 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s1 >> 24, copy) << 24)) ^
+        k.rk[42];
+  o.w = (sbox_of(te, s3 & 0xFFu, copy) | (sbox_of(te, (s0 >> 8) & 0xFFu, copy) << 8) |
+         (sbox_of(te, (s1 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s2 >> 24, copy) << 24)) ^
+        k.rk[43];
+  return o;
+}
+
+// GHASH state / H as two big-endian 64-bit halves (gcm.c's u128 {hi, lo}).
+struct Gf128 {
+  uint64_t hi, lo;
+};
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
+
+__device__ __forceinline__ Gf128 gf_from_block(u32x4 b) {  // block bytes -> BE halves
+  return Gf128{bswap64((uint64_t)b.x | ((uint64_t)b.y << 32)),
+               bswap64((uint64_t)b.z | ((uint64_t)b.w << 32))};
+}
+
+__device__ __forceinline__ u32x4 gf_to_block(Gf128 g) {
+  const uint64_t a = bswap64(g.hi), b = bswap64(g.lo);
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
+// gcm_init_4bit: Htable[i] = i * H (4-bit, bit-reflected), into LDS.
+__device__ __forceinline__ void ghash_table(Gf128* tab, Gf128 h, uint32_t lane) {
+  // lane 0 builds the 16 entries (cheap, once per wave per batch)
+  if (lane == 0) {
+    Gf128 v = h;
+    tab[0] = Gf128{0ull, 0ull};
+    tab[8] = v;
+#pragma unroll
+    for (int i = 4; i > 0; i >>= 1) {  // REDUCE1BIT
+      const uint64_t t = 0xe100000000000000ull & (0ull - (v.lo & 1ull));
+      v.lo = (v.hi << 63) | (v.lo >> 1);
+      v.hi = (v.hi >> 1) ^ t;
+      tab[i] = v;
+    }
+#pragma unroll
+    for (int i = 2; i < 16; i <<= 1)
+      for (int j = 1; j < i; ++j) tab[i + j] = Gf128{tab[i].hi ^ tab[j].hi, tab[i].lo ^ tab[j].lo};
+  }
+}
+
+// gcm_gmult_4bit: X = X * H with the 4-bit table.
+__device__ __forceinline__ Gf128 ghash_mul_table(Gf128 x, const Gf128* tab) {
+  const u32x4 xb = gf_to_block(x);
+  uint8_t xi[16];
+  __builtin_memcpy(xi, &xb, 16);
+  uint32_t nlo = xi[15], nhi = nlo >> 4;
+  nlo &= 0xFu;
+  Gf128 z = tab[nlo];
+#pragma unroll
+  for (int cnt = 15;; --cnt) {
+    uint32_t rem = (uint32_t)z.lo & 0xFu;
+    z.lo = (z.hi << 60) | (z.lo >> 4);
+    z.hi = (z.hi >> 4) ^ ((uint64_t)kRem4[rem] << 48);
+    z.hi ^= tab[nhi].hi;
+    z.lo ^= tab[nhi].lo;
+    if (cnt == 0) break;
+    nlo = xi[cnt - 1];
+    nhi = nlo >> 4;
+    nlo &= 0xFu;
+    rem = (uint32_t)z.lo & 0xFu;
+    z.lo = (z.hi << 60) | (z.lo >> 4);
+    z.hi = (z.hi >> 4) ^ ((uint64_t)kRem4[rem] << 48);
+    z.hi ^= tab[nlo].hi;
+    z.lo ^= tab[nlo].lo;
+  }
+  return z;
+}
+
+// Bit-serial X * H (SP 800-38D Algorithm 1) for waves with mixed keys.
+__device__ __forceinline__ Gf128 ghash_mul_bits(Gf128 x, Gf128 h) {
+  Gf128 z{0ull, 0ull}, v = h;
+  for (int i = 0; i < 128; ++i) {
+    const uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1ull : (x.lo >> (127 - i)) & 1ull;
+    const uint64_t m = 0ull - bit;
+    z.hi ^= v.hi & m;
+    z.lo ^= v.lo & m;
+    const uint64_t t = 0xe100000000000000ull & (0ull - (v.lo & 1ull));
+    v.lo = (v.hi << 63) | (v.lo >> 1);
+    v.hi = (v.hi >> 1) ^ t;
+  }
+  return z;
+}
+
+struct Ghash {
+  Gf128 y, h;
+  const Gf128* tab;  // nullptr: bit-serial
+};
+
+__device__ __forceinline__ void ghash_block(Ghash& g, u32x4 blk) {
+  const Gf128 b = gf_from_block(blk);
+  g.y.hi ^= b.hi;
+  g.y.lo ^= b.lo;
+  g.y = g.tab ? ghash_mul_table(g.y, g.tab) : ghash_mul_bits(g.y, g.h);
+}
+
+// Counter block for data chunk c: J0 + 1 + c, J0 = nonce || 0x00000001.
+__device__ __forceinline__ u32x4 gcm_ctr(const uint32_t (&n)[3], uint32_t c) {
+  return u32x4{n[0], n[1], n[2], __builtin_bswap32(2u + c)};
+}
+
+// Payload pass (as aead_pass for ChaCha20): XOR keystream / GHASH in or out.
+template <uint32_t SC, bool XOR, bool MAC_IN, bool MAC_OUT>
+__device__ __forceinline__ void gcm_pass(const AesKey& key, const uint32_t (&nonce)[3],
+                                         Ghash& gh, const uint32_t* te, uint32_t copy,
+                                         const StageMeta* meta, u32x4* rows, uint32_t lane,
+                                         uint32_t my_nfull, bool store) {
+  const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
+  u32x4 buf[SC];
+  if (nslab) stage_load<SC>(meta, lane, 0, buf);
+  for (uint32_t sl = 0; sl < nslab; ++sl) {
+    stage_to_lds<SC>(rows, lane, buf);
+    if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, buf);
+    for (uint32_t j = 0; j < SC; ++j) {
+      const uint32_t c = sl * SC + j;
+      if (c >= my_nfull) break;
+      u32x4& slot = rows[lane * (SC + 1u) + j];
+      u32x4 v = slot;
+      if constexpr (MAC_IN) ghash_block(gh, v);
+      if constexpr (XOR) {
+        v ^= aes_encrypt(key, gcm_ctr(nonce, c), te, copy);
+        slot = v;
+      }
+      if constexpr (MAC_OUT) ghash_block(gh, v);
+    }
+    if (store) {
+      u32x4 out[SC];
+      stage_from_lds<SC>(rows, lane, out);
+      stage_store<SC>(meta, lane, sl, out);
+    }
+  }
+}
+
+__device__ __forceinline__ void ghash_lengths(Ghash& g, uint32_t ad_len, uint32_t ct_len) {
+  // [len(A)]_64 || [len(C)]_64 in bits, big-endian
+  const uint64_t a = (uint64_t)ad_len * 8u, c = (uint64_t)ct_len * 8u;
+  g.y.hi ^= a;
+  g.y.lo ^= c;
+  g.y = g.tab ? ghash_mul_table(g.y, g.tab) : ghash_mul_bits(g.y, g.h);
+}
+
+__device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, uint32_t len) {
+  const uint32_t nfull = len >> 4;
+  for (uint32_t c = 0; c < nfull; ++c) ghash_block(g, ld16(d + 16u * c));
+  const uint32_t rem = len & 15u;
+  if (rem) {
+    uint8_t b[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; ++i) b[i] = i < rem ? d[16u * nfull + i] : (uint8_t)0;
+    u32x4 v;
+    __builtin_memcpy(&v, b, 16);
+    ghash_block(g, v);
+  }
+}
+
+template <uint32_t SC, bool OPEN>
+__global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
+  __shared__ uint32_t s_te[256 * kTeCopies];  // 32 KiB
+  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
+  __shared__ StageMeta s_meta[kWaves][64];
+  __shared__ Gf128 s_tab[kWaves][16];
+  // replicated Te0 (every thread of the block helps, then a barrier)
+  for (uint32_t i = threadIdx.x; i < 256u * kTeCopies; i += kBlock)
+    s_te[i] = kTe0[i / kTeCopies];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t copy = lane & (kTeCopies - 1u);
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t inl = p < a.io.n ? a.io.in_len[p] : 0u;
+  const bool valid = p < a.io.n && (!OPEN || inl >= kTag);
+  if (OPEN && p < a.io.n && !valid) a.io.ok[p] = 0;  // open: in_len < tag_len
+  const uint8_t* ad = nullptr;
+  const uint8_t* in = nullptr;
+  uint32_t alen = 0, plen = 0, kidx = 0;
+  AesKey key = {};
+  uint32_t nonce[3] = {0u, 0u, 0u};
+  if (valid) {
+    ad = a.io.bytes + a.io.ad_off[p];
+    in = a.io.bytes + a.io.in_off[p];
+    alen = a.io.ad_len[p];
+    plen = OPEN ? inl - kTag : inl;
+    kidx = a.key_idx[p];
+    aes_expand(key, a.keys + 16ull * kidx, s_te, copy);
+    uint32_t pre;
+    __builtin_memcpy(&pre, a.prefixes + 4ull * kidx, 4);
+    const uint64_t pn = ((uint64_t)(a.path_id ? a.path_id[p] : 0u) << 56) | a.packet_number[p];
+    nonce[0] = pre;  // nonce = prefix || LE64(path_id << 56 | packet_number)
+    nonce[1] = (uint32_t)pn;
+    nonce[2] = (uint32_t)(pn >> 32);
+  }
+  // H = E_K(0^128); the wave shares one 4-bit table when all its valid
+  // packets use the same key (table from the first valid lane's H)
+  Ghash gh;
+  gh.h = gf_from_block(valid ? aes_encrypt(key, u32x4{0u, 0u, 0u, 0u}, s_te, copy)
+                             : u32x4{0u, 0u, 0u, 0u});
+  gh.y = Gf128{0ull, 0ull};
+  gh.tab = nullptr;
+  const uint64_t vmask = __ballot(valid);
+  if (vmask != 0ull) {
+    const int src = __builtin_ctzll(vmask);  // first valid lane
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)kidx, src);
+    if (__ballot(valid && kidx != k0) == 0ull) {
+      const uint32_t hh0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gh.h.hi, src);
+      const uint32_t hh1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gh.h.hi >> 32), src);
+      const uint32_t hl0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gh.h.lo, src);
+      const uint32_t hl1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gh.h.lo >> 32), src);
+      ghash_table(s_tab[wv], Gf128{(uint64_t)hh0 | ((uint64_t)hh1 << 32),
+                                   (uint64_t)hl0 | ((uint64_t)hl1 << 32)}, lane);
+      gh.tab = s_tab[wv];
+    }
+  }
+  u32x4 tail = {0u, 0u, 0u, 0u};
+  if (valid) {
+    ghash_span_padded(gh, ad, alen);
+    tail = tail_bytes(load_tail(in, plen), plen);  // before any store (in place)
+  }
+  const uint32_t rem = plen & 15u, ctail = plen >> 4;
+  if constexpr (!OPEN) {
+    uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta[wv][lane] = StageMeta{in, o, plen >> 4};
+    gcm_pass<SC, true, false, true>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+                                    plen >> 4, true);
+    if (!valid) return;
+    if (rem) {
+      u32x4 ct = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
+      uint8_t b[16];
+      __builtin_memcpy(b, &ct, 16);
+      for (uint32_t i = rem; i < 16u; ++i) b[i] = 0;  // zero pad for GHASH
+      __builtin_memcpy(&ct, b, 16);
+      ghash_block(gh, ct);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
+    }
+    ghash_lengths(gh, alen, plen);
+    const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
+                                  copy);  // E_K(J0)
+    const u32x4 t = gf_to_block(gh.y) ^ ek0;
+    const uint32_t tag[3] = {t.x, t.y, t.z};
+    __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
+  } else {
+    uint32_t want[3] = {0u, 0u, 0u};
+    if (valid) __builtin_memcpy(want, in + plen, kTag);
+    s_meta[wv][lane] = StageMeta{in, nullptr, plen >> 4};
+    gcm_pass<SC, false, true, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+                                     plen >> 4, false);
+    bool ok = false;
+    if (valid) {
+      if (rem) ghash_block(gh, tail);  // zero padded
+      ghash_lengths(gh, alen, plen);
+      const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
+                                    copy);
+      const u32x4 t = gf_to_block(gh.y) ^ ek0;
+      ok = ((t.x ^ want[0]) | (t.y ^ want[1]) | (t.z ^ want[2])) == 0u;
+      a.io.ok[p] = ok ? 1 : 0;
+    }
+    uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta[wv][lane] = StageMeta{in, o, ok ? plen >> 4 : 0u};
+    gcm_pass<SC, true, false, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+                                     ok ? plen >> 4 : 0u, true);
+    if (ok && rem) {
+      const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
+      uint8_t b[16];
+      __builtin_memcpy(b, &pt, 16);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t s) {
@@ -708,6 +1099,38 @@ hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t
       hipLaunchKernelGGL(c20p1305_open_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
     else
       hipLaunchKernelGGL(c20p1305_seal_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace qfec
+
+namespace qfec {
+
+// AES-128-GCM slab: 128 B (8 chunks) per packet per slab — round keys (44
+// VGPRs) and GHASH state take the registers a larger slab buffer would need.
+hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
+  constexpr uint32_t SC = 8;
+  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
+  for (uint64_t p = 0; p < a0.io.n; p += chunk) {
+    AeadArgs a = a0;
+    a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;
+    a.io.ad_off += p;
+    a.io.ad_len += p;
+    a.io.in_off += p;
+    a.io.in_len += p;
+    a.io.out_off += p;
+    if (decrypt) a.io.ok += p;
+    a.key_idx += p;
+    a.packet_number += p;
+    if (a.path_id) a.path_id += p;
+    const uint32_t blocks = (uint32_t)((a.io.n + kBlock - 1) / kBlock);
+    if (decrypt)
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, false>), dim3(blocks), dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -62,6 +62,11 @@ SIGNATURES = [
     ("qfec_chacha20poly1305_open_batch", C.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p,
       C.c_uint32]),
+    ("qfec_aes128gcm_seal_batch", C.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, C.c_uint32]),
+    ("qfec_aes128gcm_open_batch", C.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p,
+      C.c_uint32]),
     ("qfec_stream_probe", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
@@ -240,6 +245,20 @@ class Context:
     def chacha20poly1305_open(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
                               ad_len, in_off, in_len, n, out, out_off, ok, *, host=False):
         return self._check(self.lib.qfec_chacha20poly1305_open_batch(
+            self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
+            _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
+            _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+
+    def aes128gcm_seal(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                       ad_len, in_off, in_len, n, out, out_off, *, host=False):
+        return self._check(self.lib.qfec_aes128gcm_seal_batch(
+            self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
+            _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
+            _ptr(out), _ptr(out_off), QFEC_PTR_HOST if host else 0))
+
+    def aes128gcm_open(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
+                       ad_len, in_off, in_len, n, out, out_off, ok, *, host=False):
+        return self._check(self.lib.qfec_aes128gcm_open_batch(
             self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
             _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
             _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
