@@ -443,6 +443,19 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
         ok), reps)
     ctx.sync()
     verified_c = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
+    # AES-128-GCM-12 (one key: every wave key-uniform, the Shoup-table GHASH path)
+    gkey = torch.arange(16, dtype=torch.uint8, device=dev) * 11 + 3
+    out = torch.empty(n * (L + 12), dtype=torch.uint8, device=dev)
+    ms_gs = _time_on(torch, stream, lambda: ctx.aes128gcm_seal(
+        gkey, pre, kidx, pn, None, data, ad_off, ad_len, pt_off, pt_len, n, out, out_off), reps)
+    cv[:, hdr:] = out.view(n, L + 12)
+    del out
+    ok.zero_()
+    ms_go = _time_on(torch, stream, lambda: ctx.aes128gcm_open(
+        gkey, pre, kidx, pn, None, cat, c_ad_off, ad_len, c_ct_off, ct_len, n, dout, d_out_off,
+        ok), reps)
+    ctx.sync()
+    verified_g = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
     b_enc = n * (hdr + L + L + 12)  # read header + payload, write tag + payload
     b_dec = n * (hdr + L + 12 + L)
     res = {"packets": n, "header": hdr, "payload": L,
@@ -458,7 +471,13 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
                "open_GiBps": round(b_dec / (ms_co / 1e3) / 2**30, 2),
                "seal_payload_GBps": round(n * L / (ms_cs / 1e3) / 1e9, 1),
                "seal_us": round(ms_cs * 1e3, 1), "open_us": round(ms_co * 1e3, 1),
-               "verified": verified_c}}
+               "verified": verified_c},
+           "aes128gcm": {
+               "seal_GiBps": round(b_enc / (ms_gs / 1e3) / 2**30, 2),
+               "open_GiBps": round(b_dec / (ms_go / 1e3) / 2**30, 2),
+               "seal_payload_GBps": round(n * L / (ms_gs / 1e3) / 1e9, 1),
+               "seal_us": round(ms_gs * 1e3, 1), "open_us": round(ms_go * 1e3, 1),
+               "verified": verified_g}}
     del cat, dout, data
     torch.cuda.empty_cache()
     if cpu:
@@ -468,12 +487,13 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
 
 def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
     res = _cpu_null_baseline(hdr, L, n, seconds)
-    res["chacha20poly1305"] = _cpu_chacha_baseline(hdr, L, n // 4, seconds)
+    res["chacha20poly1305"] = _cpu_aead_baseline("chacha20poly1305", hdr, L, n // 4, seconds)
+    res["aes128gcm"] = _cpu_aead_baseline("aes128gcm", hdr, L, n // 4, seconds)
     return res
 
 
-def _cpu_chacha_baseline(hdr, L, n, seconds):
-    """Oracle (vector-pinned scalar C) ChaCha20-Poly1305 seal on the host cores."""
+def _cpu_aead_baseline(aead, hdr, L, n, seconds):
+    """Oracle (vector-pinned scalar C) AEAD seal on the host cores."""
     from oracle import oracle_c as OC
     threads = min(16, os.cpu_count() or 1)
     rec = hdr + L
@@ -484,21 +504,24 @@ def _cpu_chacha_baseline(hdr, L, n, seconds):
     ad_len = np.full(n, hdr, np.uint16)
     pt_len = np.full(n, L, np.uint16)
     out_off = ar * np.uint64(L + 12)
-    keys = np.arange(32, dtype=np.uint8)
+    keys = np.arange(32 if aead == "chacha20poly1305" else 16, dtype=np.uint8)
+    seal = (OC.quic_c20p1305_encrypt_batch if aead == "chacha20poly1305"
+            else OC.quic_aes128gcm_encrypt_batch)
+    name = "ChaCha20-Poly1305" if aead == "chacha20poly1305" else "AES-128-GCM-12"
     pre = np.arange(4, dtype=np.uint8)
     kidx = np.zeros(n, np.uint32)
     pn = ar + np.uint64(1)
     t0, reps = time.perf_counter(), 0
     while time.perf_counter() - t0 < seconds / 2:
-        OC.quic_c20p1305_encrypt_batch(keys, pre, kidx, pn, None, data, ad_off, ad_len, pt_off,
-                                       pt_len, out_off, n * (L + 12), threads=threads)
+        seal(keys, pre, kidx, pn, None, data, ad_off, ad_len, pt_off, pt_len, out_off,
+             n * (L + 12), threads=threads)
         reps += 1
     el = time.perf_counter() - t0
     return {"value": round(reps * n * (hdr + L + L + 12) / el / 2**30, 3), "unit": "GiB/s",
             "cores": threads, "kind": "port",
-            "sample": f"oracle ChaCha20-Poly1305 seal of {n} packets, {reps} passes on {threads} "
+            "sample": f"oracle {name} seal of {n} packets, {reps} passes on {threads} "
                       f"threads (scalar C restatement pinned by BoringSSL's vectors; BoringSSL's "
-                      f"own SIMD assembly would be faster on the CPU)"}
+                      f"own SIMD/AES-NI assembly would be faster on the CPU)"}
 
 
 def _cpu_null_baseline(hdr, L, n, seconds):

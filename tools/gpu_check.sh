@@ -10,7 +10,7 @@ ok_or_fail() {  # $1 = rc, $2 = step name
   echo "[$2] rc=$1"
   if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "[$2] fatal rc=$1, stopping"; exit "$1"; fi
 }
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 ok_or_fail $? pytest_gpu
 tail -5 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1

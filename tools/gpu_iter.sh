@@ -12,7 +12,7 @@ step() {  # $1 = name, $2 = timeout, rest = command; output to $OUT/$1.log
   echo "[$name] rc=$rc"; tail -25 "$OUT/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
-step pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step pytest_gpu 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
 step ragged_variants 300 tools/debug/build/ragged_variants 6
 step tune_ragged 300 tools/tune/build/tune_ragged 10 5
 step bench 600 python bench.py --no-cpu-baseline --no-e2e
