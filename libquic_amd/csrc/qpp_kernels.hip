@@ -707,28 +707,37 @@ __constant__ uint32_t kTe0[256] = {
     0xc3414182u, 0xb0999929u, 0x772d2d5au, 0x110f0f1eu, 0xcbb0b07bu, 0xfc5454a8u, 0xd6bbbb6du, 0x3a16162cu,
 };
 
-// rem_4bit (gcm.c): reduction of the 4 bits shifted out, top 16 bits of hi
-__constant__ uint32_t kRem4[16] = {0x0000u, 0x1C20u, 0x3840u, 0x2460u, 0x7080u, 0x6CA0u,
-                                   0x48C0u, 0x54E0u, 0xE100u, 0xFD20u, 0xD940u, 0xC560u,
-                                   0x9180u, 0x8DA0u, 0xA9C0u, 0xB5E0u};
-
-constexpr uint32_t kTeCopies = 32;
+// Te0 in LDS: 256 rows of 256 B, row x = Te0[x] 64 times; lane l reads dword
+// l of a row.  ds_read_b32 banks are (a/4) mod 32 per 32-lane group, so every
+// lookup pattern is conflict-free, and the byte address of the lookup of
+// byte k of a state word s is (byte_k(s) << 8) | 4*lane: ONE v_perm_b32 per
+// lookup (the 32-copy 32 KiB layout needed a bfe + a shift-add).
+constexpr uint32_t kTeBytes = 256u * 256u;  // 64 KiB
 
 struct AesKey {
   uint32_t rk[44];  // little-endian words of the FIPS-197 round-key bytes
 };
 
-__device__ __forceinline__ uint32_t te0(const uint32_t* te, uint32_t x, uint32_t copy) {
-  return te[x * kTeCopies + copy];
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
 }
 
-__device__ __forceinline__ uint32_t sbox_of(const uint32_t* te, uint32_t x, uint32_t copy) {
-  return (te0(te, x, copy) >> 8) & 0xFFu;  // Te0 byte 1 = S(x)
+// Te0[byte k of s] from the lane's column (lane4 = 4 * lane)
+__device__ __forceinline__ uint32_t te_at(const uint32_t* te, uint32_t s, uint32_t k,
+                                          uint32_t lane4) {
+  const uint32_t addr = __builtin_amdgcn_perm(s, lane4, 0x0C0C0000u | ((4u + k) << 8));
+  return *(const uint32_t*)((const uint8_t*)te + addr);
+}
+
+// S(byte k of s): Te0 bytes 1 and 2 are S(x)
+__device__ __forceinline__ uint32_t sbox_at(const uint32_t* te, uint32_t s, uint32_t k,
+                                            uint32_t lane4) {
+  return (te_at(te, s, k, lane4) >> 8) & 0xFFu;
 }
 
 // FIPS-197 §5.2 key expansion in little-endian words.
 __device__ __forceinline__ void aes_expand(AesKey& k, const uint8_t* key, const uint32_t* te,
-                                           uint32_t copy) {
+                                           uint32_t lane4) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) __builtin_memcpy(&k.rk[i], key + 4 * i, 4);
   uint32_t rcon = 1;
@@ -736,9 +745,9 @@ __device__ __forceinline__ void aes_expand(AesKey& k, const uint8_t* key, const 
   for (int i = 4; i < 44; ++i) {
     uint32_t t = k.rk[i - 1];
     if (i % 4 == 0) {
-      t = (t >> 8) | (t << 24);  // RotWord (LE)
-      t = sbox_of(te, t & 0xFFu, copy) | (sbox_of(te, (t >> 8) & 0xFFu, copy) << 8) |
-          (sbox_of(te, (t >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, t >> 24, copy) << 24);
+      // SubWord(RotWord(t)) (LE): byte j of the result = S(byte j+1 of t)
+      t = sbox_at(te, t, 1, lane4) | (sbox_at(te, t, 2, lane4) << 8) |
+          (sbox_at(te, t, 3, lane4) << 16) | (sbox_at(te, t, 0, lane4) << 24);
       t ^= rcon;
       rcon = ((rcon << 1) ^ ((rcon & 0x80u) ? 0x1Bu : 0u)) & 0xFFu;
     }
@@ -746,135 +755,211 @@ __device__ __forceinline__ void aes_expand(AesKey& k, const uint8_t* key, const 
   }
 }
 
-__device__ __forceinline__ u32x4 aes_encrypt(const AesKey& k, u32x4 in, const uint32_t* te,
-                                             uint32_t copy) {
-  uint32_t s0 = in.x ^ k.rk[0], s1 = in.y ^ k.rk[1], s2 = in.z ^ k.rk[2], s3 = in.w ^ k.rk[3];
+// NB independent blocks through the same rounds (their LDS lookups and VALU
+// interleave).  Column c of a round = Te0[s_c.b0] ^ rot8 Te0[s_c+1.b1] ^
+// rot16 Te0[s_c+2.b2] ^ rot24 Te0[s_c+3.b3] ^ rk: 4 perms, 4 lookups,
+// 3 alignbits, 2 bitop3.  Last round: S bytes gathered by two perms.
+template <int NB>
+__device__ __forceinline__ void aes_encrypt_n(const AesKey& k, u32x4 (&io)[NB], const uint32_t* te,
+                                              uint32_t lane4) {
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    s[b][0] = io[b].x ^ k.rk[0];
+    s[b][1] = io[b].y ^ k.rk[1];
+    s[b][2] = io[b].z ^ k.rk[2];
+    s[b][3] = io[b].w ^ k.rk[3];
+  }
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    const uint32_t t0 = te0(te, s0 & 0xFFu, copy) ^
-                        rotl32(te0(te, (s1 >> 8) & 0xFFu, copy), 8) ^
-                        rotl32(te0(te, (s2 >> 16) & 0xFFu, copy), 16) ^
-                        rotl32(te0(te, s3 >> 24, copy), 24) ^ k.rk[4 * r];
-    const uint32_t t1 = te0(te, s1 & 0xFFu, copy) ^
-                        rotl32(te0(te, (s2 >> 8) & 0xFFu, copy), 8) ^
-                        rotl32(te0(te, (s3 >> 16) & 0xFFu, copy), 16) ^
-                        rotl32(te0(te, s0 >> 24, copy), 24) ^ k.rk[4 * r + 1];
-    const uint32_t t2 = te0(te, s2 & 0xFFu, copy) ^
-                        rotl32(te0(te, (s3 >> 8) & 0xFFu, copy), 8) ^
-                        rotl32(te0(te, (s0 >> 16) & 0xFFu, copy), 16) ^
-                        rotl32(te0(te, s1 >> 24, copy), 24) ^ k.rk[4 * r + 2];
-    const uint32_t t3 = te0(te, s3 & 0xFFu, copy) ^
-                        rotl32(te0(te, (s0 >> 8) & 0xFFu, copy), 8) ^
-                        rotl32(te0(te, (s1 >> 16) & 0xFFu, copy), 16) ^
-                        rotl32(te0(te, s2 >> 24, copy), 24) ^ k.rk[4 * r + 3];
-    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    uint32_t t[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        t[b][c] = xor3(xor3(te_at(te, s[b][c], 0, lane4),
+                            rotl32(te_at(te, s[b][(c + 1) & 3], 1, lane4), 8),
+                            rotl32(te_at(te, s[b][(c + 2) & 3], 2, lane4), 16)),
+                       rotl32(te_at(te, s[b][(c + 3) & 3], 3, lane4), 24), k.rk[4 * r + c]);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[b][c] = t[b][c];
   }
-  u32x4 o;
-  o.x = (sbox_of(te, s0 & 0xFFu, copy) | (sbox_of(te, (s1 >> 8) & 0xFFu, copy) << 8) |
-         (sbox_of(te, (s2 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s3 >> 24, copy) << 24)) ^
-        k.rk[40];
-  o.y = (sbox_of(te, s1 & 0xFFu, copy) | (sbox_of(te, (s2 >> 8) & 0xFFu, copy) << 8) |
-         (sbox_of(te, (s3 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s0 >> 24, copy) << 24)) ^
-        k.rk[41];
-  o.z = (sbox_of(te, s2 & 0xFFu, copy) | (sbox_of(te, (s3 >> 8) & 0xFFu, copy) << 8) |
-         (sbox_of(te, (s0 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s1 >> 24, copy) << 24)) ^
-        k.rk[42];
-  o.w = (sbox_of(te, s3 & 0xFFu, copy) | (sbox_of(te, (s0 >> 8) & 0xFFu, copy) << 8) |
-         (sbox_of(te, (s1 >> 16) & 0xFFu, copy) << 16) | (sbox_of(te, s2 >> 24, copy) << 24)) ^
-        k.rk[43];
-  return o;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    uint32_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t A = te_at(te, s[b][c], 0, lane4), B = te_at(te, s[b][(c + 1) & 3], 1, lane4);
+      const uint32_t C = te_at(te, s[b][(c + 2) & 3], 2, lane4), D = te_at(te, s[b][(c + 3) & 3], 3, lane4);
+      // [S(A) S(B) 0 0] and [0 0 S(C) S(D)] from bytes 1 / 2 of the entries
+      o[c] = xor3(__builtin_amdgcn_perm(B, A, 0x0C0C0501u), __builtin_amdgcn_perm(D, C, 0x06020C0Cu),
+                  k.rk[40 + c]);
+    }
+    io[b] = u32x4{o[0], o[1], o[2], o[3]};
+  }
 }
 
-// GHASH state / H as two big-endian 64-bit halves (gcm.c's u128 {hi, lo}).
-struct Gf128 {
-  uint64_t hi, lo;
+__device__ __forceinline__ u32x4 aes_encrypt(const AesKey& k, u32x4 in, const uint32_t* te,
+                                             uint32_t lane4) {
+  u32x4 v[1] = {in};
+  aes_encrypt_n<1>(k, v, te, lane4);
+  return v[0];
+}
+
+// ---- GHASH -----------------------------------------------------------------
+// GF(2^128) elements as four big-endian 32-bit words: w[0] holds the
+// coefficients of x^0..x^31 with x^0 at the MSB (SP 800-38D bit order; the
+// u128 {hi, lo} of gcm.c split in words).  Multiplication by x is a right
+// shift; x^128 = 1 + x + x^2 + x^7.
+//
+// Uniform-key waves (the batched-by-connection case) multiply with Shoup's
+// 4-bit tables (gcm.c gcm_init_4bit: T[n] = n*H, nibble bit 3 = x^0) in LDS,
+// but WITHOUT gcm_gmult_4bit's per-nibble reduction: the 32 nibble products
+// T[n_k] * x^(4k) are summed unreduced into a 256-bit accumulator (a Horner
+// chain of 4-bit shifts over the nibble position, the four words of X in
+// parallel), and reduced once.  That removes the rem_4bit lookup and the
+// serial dependence between nibbles.  Blocks are taken two at a time with
+// aggregated reduction: Y' = (Y ^ C1)*H^2 ^ C2*H, one fold per pair (a second
+// table holds n*H^2).  Each table is 256 B — one LDS bank row — so the
+// wave's 64 ds_read_b128 lookups never conflict.
+// Mixed-key waves fall back to the bit-serial multiply (SP 800-38D Alg. 1).
+struct Gf4 {
+  uint32_t w[4];
 };
 
-__device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
-
-__device__ __forceinline__ Gf128 gf_from_block(u32x4 b) {  // block bytes -> BE halves
-  return Gf128{bswap64((uint64_t)b.x | ((uint64_t)b.y << 32)),
-               bswap64((uint64_t)b.z | ((uint64_t)b.w << 32))};
+__device__ __forceinline__ Gf4 gf_from_block(u32x4 b) {  // block bytes -> BE words
+  return Gf4{{__builtin_bswap32(b.x), __builtin_bswap32(b.y), __builtin_bswap32(b.z),
+              __builtin_bswap32(b.w)}};
 }
 
-__device__ __forceinline__ u32x4 gf_to_block(Gf128 g) {
-  const uint64_t a = bswap64(g.hi), b = bswap64(g.lo);
-  return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+__device__ __forceinline__ u32x4 gf_to_block(const Gf4& g) {
+  return u32x4{__builtin_bswap32(g.w[0]), __builtin_bswap32(g.w[1]), __builtin_bswap32(g.w[2]),
+               __builtin_bswap32(g.w[3])};
 }
 
-// gcm_init_4bit: Htable[i] = i * H (4-bit, bit-reflected), into LDS.
-__device__ __forceinline__ void ghash_table(Gf128* tab, Gf128 h, uint32_t lane) {
-  // lane 0 builds the 16 entries (cheap, once per wave per batch)
-  if (lane == 0) {
-    Gf128 v = h;
-    tab[0] = Gf128{0ull, 0ull};
-    tab[8] = v;
-#pragma unroll
-    for (int i = 4; i > 0; i >>= 1) {  // REDUCE1BIT
-      const uint64_t t = 0xe100000000000000ull & (0ull - (v.lo & 1ull));
-      v.lo = (v.hi << 63) | (v.lo >> 1);
-      v.hi = (v.hi >> 1) ^ t;
-      tab[i] = v;
-    }
-#pragma unroll
-    for (int i = 2; i < 16; i <<= 1)
-      for (int j = 1; j < i; ++j) tab[i + j] = Gf128{tab[i].hi ^ tab[j].hi, tab[i].lo ^ tab[j].lo};
-  }
+__device__ __forceinline__ Gf4 gf_xor(const Gf4& a, const Gf4& b) {
+  return Gf4{{a.w[0] ^ b.w[0], a.w[1] ^ b.w[1], a.w[2] ^ b.w[2], a.w[3] ^ b.w[3]}};
 }
 
-// gcm_gmult_4bit: X = X * H with the 4-bit table.
-__device__ __forceinline__ Gf128 ghash_mul_table(Gf128 x, const Gf128* tab) {
-  const u32x4 xb = gf_to_block(x);
-  uint8_t xi[16];
-  __builtin_memcpy(xi, &xb, 16);
-  uint32_t nlo = xi[15], nhi = nlo >> 4;
-  nlo &= 0xFu;
-  Gf128 z = tab[nlo];
-#pragma unroll
-  for (int cnt = 15;; --cnt) {
-    uint32_t rem = (uint32_t)z.lo & 0xFu;
-    z.lo = (z.hi << 60) | (z.lo >> 4);
-    z.hi = (z.hi >> 4) ^ ((uint64_t)kRem4[rem] << 48);
-    z.hi ^= tab[nhi].hi;
-    z.lo ^= tab[nhi].lo;
-    if (cnt == 0) break;
-    nlo = xi[cnt - 1];
-    nhi = nlo >> 4;
-    nlo &= 0xFu;
-    rem = (uint32_t)z.lo & 0xFu;
-    z.lo = (z.hi << 60) | (z.lo >> 4);
-    z.hi = (z.hi >> 4) ^ ((uint64_t)kRem4[rem] << 48);
-    z.hi ^= tab[nlo].hi;
-    z.lo ^= tab[nlo].lo;
-  }
-  return z;
+// low 32 bits of (hi:lo) >> r, 0 <= r < 32 (v_alignbit_b32)
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
+  return __builtin_amdgcn_alignbit(hi, lo, r);
+}
+
+// v * x (REDUCE1BIT of gcm.c)
+__device__ __forceinline__ Gf4 gf_mul_x(const Gf4& v) {
+  const uint32_t r = (v.w[3] & 1u) ? 0xE1000000u : 0u;
+  return Gf4{{(v.w[0] >> 1) ^ r, funnel(v.w[0], v.w[1], 1), funnel(v.w[1], v.w[2], 1),
+              funnel(v.w[2], v.w[3], 1)}};
 }
 
 // Bit-serial X * H (SP 800-38D Algorithm 1) for waves with mixed keys.
-__device__ __forceinline__ Gf128 ghash_mul_bits(Gf128 x, Gf128 h) {
-  Gf128 z{0ull, 0ull}, v = h;
+__device__ __forceinline__ Gf4 gf_mul_bits(const Gf4& x, const Gf4& h) {
+  Gf4 z{{0u, 0u, 0u, 0u}}, v = h;
   for (int i = 0; i < 128; ++i) {
-    const uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1ull : (x.lo >> (127 - i)) & 1ull;
-    const uint64_t m = 0ull - bit;
-    z.hi ^= v.hi & m;
-    z.lo ^= v.lo & m;
-    const uint64_t t = 0xe100000000000000ull & (0ull - (v.lo & 1ull));
-    v.lo = (v.hi << 63) | (v.lo >> 1);
-    v.hi = (v.hi >> 1) ^ t;
+    const uint32_t m = 0u - ((x.w[i >> 5] >> (31 - (i & 31))) & 1u);
+    z.w[0] ^= v.w[0] & m;
+    z.w[1] ^= v.w[1] & m;
+    z.w[2] ^= v.w[2] & m;
+    z.w[3] ^= v.w[3] & m;
+    v = gf_mul_x(v);
   }
   return z;
 }
 
+// Fold a 256-bit unreduced product (a[4..7] = coefficients of x^128..x^255)
+// into 128 bits: E * x^128 = E ^ E*x ^ E*x^2 ^ E*x^7, whose own overflow V
+// (at most 7 bits past x^127) is folded the same way once more.
+__device__ __forceinline__ Gf4 gf_fold(const uint32_t (&a)[8]) {
+  const uint64_t eh = ((uint64_t)a[4] << 32) | a[5], el = ((uint64_t)a[6] << 32) | a[7];
+  const uint64_t v = (el << 63) ^ (el << 62) ^ (el << 57);
+  const uint64_t hi = (((uint64_t)a[0] << 32) | a[1]) ^ eh ^ (eh >> 1) ^ (eh >> 2) ^ (eh >> 7) ^
+                      v ^ (v >> 1) ^ (v >> 2) ^ (v >> 7);
+  const uint64_t lo = (((uint64_t)a[2] << 32) | a[3]) ^ el ^ ((el >> 1) | (eh << 63)) ^
+                      ((el >> 2) | (eh << 62)) ^ ((el >> 7) | (eh << 57));
+  return Gf4{{(uint32_t)(hi >> 32), (uint32_t)hi, (uint32_t)(lo >> 32), (uint32_t)lo}};
+}
+
+// Unreduced sum of X_b * T_b over NB blocks, each with its own 4-bit table
+// (LDS), then one fold.  Nibble i of word q (bits 28-4i) is coefficient block
+// 8q+i, i.e. a shift of 32q + 4i: the word offset q is placement, the 4i is
+// the Horner chain over i.
+template <int NB>
+__device__ __forceinline__ Gf4 gf_mul_tables(const Gf4 (&x)[NB], const u32x4* const (&t)[NB]) {
+  uint32_t a[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  // rolled: the nibble shift is the only per-step difference, and a fully
+  // unrolled chain lets the compiler hoist every lookup (256+ VGPRs)
+#pragma unroll 1
+  for (int i = 7; i >= 0; --i) {
+    if (i < 7) {
+#pragma unroll
+      for (int d = 7; d > 0; --d) a[d] = funnel(a[d - 1], a[d], 4);
+      a[0] >>= 4;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int b = 0; b < NB; b += 2) {
+        const u32x4 e1 = t[b][(x[b].w[q] >> (28 - 4 * i)) & 0xFu];
+        const u32x4 e2 = t[b + 1][(x[b + 1].w[q] >> (28 - 4 * i)) & 0xFu];
+        a[q] = xor3(a[q], e1.x, e2.x);
+        a[q + 1] = xor3(a[q + 1], e1.y, e2.y);
+        a[q + 2] = xor3(a[q + 2], e1.z, e2.z);
+        a[q + 3] = xor3(a[q + 3], e1.w, e2.w);
+      }
+    }
+  }
+  return gf_fold(a);
+}
+
+// Table n*H^(j+1) (gcm_init_4bit of that power): lane 16j+n of the wave
+// writes entry n of table j.
+__device__ __forceinline__ void gf_table_entry(u32x4* tab, const Gf4& h, uint32_t n) {
+  const Gf4 h1 = gf_mul_x(h), h2 = gf_mul_x(h1), h3 = gf_mul_x(h2);
+  Gf4 e{{0u, 0u, 0u, 0u}};
+  if (n & 8u) e = gf_xor(e, h);
+  if (n & 4u) e = gf_xor(e, h1);
+  if (n & 2u) e = gf_xor(e, h2);
+  if (n & 1u) e = gf_xor(e, h3);
+  tab[n] = u32x4{e.w[0], e.w[1], e.w[2], e.w[3]};
+}
+
+// GHASH blocks per step: Y' = (Y ^ C1)*H^m ^ C2*H^(m-1) ^ ... ^ Cm*H, m <= kGhNB
+constexpr int kGhNB = 4;
+
 struct Ghash {
-  Gf128 y, h;
-  const Gf128* tab;  // nullptr: bit-serial
+  Gf4 y, h;
+  const u32x4* tab;  // [16j .. 16j+15] = n*H^(j+1), j < kGhNB; nullptr: bit-serial
 };
 
+// Absorb the first m (1..NB) of blocks c[0..NB-1].  Table path: block b < m
+// uses H^(m-b); blocks past m enter as zero (T[0] = 0) — one instruction
+// stream for every m, no divergence.
+template <int NB>
+__device__ __forceinline__ void ghash_absorb(Ghash& g, const u32x4 (&c)[NB], uint32_t m) {
+  static_assert(NB <= kGhNB && NB % 2 == 0, "tables for NB powers, blocks in pairs");
+  if (g.tab) {
+    Gf4 x[NB];
+    const u32x4* t[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      x[b] = (uint32_t)b < m ? gf_from_block(c[b]) : Gf4{{0u, 0u, 0u, 0u}};
+      t[b] = g.tab + 16u * ((uint32_t)b < m ? m - 1u - b : 0u);
+    }
+    x[0] = gf_xor(x[0], g.y);
+    g.y = gf_mul_tables<NB>(x, t);
+  } else {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if ((uint32_t)b < m) g.y = gf_mul_bits(gf_xor(g.y, gf_from_block(c[b])), g.h);
+  }
+}
+
 __device__ __forceinline__ void ghash_block(Ghash& g, u32x4 blk) {
-  const Gf128 b = gf_from_block(blk);
-  g.y.hi ^= b.hi;
-  g.y.lo ^= b.lo;
-  g.y = g.tab ? ghash_mul_table(g.y, g.tab) : ghash_mul_bits(g.y, g.h);
+  const u32x4 c[2] = {blk, blk};
+  ghash_absorb<2>(g, c, 1u);
 }
 
 // Counter block for data chunk c: J0 + 1 + c, J0 = nonce || 0x00000001.
@@ -882,29 +967,42 @@ __device__ __forceinline__ u32x4 gcm_ctr(const uint32_t (&n)[3], uint32_t c) {
   return u32x4{n[0], n[1], n[2], __builtin_bswap32(2u + c)};
 }
 
-// Payload pass (as aead_pass for ChaCha20): XOR keystream / GHASH in or out.
-template <uint32_t SC, bool XOR, bool MAC_IN, bool MAC_OUT>
+// Payload pass (as aead_pass for ChaCha20): XOR keystream / GHASH in or out,
+// NB chunks per step (NB independent AES blocks interleaved; GHASH with
+// aggregated reduction over the step).
+template <uint32_t SC, int NB, bool XOR, bool MAC_IN, bool MAC_OUT>
 __device__ __forceinline__ void gcm_pass(const AesKey& key, const uint32_t (&nonce)[3],
                                          Ghash& gh, const uint32_t* te, uint32_t copy,
                                          const StageMeta* meta, u32x4* rows, uint32_t lane,
                                          uint32_t my_nfull, bool store) {
+  static_assert(SC % NB == 0u, "whole steps per slab");
   const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
   u32x4 buf[SC];
   if (nslab) stage_load<SC>(meta, lane, 0, buf);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
     stage_to_lds<SC>(rows, lane, buf);
     if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, buf);
-    for (uint32_t j = 0; j < SC; ++j) {
+    for (uint32_t j = 0; j < SC; j += NB) {
       const uint32_t c = sl * SC + j;
       if (c >= my_nfull) break;
-      u32x4& slot = rows[lane * (SC + 1u) + j];
-      u32x4 v = slot;
-      if constexpr (MAC_IN) ghash_block(gh, v);
+      const uint32_t m = min((uint32_t)NB, my_nfull - c);
+      u32x4* slot = rows + lane * (SC + 1u) + j;
+      u32x4 v[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) v[b] = slot[b];
+      if constexpr (MAC_IN) ghash_absorb<NB>(gh, v, m);
       if constexpr (XOR) {
-        v ^= aes_encrypt(key, gcm_ctr(nonce, c), te, copy);
-        slot = v;
+        u32x4 k[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) k[b] = gcm_ctr(nonce, c + b);
+        aes_encrypt_n<NB>(key, k, te, copy);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          v[b] ^= k[b];
+          slot[b] = v[b];  // chunks past the packet's end are never stored
+        }
       }
-      if constexpr (MAC_OUT) ghash_block(gh, v);
+      if constexpr (MAC_OUT) ghash_absorb<NB>(gh, v, m);
     }
     if (store) {
       u32x4 out[SC];
@@ -917,14 +1015,18 @@ __device__ __forceinline__ void gcm_pass(const AesKey& key, const uint32_t (&non
 __device__ __forceinline__ void ghash_lengths(Ghash& g, uint32_t ad_len, uint32_t ct_len) {
   // [len(A)]_64 || [len(C)]_64 in bits, big-endian
   const uint64_t a = (uint64_t)ad_len * 8u, c = (uint64_t)ct_len * 8u;
-  g.y.hi ^= a;
-  g.y.lo ^= c;
-  g.y = g.tab ? ghash_mul_table(g.y, g.tab) : ghash_mul_bits(g.y, g.h);
+  const u32x4 blk = gf_to_block(Gf4{{(uint32_t)(a >> 32), (uint32_t)a, (uint32_t)(c >> 32),
+                                     (uint32_t)c}});
+  ghash_block(g, blk);
 }
 
 __device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, uint32_t len) {
   const uint32_t nfull = len >> 4;
-  for (uint32_t c = 0; c < nfull; ++c) ghash_block(g, ld16(d + 16u * c));
+  uint32_t c = 0;
+  for (; c < nfull; c += 2u) {
+    const u32x4 v[2] = {ld16(d + 16u * c), ld16(d + 16u * min(c + 1u, nfull - 1u))};
+    ghash_absorb<2>(g, v, min(2u, nfull - c));
+  }
   const uint32_t rem = len & 15u;
   if (rem) {
     uint8_t b[16];
@@ -936,19 +1038,36 @@ __device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, ui
   }
 }
 
+// 512-thread blocks: the 64 KiB table is shared by 8 waves; LDS 152 KiB per
+// block = one block per CU = 2 waves/SIMD (the VGPR budget allows 2 as well).
+constexpr int kGcmBlock = 512;
+constexpr int kGcmWaves = kGcmBlock / 64;
+constexpr int kGcmNB = 4;  // chunks per step of the payload passes
+
 template <uint32_t SC, bool OPEN>
-__global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
-  __shared__ uint32_t s_te[256 * kTeCopies];  // 32 KiB
-  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
-  __shared__ StageMeta s_meta[kWaves][64];
-  __shared__ Gf128 s_tab[kWaves][16];
-  // replicated Te0 (every thread of the block helps, then a barrier)
-  for (uint32_t i = threadIdx.x; i < 256u * kTeCopies; i += kBlock)
-    s_te[i] = kTe0[i / kTeCopies];
+__global__ __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void aes128gcm_kernel(AeadArgs a) {
+  // one LDS object with the table first: it sits at LDS address 0, so the
+  // v_perm result IS the lookup address (no base add per lookup)
+  struct Smem {
+    uint32_t te[kTeBytes / 4u];
+    u32x4 tab[kGcmWaves][16 * kGhNB];  // n*H^j per wave (256-B aligned tables)
+    u32x4 rows[kGcmWaves][64 * (SC + 1u)];
+    StageMeta meta[kGcmWaves][64];
+  };
+  __shared__ Smem sm;
+  uint32_t* const s_te = sm.te;
+  auto& s_rows = sm.rows;
+  auto& s_meta = sm.meta;
+  auto& s_tab = sm.tab;
+  // replicated Te0, 16-B stores (every thread of the block helps, then a barrier)
+  for (uint32_t i = threadIdx.x; i < kTeBytes / 16u; i += kGcmBlock) {
+    const uint32_t e = kTe0[i >> 4];
+    reinterpret_cast<u32x4*>(s_te)[i] = u32x4{e, e, e, e};
+  }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t copy = lane & (kTeCopies - 1u);
-  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t copy = lane * 4u;  // the lane's byte column in every table row
+  const uint64_t p = (uint64_t)blockIdx.x * kGcmBlock + threadIdx.x;
   const uint32_t inl = p < a.io.n ? a.io.in_len[p] : 0u;
   const bool valid = p < a.io.n && (!OPEN || inl >= kTag);
   if (OPEN && p < a.io.n && !valid) a.io.ok[p] = 0;  // open: in_len < tag_len
@@ -971,24 +1090,27 @@ __global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
     nonce[1] = (uint32_t)pn;
     nonce[2] = (uint32_t)(pn >> 32);
   }
-  // H = E_K(0^128); the wave shares one 4-bit table when all its valid
-  // packets use the same key (table from the first valid lane's H)
+  // H = E_K(0^128); the wave shares the 4-bit tables when all its valid
+  // packets use the same key (tables from the first valid lane's H)
   Ghash gh;
   gh.h = gf_from_block(valid ? aes_encrypt(key, u32x4{0u, 0u, 0u, 0u}, s_te, copy)
                              : u32x4{0u, 0u, 0u, 0u});
-  gh.y = Gf128{0ull, 0ull};
+  gh.y = Gf4{{0u, 0u, 0u, 0u}};
   gh.tab = nullptr;
   const uint64_t vmask = __ballot(valid);
   if (vmask != 0ull) {
     const int src = __builtin_ctzll(vmask);  // first valid lane
     const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)kidx, src);
     if (__ballot(valid && kidx != k0) == 0ull) {
-      const uint32_t hh0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gh.h.hi, src);
-      const uint32_t hh1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gh.h.hi >> 32), src);
-      const uint32_t hl0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gh.h.lo, src);
-      const uint32_t hl1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gh.h.lo >> 32), src);
-      ghash_table(s_tab[wv], Gf128{(uint64_t)hh0 | ((uint64_t)hh1 << 32),
-                                   (uint64_t)hl0 | ((uint64_t)hl1 << 32)}, lane);
+      Gf4 h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)gh.h.w[i], src);
+      Gf4 hp = h;  // H^(j+1) for lane 16j+n (once per wave)
+      for (uint32_t j = 0; j < lane / 16u; ++j) hp = gf_mul_bits(hp, h);
+      if (lane < 16u * kGhNB) gf_table_entry(s_tab[wv] + (lane & ~15u), hp, lane & 15u);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       gh.tab = s_tab[wv];
     }
   }
@@ -1001,7 +1123,7 @@ __global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
   if constexpr (!OPEN) {
     uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta[wv][lane] = StageMeta{in, o, plen >> 4};
-    gcm_pass<SC, true, false, true>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+    gcm_pass<SC, kGcmNB, true, false, true>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
                                     plen >> 4, true);
     if (!valid) return;
     if (rem) {
@@ -1023,7 +1145,7 @@ __global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
     uint32_t want[3] = {0u, 0u, 0u};
     if (valid) __builtin_memcpy(want, in + plen, kTag);
     s_meta[wv][lane] = StageMeta{in, nullptr, plen >> 4};
-    gcm_pass<SC, false, true, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+    gcm_pass<SC, kGcmNB, false, true, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
                                      plen >> 4, false);
     bool ok = false;
     if (valid) {
@@ -1037,7 +1159,7 @@ __global__ __launch_bounds__(kBlock) void aes128gcm_kernel(AeadArgs a) {
     }
     uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta[wv][lane] = StageMeta{in, o, ok ? plen >> 4 : 0u};
-    gcm_pass<SC, true, false, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+    gcm_pass<SC, kGcmNB, true, false, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
                                      ok ? plen >> 4 : 0u, true);
     if (ok && rem) {
       const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
@@ -1113,7 +1235,7 @@ namespace qfec {
 // VGPRs) and GHASH state take the registers a larger slab buffer would need.
 hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
   constexpr uint32_t SC = 8;
-  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
+  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kGcmBlock;
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;
     a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;
@@ -1126,11 +1248,11 @@ hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
     a.key_idx += p;
     a.packet_number += p;
     if (a.path_id) a.path_id += p;
-    const uint32_t blocks = (uint32_t)((a.io.n + kBlock - 1) / kBlock);
+    const uint32_t blocks = (uint32_t)((a.io.n + kGcmBlock - 1) / kGcmBlock);
     if (decrypt)
-      hipLaunchKernelGGL((aes128gcm_kernel<SC, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, true>), dim3(blocks), dim3(kGcmBlock), 0, s, a);
     else
-      hipLaunchKernelGGL((aes128gcm_kernel<SC, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, false>), dim3(blocks), dim3(kGcmBlock), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -19,7 +19,10 @@ cat "$OUT/smoke.log"
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok_or_fail $? bench
 cat "$OUT/bench.json"
+# the same default bench command under the profiler: its JSON line and the
+# kernel stats come from one process (bench_prof.json)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-  -- python bench.py --profile-only --steps 10 --no-verify > "$OUT/prof.log" 2>&1
+  -- python bench.py > "$OUT/bench_prof.json" 2> "$OUT/prof.log"
 ok_or_fail $? rocprof_stats
 find "$OUT/prof" -name '*stats*' | head
+python tools/kernel_by_grid.py "$OUT/prof/run_kernel_trace.csv" "$OUT/prof/kernel_by_grid.csv"
