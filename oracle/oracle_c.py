@@ -237,8 +237,8 @@ def null_decrypt(ad, ct):
     return bool(ok), out[:n.value]
 
 
-def null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, out_size, threads=1):
-    out = np.zeros(out_size, np.uint8)
+def null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, out_size, threads=1, out=None):
+    out = np.zeros(out_size, np.uint8) if out is None else out
     args = [_p(data), _p(ad_off), _p(ad_len), _p(pt_off), _p(pt_len), pt_len.size, _p(out),
             _p(out_off)]
     if threads > 1:
@@ -309,8 +309,8 @@ def quic_c20p1305_decrypt(key, prefix, packet_number, ad, ct, path_id=0):
 
 
 def quic_c20p1305_encrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
-                                ad_len, pt_off, pt_len, out_off, out_size, threads=1):
-    out = np.zeros(out_size, np.uint8)
+                                ad_len, pt_off, pt_len, out_off, out_size, threads=1, out=None):
+    out = np.zeros(out_size, np.uint8) if out is None else out
     lib().qo_quic_c20p1305_encrypt_batch(
         _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
         None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(pt_off),
@@ -355,8 +355,8 @@ def aes128gcm_open(key, iv, ct, ad, tag_len=16):
 
 
 def quic_aes128gcm_encrypt_batch(keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
-                                 ad_len, pt_off, pt_len, out_off, out_size, threads=1):
-    out = np.zeros(out_size, np.uint8)
+                                 ad_len, pt_off, pt_len, out_off, out_size, threads=1, out=None):
+    out = np.zeros(out_size, np.uint8) if out is None else out
     lib().qo_quic_aes128gcm_encrypt_batch(
         _p(keys), _p(prefixes), _p(key_idx), _p(packet_number),
         None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(pt_off),

@@ -90,3 +90,75 @@ REF_API int ref_aes128gcm_seal(uint8_t* out, const uint8_t* key, const uint8_t* 
   CRYPTO_gcm128_tag(&gcm, out + in_len, tag_len);
   return 1;
 }
+
+// ---- CPU baselines (bench.py cpu_baseline, kind "reference") ---------------
+// Batches of packets through the reference's own code on `threads` host
+// threads (contiguous packet ranges), the way a connection thread would call
+// it once per packet.  Packet p: header bytes[ad_off[p], +ad_len[p]), payload
+// bytes[pt_off[p], +pt_len[p]); output at out + out_off[p].
+#include <thread>
+#include <vector>
+
+template <typename F>
+static void ref_parallel(uint64_t n, int threads, F f) {
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> ts;
+  const uint64_t per = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    const uint64_t a = t * per, b = a + per < n ? a + per : n;
+    if (a >= b) break;
+    ts.emplace_back([=] { f(a, b); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+// NullEncrypter::EncryptPacket per packet (tag || payload, 12 + pt_len bytes)
+REF_API void ref_null_encrypt_batch(const uint8_t* bytes, const uint64_t* ad_off,
+                                    const uint16_t* ad_len, const uint64_t* pt_off,
+                                    const uint16_t* pt_len, uint64_t n, uint8_t* out,
+                                    const uint64_t* out_off, int threads) {
+  ref_parallel(n, threads, [&](uint64_t a, uint64_t b) {
+    net::NullEncrypter e;
+    for (uint64_t p = a; p < b; ++p) {
+      size_t olen = 0;
+      e.EncryptPacket(net::kDefaultPathId, p + 1,
+                      base::StringPiece((const char*)bytes + ad_off[p], ad_len[p]),
+                      base::StringPiece((const char*)bytes + pt_off[p], pt_len[p]),
+                      (char*)out + out_off[p], &olen, (size_t)pt_len[p] + 12);
+    }
+  });
+}
+
+// AES-128-GCM-12 seal per packet as AeadBaseEncrypter::EncryptPacket does it
+// (aead_base_encrypter.cc:107-134): nonce = 4-byte prefix || LE64(packet
+// number), then aead_aes_gcm_seal's steps over gcm.c.  The key schedule and
+// GHASH table are set up once per key (SetKey / EVP_AEAD_CTX_init), the
+// context is copied per packet.
+REF_API void ref_quic_aes128gcm_seal_batch(const uint8_t* keys, const uint8_t* prefixes,
+                                           const uint32_t* key_idx, const uint64_t* pn,
+                                           uint32_t n_keys, const uint8_t* bytes,
+                                           const uint64_t* ad_off, const uint16_t* ad_len,
+                                           const uint64_t* pt_off, const uint16_t* pt_len,
+                                           uint64_t n, uint8_t* out, const uint64_t* out_off,
+                                           int threads) {
+  std::vector<AES_KEY> ks(n_keys);
+  std::vector<GCM128_CONTEXT> ctx(n_keys);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    AES_set_encrypt_key(keys + 16u * k, 128, &ks[k]);
+    CRYPTO_gcm128_init(&ctx[k], &ks[k], (block128_f)AES_encrypt);
+  }
+  ref_parallel(n, threads, [&](uint64_t a, uint64_t b) {
+    for (uint64_t p = a; p < b; ++p) {
+      const uint32_t k = key_idx[p];
+      uint8_t nonce[12];
+      for (int i = 0; i < 4; ++i) nonce[i] = prefixes[4u * k + i];
+      for (int i = 0; i < 8; ++i) nonce[4 + i] = (uint8_t)(pn[p] >> (8 * i));
+      GCM128_CONTEXT g = ctx[k];
+      CRYPTO_gcm128_setiv(&g, &ks[k], nonce, 12);
+      if (ad_len[p]) CRYPTO_gcm128_aad(&g, bytes + ad_off[p], ad_len[p]);
+      uint8_t* o = out + out_off[p];
+      CRYPTO_gcm128_encrypt(&g, &ks[k], bytes + pt_off[p], o, pt_len[p]);
+      CRYPTO_gcm128_tag(&g, o + pt_len[p], 12);
+    }
+  });
+}

@@ -53,6 +53,12 @@ def lib():
         L.ref_aes128gcm_seal.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                          C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                          C.c_size_t]
+        L.ref_null_encrypt_batch.restype = None
+        L.ref_null_encrypt_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
+                                                                C.c_void_p, C.c_int]
+        L.ref_quic_aes128gcm_seal_batch.restype = None
+        L.ref_quic_aes128gcm_seal_batch.argtypes = [C.c_void_p] * 4 + [C.c_uint32] + \
+            [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -131,4 +137,29 @@ def aes128gcm_seal(key, iv, pt, ad, tag_len=16):
     ok = lib().ref_aes128gcm_seal(out.ctypes.data_as(C.c_void_p), _ptr(k), _ptr(n), n.size, _ptr(p),
                                   p.size, _ptr(a), a.size, tag_len)
     assert ok
+    return out
+
+
+def _pa(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, out_size, threads=1, out=None):
+    """NullEncrypter::EncryptPacket per packet (CPU baseline, bench.py)."""
+    out = np.zeros(out_size, np.uint8) if out is None else out
+    lib().ref_null_encrypt_batch(_pa(data), _pa(ad_off), _pa(ad_len), _pa(pt_off), _pa(pt_len),
+                                 pt_len.size, _pa(out), _pa(out_off), threads)
+    return out
+
+
+def quic_aes128gcm_encrypt_batch(keys, prefixes, key_idx, packet_number, data, ad_off, ad_len,
+                                 pt_off, pt_len, out_off, out_size, threads=1, out=None):
+    """Aes128Gcm12Encrypter-equivalent seal per packet over the reference's
+    aes.c + gcm.c (CPU baseline, bench.py)."""
+    out = np.zeros(out_size, np.uint8) if out is None else out
+    n_keys = int(key_idx.max()) + 1 if key_idx.size else 0
+    lib().ref_quic_aes128gcm_seal_batch(_pa(keys), _pa(prefixes), _pa(key_idx),
+                                        _pa(packet_number), n_keys, _pa(data), _pa(ad_off),
+                                        _pa(ad_len), _pa(pt_off), _pa(pt_len), pt_len.size,
+                                        _pa(out), _pa(out_off), threads)
     return out

@@ -142,3 +142,28 @@ def test_gcm_vs_reference_random(ref):
         ad = rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8)
         assert np.array_equal(OC.aes128gcm_seal(key, iv, pt, ad, 12),
                               ref.aes128gcm_seal(key, iv, pt, ad, 12))
+
+
+def test_quic_gcm_batch_vs_reference(ref):
+    """The QUIC packet form (prefix || LE64 packet number nonce, 12-byte tag,
+    many keys) over the reference's gcm.c — the bench's CPU baseline — equals
+    the oracle's batch."""
+    rng = np.random.default_rng(17)
+    n = 300
+    L = rng.integers(0, 1453, n).astype(np.uint16)
+    A = rng.integers(0, 40, n).astype(np.uint16)
+    rec = A.astype(np.uint64) + L
+    ad_off = np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.uint64)
+    pt_off = ad_off + A
+    data = rng.integers(0, 256, int(rec.sum()), dtype=np.uint8)
+    out_off = np.concatenate([[0], np.cumsum(L.astype(np.uint64) + 12)[:-1]]).astype(np.uint64)
+    tot = int((L.astype(np.uint64) + 12).sum())
+    keys = rng.integers(0, 256, 16 * 5, dtype=np.uint8)
+    pre = rng.integers(0, 256, 4 * 5, dtype=np.uint8)
+    kidx = rng.integers(0, 5, n).astype(np.uint32)
+    pn = rng.integers(1, 2**40, n).astype(np.uint64)
+    a = ref.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, data, ad_off, A, pt_off, L,
+                                         out_off, tot, threads=2)
+    b = OC.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, None, data, ad_off, A, pt_off, L,
+                                        out_off, tot)
+    assert np.array_equal(a, b)

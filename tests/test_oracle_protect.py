@@ -96,3 +96,21 @@ def test_reference_capacity_and_short_input(ref):
     ok, _ = ref.null_encrypt(b"h", b"payload", cap=18)
     assert not ok
     assert not OC.null_decrypt(b"h", b"short")[0] and not ref.null_decrypt(b"h", b"short")[0]
+
+
+def test_reference_batch_equals_oracle_batch(ref):
+    """ref_null_encrypt_batch (the bench's reference CPU baseline) equals the
+    oracle's batch on ragged packets."""
+    rng = np.random.default_rng(23)
+    n = 400
+    L = rng.integers(0, 1453, n).astype(np.uint16)
+    A = rng.integers(0, 40, n).astype(np.uint16)
+    rec = A.astype(np.uint64) + L
+    ad_off = np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.uint64)
+    pt_off = ad_off + A
+    data = rng.integers(0, 256, int(rec.sum()), dtype=np.uint8)
+    out_off = np.concatenate([[0], np.cumsum(L.astype(np.uint64) + 12)[:-1]]).astype(np.uint64)
+    tot = int((L.astype(np.uint64) + 12).sum())
+    a = ref.null_encrypt_batch(data, ad_off, A, pt_off, L, out_off, tot, threads=2)
+    b = OC.null_encrypt_batch(data, ad_off, A, pt_off, L, out_off, tot)
+    assert np.array_equal(a, b)
