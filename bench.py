@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-ragged", action="store_true")
     p.add_argument("--no-protect", action="store_true")
+    p.add_argument("--no-entropy", action="store_true")
     p.add_argument("--no-ceilings", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -287,6 +288,9 @@ def main():
             line["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
         if not args.no_protect:
             line["protect"] = bench_protect(ctx, torch, dev, stream, G, k, L,
+                                            cpu=not args.no_cpu_baseline)
+        if not args.no_entropy:
+            line["entropy"] = bench_entropy(ctx, torch, dev, stream,
                                             cpu=not args.no_cpu_baseline)
         if not args.no_e2e:
             line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
@@ -571,6 +575,104 @@ def _cpu_null_baseline(hdr, L, n, seconds):
             "single_core_value": round(st, 3),
             "sample": f"NULL encrypt of {n} packets ({hdr}+{L} B), {reps_mt} passes on "
                       f"{threads} threads ({what})"}
+
+
+def entropy_workload(C, W, seed=7):
+    """C connections x W-packet windows of sent-packet entropy hashes (random
+    entropy bits, hash = flag << (pn % 8)), one ack per connection with two
+    missing intervals and its true claimed hash (host numpy; the claim is what
+    the peer would send)."""
+    rng = np.random.default_rng(seed)
+    pn0 = rng.integers(1, 1 << 30, C).astype(np.uint64)
+    flags = rng.integers(0, 2, (C, W)).astype(np.uint8)
+    e = (flags << ((pn0[:, None] + np.arange(W, dtype=np.uint64)) % np.uint64(8))
+         .astype(np.uint8)).astype(np.uint8)
+    base = rng.integers(0, 256, C).astype(np.uint8)
+    cum = np.bitwise_xor.accumulate(e, axis=1) ^ base[:, None]
+    off = np.sort(rng.integers(0, W, (C, 4)), axis=1)  # window offsets of 2 intervals
+    off[:, 1] += 1
+    off[:, 3] += 1
+    off[:, 2] = np.maximum(off[:, 2], off[:, 1])
+    off[:, 3] = np.maximum(off[:, 3], off[:, 2] + 1)
+    off = np.minimum(off, W)
+    largest_off = np.full(C, W - 1)
+    rows = np.arange(C)
+
+    def at(o):  # cumulative through window offset o-1 (o = 0: the base)
+        return np.where(o > 0, cum[rows, np.maximum(o - 1, 0)], base)
+    claimed = cum[rows, largest_off] ^ at(off[:, 1]) ^ at(off[:, 0]) ^ at(off[:, 3]) ^ at(off[:, 2])
+    lo = (pn0[:, None] + off[:, [0, 2]].astype(np.uint64)).reshape(-1)
+    hi = (pn0[:, None] + off[:, [1, 3]].astype(np.uint64)).reshape(-1)
+    return {"entropy": e.reshape(-1), "conn_ptr": np.arange(C + 1, dtype=np.uint64) * np.uint64(W),
+            "first_pn": pn0, "cum_base": base, "ack_conn": rows.astype(np.uint32),
+            "largest": pn0 + largest_off.astype(np.uint64), "claimed": claimed.astype(np.uint8),
+            "range_ptr": (np.arange(C + 1) * 2).astype(np.uint32), "range_lo": lo,
+            "range_hi": hi, "cum": cum.reshape(-1)}
+
+
+def bench_entropy(ctx, torch, dev, stream, C=1 << 20, W=128, reps=10, cpu=True):
+    """cumulative entropy of every sent packet of 2^20
+    connections (128-packet windows) + validation of one ack per connection
+    (two missing intervals each), device-resident."""
+    d = entropy_workload(C, W)
+
+    def dv(a):
+        sig = {1: np.uint8, 4: np.int32, 8: np.int64}[a.dtype.itemsize]
+        return torch.from_numpy(np.ascontiguousarray(a).view(sig)).to(dev)
+    t = {k: dv(v) for k, v in d.items() if k != "cum"}
+    cum = torch.empty(C * W, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(C, dtype=torch.uint8, device=dev)
+    scan = lambda: ctx.entropy_cumulative(t["entropy"], t["conn_ptr"], t["cum_base"], C, cum)  # noqa: E731
+    val = lambda: ctx.entropy_validate(cum, t["conn_ptr"], t["first_pn"], t["cum_base"], C,  # noqa: E731
+                                       t["ack_conn"], t["largest"], t["claimed"], t["range_ptr"],
+                                       t["range_lo"], t["range_hi"], C, ok)
+    ms_s = _time_on(torch, stream, scan, reps)
+    ms_v = _time_on(torch, stream, val, reps)
+    ctx.sync()
+    verified = bool(ok.all()) and np.array_equal(cum.cpu().numpy(), d["cum"])
+    # algorithmic bytes: scan reads 1 B + writes 1 B per packet (+ 9 B/connection
+    # of pointers and base); validation reads 8+8+4+1 B per ack, 16 B per
+    # interval, 4 cumulative bytes + 2 window pointers (16 B) and writes 1 B
+    b_scan = C * W * 2 + C * 9
+    b_val = C * (8 + 8 + 4 + 1 + 4 + 2 * 16 + 4 + 16 + 8 + 1 + 1)
+    res = {"connections": C, "window": W, "acks": C,
+           "cumulative_GBps": round(b_scan / (ms_s / 1e3) / 1e9, 1),
+           "cumulative_us": round(ms_s * 1e3, 1),
+           "cumulative_Gpackets_per_s": round(C * W / (ms_s / 1e3) / 1e9, 2),
+           "validate_us": round(ms_v * 1e3, 1),
+           "validate_Macks_per_s": round(C / (ms_v / 1e3) / 1e6, 1),
+           "validate_GBps": round(b_val / (ms_v / 1e3) / 1e9, 1),
+           "bound": "hbm (1-byte hashes; scan: 2 B/packet)", "verified": verified}
+    del t, cum, ok
+    torch.cuda.empty_cache()
+    if cpu:
+        res["cpu_baseline"] = _cpu_entropy_baseline(d, C)
+    return res
+
+
+def _cpu_entropy_baseline(d, C, n=1 << 16, seconds=3.0):
+    """Oracle (reference-pinned restatement of QuicSentEntropyManager's
+    cumulative / IsValidEntropy walk) on one host core over a sample."""
+    from oracle import oracle_c as OC
+    W = int(d["conn_ptr"][1])
+    sub = {"entropy": d["entropy"][:n * W], "conn_ptr": d["conn_ptr"][:n + 1],
+           "first_pn": d["first_pn"][:n], "cum_base": d["cum_base"][:n],
+           "ack_conn": d["ack_conn"][:n], "largest": d["largest"][:n],
+           "claimed": d["claimed"][:n], "range_ptr": d["range_ptr"][:n + 1],
+           "range_lo": d["range_lo"][:2 * n], "range_hi": d["range_hi"][:2 * n]}
+    t0, reps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        cum = OC.entropy_cumulative_batch(sub["entropy"], sub["conn_ptr"], sub["cum_base"])
+        OC.entropy_validate_batch(cum, sub["conn_ptr"], sub["first_pn"], sub["cum_base"],
+                                  sub["ack_conn"], sub["largest"], sub["claimed"],
+                                  sub["range_ptr"], sub["range_lo"], sub["range_hi"])
+        reps += 1
+    el = time.perf_counter() - t0
+    return {"value": round(reps * n * W / el / 1e9, 3), "unit": "Gpackets/s (cumulative + validate)",
+            "cores": 1, "kind": "port",
+            "sample": f"oracle over {n} connections x {W} packets + {n} acks, {reps} passes "
+                      f"(restatement pinned against the reference's QuicSentEntropyManager; "
+                      f"the reference runs it per connection on the connection thread)"}
 
 
 def bench_e2e(ctx, torch, k, L, G=1 << 18):

@@ -224,6 +224,41 @@ int qfec_aes128gcm_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t*
                               const uint16_t* in_len, uint64_t n_packets, uint8_t* out,
                               const uint64_t* out_off, uint8_t* ok, uint32_t flags);
 
+/* ---- packet-entropy bookkeeping (QUIC <= v33) --------------------------- */
+/* The 1-byte entropy hashes the sender records per packet and checks acks
+ * against, batched over connections.  Connection c
+ * holds the hashes of its packets first_pn[c] .. first_pn[c] + n_c - 1 at
+ * entropy[conn_ptr[c] .. conn_ptr[c+1]) — QuicSentEntropyManager's deque after
+ * ClearEntropyBefore(first_pn[c]) — and cum_base[c] is the cumulative entropy
+ * through first_pn[c] - 1 (NULL: 0).  A packet's hash is
+ * entropy_flag << (packet_number % 8) (QuicFramer::GetPacketEntropyHash,
+ * quic_framer.cc:351-354).
+ *
+ * qfec_entropy_cumulative_batch: cum[i] = cum_base[c] ^ entropy[conn_ptr[c]]
+ *   ^ ... ^ entropy[i] — QuicSentEntropyManager::GetCumulativeEntropy for every
+ *   packet (quic_sent_entropy_manager.cc:33-41, :57-66); with 0 for packets not
+ *   received it is the receiver's EntropyTracker::EntropyHash
+ *   (quic_received_packet_manager.cc:40-56).
+ * qfec_entropy_validate_batch: ack a of connection ack_conn[a] with
+ *   largest_observed[a], missing packets as the disjoint intervals
+ *   [range_lo[r], range_hi[r]), r in range_ptr[a] .. range_ptr[a+1] (the
+ *   PacketNumberQueue), and the claimed hash: ok[a] = IsValidEntropy(...)
+ *   (quic_sent_entropy_manager.cc:68-96, called by QuicConnection::
+ *   ValidateAckFrame, quic_connection.cc:854), given `cum` from the first call.
+ *   Where the reference's behaviour is undefined — a missing packet above the
+ *   largest recorded one, largest_observed below the window, ack_conn out of
+ *   range — ok[a] = 0.  An invalid ack is a result (ok = 0), not an error. */
+int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const uint64_t* conn_ptr,
+                                  const uint8_t* cum_base, uint64_t n_conns, uint8_t* cum,
+                                  uint32_t flags);
+int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_t* conn_ptr,
+                                const uint64_t* first_pn, const uint8_t* cum_base,
+                                uint64_t n_conns, const uint32_t* ack_conn,
+                                const uint64_t* largest_observed, const uint8_t* claimed,
+                                const uint32_t* range_ptr, const uint64_t* range_lo,
+                                const uint64_t* range_hi, uint64_t n_acks, uint8_t* ok,
+                                uint32_t flags);
+
 /* ---- measurement support (bench.py, device pointers) ------------------- */
 /* Streaming bandwidth probe over n bytes of src (n rounded down to 16):
  * mode 0 = read only (nt loads, XOR-folded; dst receives at most 16 bytes),

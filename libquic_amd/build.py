@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqfec.so")
 ARCH = os.environ.get("QFEC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["qfec_kernels.hip", "qpp_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc",
+SOURCES = ["qfec_kernels.hip", "qpp_kernels.hip", "qent_kernels.hip", "qfec_capi.cpp", "quic_fec_group.cc",
            "quic_fec_wire.cc", "quic_fec_connection.cc"]
 HEADERS = ["qfec_internal.h", "quic_fec_group.h", "quic_fec_wire.h", "quic_fec_connection.h"]
 

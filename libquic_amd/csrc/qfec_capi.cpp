@@ -888,4 +888,95 @@ int qfec_synth_ragged(qfec_ctx* ctx, uint8_t* bytes, const uint64_t* pkt_off,
   return QFEC_OK;
 }
 
+int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const uint64_t* conn_ptr,
+                                  const uint8_t* cum_base, uint64_t n_conns, uint8_t* cum,
+                                  uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n_conns == 0) return QFEC_OK;
+  if (!entropy || !conn_ptr || !cum) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  qfec::EntropyScanArgs a{entropy, conn_ptr, cum_base, n_conns, cum};
+  if (flags & QFEC_PTR_HOST) {
+    const uint64_t n = conn_ptr[n_conns];
+    DevBuf d_e, d_ptr, d_base, d_cum;
+    QFEC_HIP(ctx, hipMalloc(&d_e.p, n + 1));
+    QFEC_HIP(ctx, hipMalloc(&d_ptr.p, 8 * (n_conns + 1)));
+    QFEC_HIP(ctx, hipMalloc(&d_cum.p, n + 1));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_e.p, entropy, n, hipMemcpyHostToDevice, ctx->stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(d_ptr.p, conn_ptr, 8 * (n_conns + 1), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    if (cum_base) {
+      QFEC_HIP(ctx, hipMalloc(&d_base.p, n_conns));
+      QFEC_HIP(ctx, hipMemcpyAsync(d_base.p, cum_base, n_conns, hipMemcpyHostToDevice,
+                                   ctx->stream));
+    }
+    a.entropy = static_cast<const uint8_t*>(d_e.p);
+    a.conn_ptr = static_cast<const uint64_t*>(d_ptr.p);
+    a.cum_base = static_cast<const uint8_t*>(d_base.p);
+    a.cum = static_cast<uint8_t*>(d_cum.p);
+    QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(cum, d_cum.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return QFEC_OK;
+  }
+  QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_t* conn_ptr,
+                                const uint64_t* first_pn, const uint8_t* cum_base,
+                                uint64_t n_conns, const uint32_t* ack_conn,
+                                const uint64_t* largest_observed, const uint8_t* claimed,
+                                const uint32_t* range_ptr, const uint64_t* range_lo,
+                                const uint64_t* range_hi, uint64_t n_acks, uint8_t* ok,
+                                uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (n_acks == 0) return QFEC_OK;
+  if (!cum || !conn_ptr || !first_pn || !ack_conn || !largest_observed || !claimed ||
+      !range_ptr || !ok || ((!range_lo || !range_hi) && (flags & QFEC_PTR_HOST) &&
+                            range_ptr[n_acks] != range_ptr[0]))
+    return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  qfec::EntropyValidateArgs a{cum, conn_ptr, first_pn, cum_base, n_conns, ack_conn,
+                              largest_observed, claimed, range_ptr, range_lo, range_hi, n_acks,
+                              ok};
+  if (flags & QFEC_PTR_HOST) {
+    const uint64_t n = n_conns ? conn_ptr[n_conns] : 0, nr = range_ptr[n_acks];
+    DevBuf d_cum, d_ptr, d_first, d_base, d_conn, d_larg, d_claim, d_rptr, d_lo, d_hi, d_ok;
+    struct In {
+      DevBuf* d;
+      const void* h;
+      uint64_t bytes;
+    } ins[] = {{&d_cum, cum, n},          {&d_ptr, conn_ptr, 8 * (n_conns + 1)},
+               {&d_first, first_pn, 8 * n_conns}, {&d_base, cum_base, cum_base ? n_conns : 0},
+               {&d_conn, ack_conn, 4 * n_acks}, {&d_larg, largest_observed, 8 * n_acks},
+               {&d_claim, claimed, n_acks},   {&d_rptr, range_ptr, 4 * (n_acks + 1)},
+               {&d_lo, range_lo, 8 * nr},      {&d_hi, range_hi, 8 * nr}};
+    for (auto& i : ins) {
+      if (!i.h) continue;
+      QFEC_HIP(ctx, hipMalloc(&i.d->p, i.bytes + 8));
+      if (i.bytes)
+        QFEC_HIP(ctx, hipMemcpyAsync(i.d->p, i.h, i.bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
+    QFEC_HIP(ctx, hipMalloc(&d_ok.p, n_acks));
+    a.cum = static_cast<const uint8_t*>(d_cum.p);
+    a.conn_ptr = static_cast<const uint64_t*>(d_ptr.p);
+    a.first_pn = static_cast<const uint64_t*>(d_first.p);
+    a.cum_base = static_cast<const uint8_t*>(d_base.p);
+    a.ack_conn = static_cast<const uint32_t*>(d_conn.p);
+    a.largest_observed = static_cast<const uint64_t*>(d_larg.p);
+    a.claimed = static_cast<const uint8_t*>(d_claim.p);
+    a.range_ptr = static_cast<const uint32_t*>(d_rptr.p);
+    a.range_lo = static_cast<const uint64_t*>(d_lo.p);
+    a.range_hi = static_cast<const uint64_t*>(d_hi.p);
+    a.ok = static_cast<uint8_t*>(d_ok.p);
+    QFEC_HIP(ctx, qfec::launch_entropy_validate(a, ctx->stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(ok, d_ok.p, n_acks, hipMemcpyDeviceToHost, ctx->stream));
+    QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return QFEC_OK;
+  }
+  QFEC_HIP(ctx, qfec::launch_entropy_validate(a, ctx->stream));
+  return QFEC_OK;
+}
+
 }  // extern "C"

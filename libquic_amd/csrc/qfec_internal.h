@@ -80,6 +80,34 @@ hipError_t launch_chacha20poly1305(const AeadArgs& a, bool decrypt, hipStream_t 
 // AES-128-GCM (QUIC: 12-byte tag; keys are 16 B each).
 hipError_t launch_aes128gcm(const AeadArgs& a, bool decrypt, hipStream_t s);
 
+// Packet-entropy bookkeeping (qent_kernels.hip); layout as include/qfec.h.
+struct EntropyScanArgs {
+  const uint8_t* entropy;
+  const uint64_t* conn_ptr;  // n_conns + 1
+  const uint8_t* cum_base;   // nullable: 0
+  uint64_t n_conns;
+  uint8_t* cum;
+};
+
+struct EntropyValidateArgs {
+  const uint8_t* cum;
+  const uint64_t* conn_ptr;
+  const uint64_t* first_pn;
+  const uint8_t* cum_base;  // nullable: 0
+  uint64_t n_conns;
+  const uint32_t* ack_conn;
+  const uint64_t* largest_observed;
+  const uint8_t* claimed;
+  const uint32_t* range_ptr;  // n_acks + 1
+  const uint64_t* range_lo;
+  const uint64_t* range_hi;
+  uint64_t n_acks;
+  uint8_t* ok;
+};
+
+hipError_t launch_entropy_scan(const EntropyScanArgs& a, hipStream_t s);
+hipError_t launch_entropy_validate(const EntropyValidateArgs& a, hipStream_t s);
+
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);

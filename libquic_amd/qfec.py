@@ -67,6 +67,11 @@ SIGNATURES = [
     ("qfec_aes128gcm_open_batch", C.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p,
       C.c_uint32]),
+    ("qfec_entropy_cumulative_batch", C.c_int,
+     [_vp, _u8p, _vp, _u8p, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_entropy_validate_batch", C.c_int,
+     [_vp, _u8p, _vp, _vp, _u8p, C.c_uint64, _vp, _vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p,
+      C.c_uint32]),
     ("qfec_stream_probe", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
@@ -262,6 +267,19 @@ class Context:
             self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
             _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
             _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+
+    # -- packet-entropy bookkeeping --------------------------------------------
+    def entropy_cumulative(self, entropy, conn_ptr, cum_base, n_conns, cum, *, host=False):
+        return self._check(self.lib.qfec_entropy_cumulative_batch(
+            self.ctx, _ptr(entropy), _ptr(conn_ptr), _ptr(cum_base), n_conns, _ptr(cum),
+            QFEC_PTR_HOST if host else 0))
+
+    def entropy_validate(self, cum, conn_ptr, first_pn, cum_base, n_conns, ack_conn, largest,
+                         claimed, range_ptr, range_lo, range_hi, n_acks, ok, *, host=False):
+        return self._check(self.lib.qfec_entropy_validate_batch(
+            self.ctx, _ptr(cum), _ptr(conn_ptr), _ptr(first_pn), _ptr(cum_base), n_conns,
+            _ptr(ack_conn), _ptr(largest), _ptr(claimed), _ptr(range_ptr), _ptr(range_lo),
+            _ptr(range_hi), n_acks, _ptr(ok), QFEC_PTR_HOST if host else 0))
 
     def stream_probe(self, src, n, dst, copy=False):
         return self._check(self.lib.qfec_stream_probe(self.ctx, _ptr(src), n, _ptr(dst),

@@ -54,3 +54,59 @@ def ragged_layout(g0, n, kmin=5, kmax=15, lmin=64, lmax=1350, seed=SEED_RAGGED):
     if ln.size > 1:
         off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
     return ks, ptr, ln, off
+
+
+def entropy_batch(rng, n_conns, max_packets=300, acks_per_conn=3, max_ranges=4,
+                  corrupt=0.3):
+    """Synthetic entropy workload (host numpy), ragged: connection c sent
+    packets 1..N_c with random entropy bits (hash = flag << (pn % 8),
+    quic_framer.cc:351-354), its window starts at first_pn[c] (packets before it
+    cleared, their XOR carried in cum_base[c]); each connection gets acks with
+    non-decreasing largest_observed, disjoint missing intervals inside the
+    window, and a claimed hash that is the true one (what a peer that received
+    the acknowledged packets sends) or, with probability `corrupt`, a wrong one.
+    Returns a dict of arrays in the qfec_entropy_* layout plus `full` (the
+    per-connection hashes of packets 1..N_c, for the reference)."""
+    full, first, windows = [], [], []
+    for _ in range(n_conns):
+        n = int(rng.integers(0, max_packets + 1))
+        pn = np.arange(1, n + 1, dtype=np.uint64)
+        flags = rng.integers(0, 2, n).astype(np.uint8)
+        e = (flags << (pn % np.uint64(8)).astype(np.uint8)).astype(np.uint8)
+        f = int(rng.integers(1, n + 2))
+        full.append(e)
+        first.append(f)
+        windows.append(e[f - 1:])
+    conn_ptr = np.zeros(n_conns + 1, np.uint64)
+    conn_ptr[1:] = np.cumsum([w.size for w in windows])
+    entropy = np.concatenate(windows) if n_conns else np.zeros(0, np.uint8)
+    cum_base = np.array([np.bitwise_xor.reduce(e[:f - 1]) if f > 1 else 0
+                         for e, f in zip(full, first)], np.uint8)
+    ack_conn, largest, claimed, rptr, lo, hi = [], [], [], [0], [], []
+    for c, (e, f) in enumerate(zip(full, first)):
+        n = e.size
+        if n < f:
+            continue
+        ls = np.sort(rng.integers(f, n + 1, acks_per_conn))
+        for L in ls:
+            L = int(L)
+            # disjoint intervals in [f, L]
+            cuts = np.sort(rng.choice(np.arange(f, L + 2), size=min(2 * int(rng.integers(0, max_ranges + 1)), L + 2 - f), replace=False)) if L + 2 - f > 0 else []
+            h = int(np.bitwise_xor.reduce(e[:L])) if L else 0
+            for i in range(0, len(cuts) - 1, 2):
+                a, b = int(cuts[i]), int(cuts[i + 1])
+                if a < b:
+                    lo.append(a)
+                    hi.append(b)
+                    h ^= int(np.bitwise_xor.reduce(e[a - 1:b - 1]))
+            rptr.append(len(lo))
+            if rng.random() < corrupt:
+                h ^= int(rng.integers(1, 256))
+            ack_conn.append(c)
+            largest.append(L)
+            claimed.append(h)
+    return {"entropy": entropy, "conn_ptr": conn_ptr, "first_pn": np.array(first, np.uint64),
+            "cum_base": cum_base, "ack_conn": np.array(ack_conn, np.uint32),
+            "largest": np.array(largest, np.uint64), "claimed": np.array(claimed, np.uint8),
+            "range_ptr": np.array(rptr, np.uint32), "range_lo": np.array(lo, np.uint64),
+            "range_hi": np.array(hi, np.uint64), "full": full}

@@ -29,6 +29,13 @@ def lib():
         if not os.path.exists(_SO):
             build()
         L = C.CDLL(_SO)
+        L.qo_entropy_cumulative_batch.restype = None
+        L.qo_entropy_cumulative_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                  C.c_void_p]
+        L.qo_entropy_validate_batch.restype = None
+        L.qo_entropy_validate_batch.argtypes = [C.c_void_p] * 10 + [C.c_uint64, C.c_void_p]
+        L.qo_packet_entropy_hash.restype = C.c_uint8
+        L.qo_packet_entropy_hash.argtypes = [C.c_int, C.c_uint64]
         L.qo_splitmix64.restype = C.c_uint64
         L.qo_splitmix64.argtypes = [C.c_uint64]
         L.qo_synth_fixed.restype = None
@@ -373,3 +380,26 @@ def quic_aes128gcm_decrypt_batch(keys, prefixes, key_idx, packet_number, path_id
         None if path_id is None else _p(path_id), _p(data), _p(ad_off), _p(ad_len), _p(ct_off),
         _p(ct_len), ct_len.size, _p(out), _p(out_off), _p(ok))
     return out, ok
+
+
+# ---- entropy bookkeeping (qent_oracle.c) ------------------------------------
+def packet_entropy_hash(flag, packet_number):
+    return int(lib().qo_packet_entropy_hash(int(bool(flag)), int(packet_number)))
+
+
+def entropy_cumulative_batch(entropy, conn_ptr, cum_base):
+    cum = np.zeros(entropy.size, np.uint8)
+    n = conn_ptr.size - 1
+    lib().qo_entropy_cumulative_batch(_p(entropy), _p(conn_ptr),
+                                      None if cum_base is None else _p(cum_base), n, _p(cum))
+    return cum
+
+
+def entropy_validate_batch(cum, conn_ptr, first_pn, cum_base, ack_conn, largest, claimed,
+                           range_ptr, range_lo, range_hi):
+    ok = np.zeros(ack_conn.size, np.uint8)
+    lib().qo_entropy_validate_batch(_p(cum), _p(conn_ptr), _p(first_pn),
+                                    None if cum_base is None else _p(cum_base), _p(ack_conn),
+                                    _p(largest), _p(claimed), _p(range_ptr), _p(range_lo),
+                                    _p(range_hi), ack_conn.size, _p(ok))
+    return ok

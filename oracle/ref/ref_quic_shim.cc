@@ -162,3 +162,27 @@ REF_API void ref_quic_aes128gcm_seal_batch(const uint8_t* keys, const uint8_t* p
     }
   });
 }
+
+// ---- entropy bookkeeping (QuicSentEntropyManager) --------------------------
+#include "net/quic/core/quic_sent_entropy_manager.h"
+
+// One connection's sender: RecordPacketEntropyHash for packets 1..n_total
+// (entropy[pn-1]), ClearEntropyBefore(first_pn), then GetCumulativeEntropy
+// for first_pn..n_total into cum (n_total - first_pn + 1 bytes), then the
+// IsValidEntropy queries in the given (non-decreasing largest) order: query q
+// has missing intervals [lo[r], hi[r]) for r in range_ptr[q]..range_ptr[q+1].
+REF_API void ref_sent_entropy_run(const uint8_t* entropy, uint64_t n_total, uint64_t first_pn,
+                                  uint8_t* cum, uint64_t n_q, const uint64_t* largest,
+                                  const uint8_t* claimed, const uint32_t* range_ptr,
+                                  const uint64_t* lo, const uint64_t* hi, uint8_t* ok) {
+  net::QuicSentEntropyManager m;
+  for (uint64_t pn = 1; pn <= n_total; ++pn) m.RecordPacketEntropyHash(pn, entropy[pn - 1]);
+  if (first_pn > 1) m.ClearEntropyBefore(first_pn);
+  for (uint64_t pn = first_pn; pn <= n_total; ++pn)
+    cum[pn - first_pn] = m.GetCumulativeEntropy(pn);
+  for (uint64_t q = 0; q < n_q; ++q) {
+    net::PacketNumberQueue missing;
+    for (uint32_t r = range_ptr[q]; r < range_ptr[q + 1]; ++r) missing.Add(lo[r], hi[r]);
+    ok[q] = m.IsValidEntropy(largest[q], missing, claimed[q]) ? 1 : 0;
+  }
+}

@@ -59,6 +59,9 @@ def lib():
         L.ref_quic_aes128gcm_seal_batch.restype = None
         L.ref_quic_aes128gcm_seal_batch.argtypes = [C.c_void_p] * 4 + [C.c_uint32] + \
             [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.ref_sent_entropy_run.restype = None
+        L.ref_sent_entropy_run.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                           C.c_uint64] + [C.c_void_p] * 6
         _lib = L
     return _lib
 
@@ -163,3 +166,16 @@ def quic_aes128gcm_encrypt_batch(keys, prefixes, key_idx, packet_number, data, a
                                         _pa(ad_len), _pa(pt_off), _pa(pt_len), pt_len.size,
                                         _pa(out), _pa(out_off), threads)
     return out
+
+
+def sent_entropy_run(entropy, first_pn, largest, claimed, range_ptr, lo, hi):
+    """QuicSentEntropyManager (quic_sent_entropy_manager.cc) of one connection:
+    record packets 1..len(entropy), ClearEntropyBefore(first_pn),
+    GetCumulativeEntropy(first_pn..), then IsValidEntropy per query."""
+    e = np.ascontiguousarray(entropy, np.uint8)
+    n = e.size
+    cum = np.zeros(max(n - first_pn + 1, 1), np.uint8)
+    ok = np.zeros(max(largest.size, 1), np.uint8)
+    lib().ref_sent_entropy_run(_pa(e), n, first_pn, _pa(cum), largest.size, _pa(largest),
+                               _pa(claimed), _pa(range_ptr), _pa(lo), _pa(hi), _pa(ok))
+    return cum[:n - first_pn + 1], ok[:largest.size]
