@@ -622,7 +622,8 @@ def bench_entropy(ctx, torch, dev, stream, C=1 << 20, W=128, reps=10, cpu=True):
     t = {k: dv(v) for k, v in d.items() if k != "cum"}
     cum = torch.empty(C * W, dtype=torch.uint8, device=dev)
     ok = torch.zeros(C, dtype=torch.uint8, device=dev)
-    scan = lambda: ctx.entropy_cumulative(t["entropy"], t["conn_ptr"], t["cum_base"], C, cum)  # noqa: E731
+    scan = lambda: ctx.entropy_cumulative(t["entropy"], t["conn_ptr"], t["cum_base"], C, cum,  # noqa: E731
+                                          n_packets=C * W)
     val = lambda: ctx.entropy_validate(cum, t["conn_ptr"], t["first_pn"], t["cum_base"], C,  # noqa: E731
                                        t["ack_conn"], t["largest"], t["claimed"], t["range_ptr"],
                                        t["range_lo"], t["range_hi"], C, ok)

@@ -238,7 +238,9 @@ int qfec_aes128gcm_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t*
  *   ^ ... ^ entropy[i] — QuicSentEntropyManager::GetCumulativeEntropy for every
  *   packet (quic_sent_entropy_manager.cc:33-41, :57-66); with 0 for packets not
  *   received it is the receiver's EntropyTracker::EntropyHash
- *   (quic_received_packet_manager.cc:40-56).
+ *   (quic_received_packet_manager.cc:40-56).  n_packets = conn_ptr[n_conns] -
+ *   conn_ptr[0] is a launch-shape hint (lanes per connection from the mean
+ *   window); 0 = unknown.  It never changes the result.
  * qfec_entropy_validate_batch: ack a of connection ack_conn[a] with
  *   largest_observed[a], missing packets as the disjoint intervals
  *   [range_lo[r], range_hi[r]), r in range_ptr[a] .. range_ptr[a+1] (the
@@ -249,8 +251,8 @@ int qfec_aes128gcm_open_batch(qfec_ctx* ctx, const uint8_t* keys, const uint8_t*
  *   largest recorded one, largest_observed below the window, ack_conn out of
  *   range — ok[a] = 0.  An invalid ack is a result (ok = 0), not an error. */
 int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const uint64_t* conn_ptr,
-                                  const uint8_t* cum_base, uint64_t n_conns, uint8_t* cum,
-                                  uint32_t flags);
+                                  const uint8_t* cum_base, uint64_t n_conns, uint64_t n_packets,
+                                  uint8_t* cum, uint32_t flags);
 int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_t* conn_ptr,
                                 const uint64_t* first_pn, const uint8_t* cum_base,
                                 uint64_t n_conns, const uint32_t* ack_conn,

@@ -889,8 +889,8 @@ int qfec_synth_ragged(qfec_ctx* ctx, uint8_t* bytes, const uint64_t* pkt_off,
 }
 
 int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const uint64_t* conn_ptr,
-                                  const uint8_t* cum_base, uint64_t n_conns, uint8_t* cum,
-                                  uint32_t flags) {
+                                  const uint8_t* cum_base, uint64_t n_conns, uint64_t n_packets,
+                                  uint8_t* cum, uint32_t flags) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (n_conns == 0) return QFEC_OK;
@@ -914,12 +914,12 @@ int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const u
     a.conn_ptr = static_cast<const uint64_t*>(d_ptr.p);
     a.cum_base = static_cast<const uint8_t*>(d_base.p);
     a.cum = static_cast<uint8_t*>(d_cum.p);
-    QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream));
+    QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream, n - conn_ptr[0]));
     QFEC_HIP(ctx, hipMemcpyAsync(cum, d_cum.p, n, hipMemcpyDeviceToHost, ctx->stream));
     QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return QFEC_OK;
   }
-  QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream));
+  QFEC_HIP(ctx, qfec::launch_entropy_scan(a, ctx->stream, n_packets));
   return QFEC_OK;
 }
 

@@ -105,7 +105,9 @@ struct EntropyValidateArgs {
   uint8_t* ok;
 };
 
-hipError_t launch_entropy_scan(const EntropyScanArgs& a, hipStream_t s);
+// total_bytes = conn_ptr[n_conns] - conn_ptr[0] (host-known: picks lanes per
+// connection), or 0 when unknown.
+hipError_t launch_entropy_scan(const EntropyScanArgs& a, hipStream_t s, uint64_t total_bytes);
 hipError_t launch_entropy_validate(const EntropyValidateArgs& a, hipStream_t s);
 
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)

@@ -163,6 +163,17 @@ struct StageMeta {
   uint32_t nfull;      // full 16-B chunks
 };
 
+// The staged rows pass data between lanes of one wave through LDS: the LDS
+// executes a wave's accesses in program order, so no hardware wait is needed,
+// but the compiler must not move a lane's own-row access across another
+// lane's cooperative access (it sees no aliasing for the single lane).
+// Wavefront-scope fences around a wave barrier pin that order (no s_waitcnt).
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Cooperative load of slab `sl` (SC chunks per packet) for the wave's 64
 // packets: lane (SC*i + m) of instruction I takes chunk m of packet
 // (64/SC)*I + i; SC instructions cover the 64 packets.
@@ -171,11 +182,13 @@ __device__ __forceinline__ void stage_load(const StageMeta* meta, uint32_t lane,
                                            u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
   const uint32_t c = sl * SC + m;
+  wave_lds_order();  // the lanes' meta entries are written (cross-lane reads follow)
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
     if (c < q.nfull) v[I] = ld16(q.src + 16u * c);
   }
+  wave_lds_order();
 }
 
 template <uint32_t SC>
@@ -183,11 +196,13 @@ __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane
                                             const u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
   const uint32_t c = sl * SC + m;
+  wave_lds_order();
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
     if (c < q.nfull && q.dst) st16(q.dst + 16u * c, v[I]);
   }
+  wave_lds_order();  // before a lane rewrites its meta entry
 }
 
 // LDS rows of SC + 1 chunks (16 B of padding: the hashing lanes' ds_read_b128
@@ -195,8 +210,10 @@ __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane
 template <uint32_t SC>
 __device__ __forceinline__ void stage_to_lds(u32x4* rows, uint32_t lane, const u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
+  wave_lds_order();  // earlier reads of the rows (own row, stage_from_lds) first
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) rows[((64u / SC) * I + i) * (SC + 1u) + m] = v[I];
+  wave_lds_order();  // then the lanes read their own rows
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -481,8 +498,10 @@ __device__ __forceinline__ u32x4 ks_chunk(const uint32_t (&ks)[16], uint32_t j) 
 template <uint32_t SC>
 __device__ __forceinline__ void stage_from_lds(const u32x4* rows, uint32_t lane, u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
+  wave_lds_order();  // the lanes' writes to their own rows first
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) v[I] = rows[((64u / SC) * I + i) * (SC + 1u) + m];
+  wave_lds_order();
 }
 
 __device__ __forceinline__ ChachaKey load_key(const AeadArgs& a, uint64_t p) {
@@ -1038,14 +1057,90 @@ __device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, ui
   }
 }
 
-// 512-thread blocks: the 64 KiB table is shared by 8 waves; LDS 152 KiB per
-// block = one block per CU = 2 waves/SIMD (the VGPR budget allows 2 as well).
-constexpr int kGcmBlock = 512;
-constexpr int kGcmWaves = kGcmBlock / 64;
-constexpr int kGcmNB = 4;  // chunks per step of the payload passes
+// 768-thread blocks: the 64 KiB table is shared by 12 waves with 64-B slabs
+// (SC = 4): LDS 154 KiB per block = one block per CU = 3 waves/SIMD, which the
+// key-uniform path's SGPR round keys make fit in 168 VGPRs (148 used).
+// Measured vs 512 threads / SC = 8 / 2 waves: seal +6.5%, open +1.3%
+// (profiles/round1/tune_gcm_g8.txt).
+constexpr int kGcmBlock = 768;
+constexpr int kGcmSC = 4;   // 16-B chunks per packet per slab
+constexpr int kGcmWPE = 3;  // waves per SIMD
+constexpr int kGcmNB = 4;   // chunks per step of the payload passes
 
-template <uint32_t SC, bool OPEN>
-__global__ __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void aes128gcm_kernel(AeadArgs a) {
+// Everything after the key setup, for one packet per lane.  Instantiated
+// twice in the kernel when UNI: with the key-uniform wave's round keys as
+// wave-uniform values (SGPRs, 44 VGPRs freed) and with per-lane keys.
+template <uint32_t SC, bool OPEN, int NB>
+__device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
+                                           const uint32_t (&nonce)[3], Ghash& gh,
+                                           const uint32_t* s_te, uint32_t copy, StageMeta* meta,
+                                           u32x4* rows, uint32_t lane, uint64_t p, bool valid,
+                                           const uint8_t* ad, const uint8_t* in, uint32_t alen,
+                                           uint32_t plen) {
+  StageMeta* const s_meta_w = meta;
+  u32x4* const s_rows_w = rows;
+
+  u32x4 tail = {0u, 0u, 0u, 0u};
+  if (valid) {
+    ghash_span_padded(gh, ad, alen);
+    tail = tail_bytes(load_tail(in, plen), plen);  // before any store (in place)
+  }
+  const uint32_t rem = plen & 15u, ctail = plen >> 4;
+  if constexpr (!OPEN) {
+    uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta_w[lane] = StageMeta{in, o, plen >> 4};
+    gcm_pass<SC, NB, true, false, true>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+                                    plen >> 4, true);
+    if (!valid) return;
+    if (rem) {
+      u32x4 ct = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
+      uint8_t b[16];
+      __builtin_memcpy(b, &ct, 16);
+      for (uint32_t i = rem; i < 16u; ++i) b[i] = 0;  // zero pad for GHASH
+      __builtin_memcpy(&ct, b, 16);
+      ghash_block(gh, ct);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
+    }
+    ghash_lengths(gh, alen, plen);
+    const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
+                                  copy);  // E_K(J0)
+    const u32x4 t = gf_to_block(gh.y) ^ ek0;
+    const uint32_t tag[3] = {t.x, t.y, t.z};
+    __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
+  } else {
+    uint32_t want[3] = {0u, 0u, 0u};
+    if (valid) __builtin_memcpy(want, in + plen, kTag);
+    s_meta_w[lane] = StageMeta{in, nullptr, plen >> 4};
+    gcm_pass<SC, NB, false, true, false>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+                                     plen >> 4, false);
+    bool ok = false;
+    if (valid) {
+      if (rem) ghash_block(gh, tail);  // zero padded
+      ghash_lengths(gh, alen, plen);
+      const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
+                                    copy);
+      const u32x4 t = gf_to_block(gh.y) ^ ek0;
+      ok = ((t.x ^ want[0]) | (t.y ^ want[1]) | (t.z ^ want[2])) == 0u;
+      a.io.ok[p] = ok ? 1 : 0;
+    }
+    uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta_w[lane] = StageMeta{in, o, ok ? plen >> 4 : 0u};
+    gcm_pass<SC, NB, true, false, false>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+                                     ok ? plen >> 4 : 0u, true);
+    if (ok && rem) {
+      const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
+      uint8_t b[16];
+      __builtin_memcpy(b, &pt, 16);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
+    }
+  }
+}
+
+template <uint32_t SC, bool OPEN, int NB = kGcmNB, int BLOCK = kGcmBlock, int WPE = kGcmWPE,
+          bool UNI = true>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
+aes128gcm_kernel(AeadArgs a) {
+  constexpr int kGcmWaves = BLOCK / 64;
   // one LDS object with the table first: it sits at LDS address 0, so the
   // v_perm result IS the lookup address (no base add per lookup)
   struct Smem {
@@ -1060,14 +1155,14 @@ __global__ __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   auto& s_meta = sm.meta;
   auto& s_tab = sm.tab;
   // replicated Te0, 16-B stores (every thread of the block helps, then a barrier)
-  for (uint32_t i = threadIdx.x; i < kTeBytes / 16u; i += kGcmBlock) {
+  for (uint32_t i = threadIdx.x; i < kTeBytes / 16u; i += BLOCK) {
     const uint32_t e = kTe0[i >> 4];
     reinterpret_cast<u32x4*>(s_te)[i] = u32x4{e, e, e, e};
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t copy = lane * 4u;  // the lane's byte column in every table row
-  const uint64_t p = (uint64_t)blockIdx.x * kGcmBlock + threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t inl = p < a.io.n ? a.io.in_len[p] : 0u;
   const bool valid = p < a.io.n && (!OPEN || inl >= kTag);
   if (OPEN && p < a.io.n && !valid) a.io.ok[p] = 0;  // open: in_len < tag_len
@@ -1098,8 +1193,8 @@ __global__ __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   gh.y = Gf4{{0u, 0u, 0u, 0u}};
   gh.tab = nullptr;
   const uint64_t vmask = __ballot(valid);
+  const int src = vmask ? __builtin_ctzll(vmask) : 0;  // first valid lane
   if (vmask != 0ull) {
-    const int src = __builtin_ctzll(vmask);  // first valid lane
     const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)kidx, src);
     if (__ballot(valid && kidx != k0) == 0ull) {
       Gf4 h;
@@ -1114,59 +1209,15 @@ __global__ __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
       gh.tab = s_tab[wv];
     }
   }
-  u32x4 tail = {0u, 0u, 0u, 0u};
-  if (valid) {
-    ghash_span_padded(gh, ad, alen);
-    tail = tail_bytes(load_tail(in, plen), plen);  // before any store (in place)
-  }
-  const uint32_t rem = plen & 15u, ctail = plen >> 4;
-  if constexpr (!OPEN) {
-    uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
-    s_meta[wv][lane] = StageMeta{in, o, plen >> 4};
-    gcm_pass<SC, kGcmNB, true, false, true>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
-                                    plen >> 4, true);
-    if (!valid) return;
-    if (rem) {
-      u32x4 ct = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
-      uint8_t b[16];
-      __builtin_memcpy(b, &ct, 16);
-      for (uint32_t i = rem; i < 16u; ++i) b[i] = 0;  // zero pad for GHASH
-      __builtin_memcpy(&ct, b, 16);
-      ghash_block(gh, ct);
-      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
-    }
-    ghash_lengths(gh, alen, plen);
-    const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
-                                  copy);  // E_K(J0)
-    const u32x4 t = gf_to_block(gh.y) ^ ek0;
-    const uint32_t tag[3] = {t.x, t.y, t.z};
-    __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
+  if (UNI && gh.tab) {
+    AesKey ks;  // the wave's key as uniform values
+#pragma unroll
+    for (int i = 0; i < 44; ++i) ks.rk[i] = (uint32_t)__builtin_amdgcn_readlane((int)key.rk[i], src);
+    gcm_packet<SC, OPEN, NB>(a, ks, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane, p, valid,
+                             ad, in, alen, plen);
   } else {
-    uint32_t want[3] = {0u, 0u, 0u};
-    if (valid) __builtin_memcpy(want, in + plen, kTag);
-    s_meta[wv][lane] = StageMeta{in, nullptr, plen >> 4};
-    gcm_pass<SC, kGcmNB, false, true, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
-                                     plen >> 4, false);
-    bool ok = false;
-    if (valid) {
-      if (rem) ghash_block(gh, tail);  // zero padded
-      ghash_lengths(gh, alen, plen);
-      const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
-                                    copy);
-      const u32x4 t = gf_to_block(gh.y) ^ ek0;
-      ok = ((t.x ^ want[0]) | (t.y ^ want[1]) | (t.z ^ want[2])) == 0u;
-      a.io.ok[p] = ok ? 1 : 0;
-    }
-    uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
-    s_meta[wv][lane] = StageMeta{in, o, ok ? plen >> 4 : 0u};
-    gcm_pass<SC, kGcmNB, true, false, false>(key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
-                                     ok ? plen >> 4 : 0u, true);
-    if (ok && rem) {
-      const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
-      uint8_t b[16];
-      __builtin_memcpy(b, &pt, 16);
-      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
-    }
+    gcm_packet<SC, OPEN, NB>(a, key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane, p,
+                             valid, ad, in, alen, plen);
   }
 }
 
@@ -1231,10 +1282,9 @@ hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t
 
 namespace qfec {
 
-// AES-128-GCM slab: 128 B (8 chunks) per packet per slab — round keys (44
-// VGPRs) and GHASH state take the registers a larger slab buffer would need.
+// AES-128-GCM: 64-B slabs at 3 waves/SIMD (see kGcmBlock).
 hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
-  constexpr uint32_t SC = 8;
+  constexpr uint32_t SC = kGcmSC;
   const uint64_t chunk = (uint64_t)0x7FFFFFFF * kGcmBlock;
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;

@@ -68,7 +68,7 @@ SIGNATURES = [
      [_vp, _vp, _vp, _vp, _vp, _vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _u8p,
       C.c_uint32]),
     ("qfec_entropy_cumulative_batch", C.c_int,
-     [_vp, _u8p, _vp, _u8p, C.c_uint64, _u8p, C.c_uint32]),
+     [_vp, _u8p, _vp, _u8p, C.c_uint64, C.c_uint64, _u8p, C.c_uint32]),
     ("qfec_entropy_validate_batch", C.c_int,
      [_vp, _u8p, _vp, _vp, _u8p, C.c_uint64, _vp, _vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p,
       C.c_uint32]),
@@ -269,10 +269,11 @@ class Context:
             _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
 
     # -- packet-entropy bookkeeping --------------------------------------------
-    def entropy_cumulative(self, entropy, conn_ptr, cum_base, n_conns, cum, *, host=False):
+    def entropy_cumulative(self, entropy, conn_ptr, cum_base, n_conns, cum, *, n_packets=0,
+                           host=False):
         return self._check(self.lib.qfec_entropy_cumulative_batch(
-            self.ctx, _ptr(entropy), _ptr(conn_ptr), _ptr(cum_base), n_conns, _ptr(cum),
-            QFEC_PTR_HOST if host else 0))
+            self.ctx, _ptr(entropy), _ptr(conn_ptr), _ptr(cum_base), n_conns, n_packets,
+            _ptr(cum), QFEC_PTR_HOST if host else 0))
 
     def entropy_validate(self, cum, conn_ptr, first_pn, cum_base, n_conns, ack_conn, largest,
                          claimed, range_ptr, range_lo, range_hi, n_acks, ok, *, host=False):

@@ -27,7 +27,7 @@ def dv(a):
     return torch.from_numpy(a.view(sig).copy()).to(DEV)
 
 
-def run_gpu(ctx, d, host=False):
+def run_gpu(ctx, d, host=False, mean_hint=None):
     n_conns = d["conn_ptr"].size - 1
     n_acks = d["ack_conn"].size
     if host:
@@ -43,7 +43,9 @@ def run_gpu(ctx, d, host=False):
                                "largest", "claimed", "range_ptr", "range_lo", "range_hi")}
     cum = torch.zeros(max(d["entropy"].size, 1), dtype=torch.uint8, device=DEV)
     ok = torch.full((max(n_acks, 1),), 7, dtype=torch.uint8, device=DEV)
-    ctx.entropy_cumulative(t["entropy"], t["conn_ptr"], t["cum_base"], n_conns, cum)
+    hint = 0 if mean_hint is None else mean_hint * n_conns  # launch shape only
+    ctx.entropy_cumulative(t["entropy"], t["conn_ptr"], t["cum_base"], n_conns, cum,
+                           n_packets=hint)
     ctx.entropy_validate(cum, t["conn_ptr"], t["first_pn"], t["cum_base"], n_conns, t["ack_conn"],
                          t["largest"], t["claimed"], t["range_ptr"], t["range_lo"], t["range_hi"],
                          n_acks, ok)
@@ -67,11 +69,12 @@ def test_reference_fixture(ctx, host):
     assert np.array_equal(ok, g["ref_ok"])
 
 
+@pytest.mark.parametrize("mean_hint", [None, 100, 200, 400, 1000])  # 8/16/32/64 lanes/conn
 @pytest.mark.parametrize("seed,max_packets", [(11, 50), (12, 700), (13, 3000)])
-def test_random_ragged_vs_oracle(ctx, seed, max_packets):
+def test_random_ragged_vs_oracle(ctx, seed, max_packets, mean_hint):
     rng = np.random.default_rng(seed)
     d = synth.entropy_batch(rng, 257, max_packets=max_packets, acks_per_conn=3, max_ranges=5)
-    cum, ok = run_gpu(ctx, d)
+    cum, ok = run_gpu(ctx, d, mean_hint=mean_hint)
     rc, rok = oracle(d)
     assert np.array_equal(cum, rc)
     assert np.array_equal(ok, rok)
@@ -100,7 +103,7 @@ def test_large_batch_accumulate(ctx):
     d["range_ptr"] = np.zeros(2 * C + 1, np.uint32)
     d["range_lo"] = np.zeros(0, np.uint64)
     d["range_hi"] = np.zeros(0, np.uint64)
-    cum, ok = run_gpu(ctx, d)
+    cum, ok = run_gpu(ctx, d, mean_hint=W)
     assert np.array_equal(cum, want.reshape(-1))
     assert ok[:C].all() and not ok[C:].any()
 

@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 21);
   const int reps = argc > 2 ? atoi(argv[2]) : 3, rounds = 3;
   const uint32_t L = 1350, H = 22;
-  constexpr uint32_t SC = 8;
+  constexpr uint32_t SC = qfec::kGcmSC;
   std::vector<uint64_t> ad_off(n), in_off(n), out_off(n), cad_off(n), cct_off(n), dout_off(n);
   std::vector<uint16_t> ad_len(n, H), in_len(n, L), ct_len(n, L + 12);
   for (uint64_t p = 0; p < n; ++p) {
@@ -116,13 +116,13 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((qfec::aes128gcm_kernel<SC, false>), dim3(ggrid), dim3(gb), 0, 0, a);
   };
   auto seal_old = [&](const qfec::AeadArgs& a) {
-    hipLaunchKernelGGL((qfec::gcm_v1::aes128gcm_kernel<SC, false>), dim3(grid), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((qfec::gcm_v1::aes128gcm_kernel<8, false>), dim3(grid), dim3(256), 0, 0, a);
   };
   auto open_new = [&](const qfec::AeadArgs& a) {
     hipLaunchKernelGGL((qfec::aes128gcm_kernel<SC, true>), dim3(ggrid), dim3(gb), 0, 0, a);
   };
   auto open_old = [&](const qfec::AeadArgs& a) {
-    hipLaunchKernelGGL((qfec::gcm_v1::aes128gcm_kernel<SC, true>), dim3(grid), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((qfec::gcm_v1::aes128gcm_kernel<8, true>), dim3(grid), dim3(256), 0, 0, a);
   };
   int bad = 0;
   // correctness: new vs old seal, key-uniform and mixed-key; open(seal) ok
@@ -157,6 +157,92 @@ int main(int argc, char** argv) {
     bad |= good != n;
     if (kmix) CK(hipFree(kmix));
   }
+  {  // the 3-wave variant against the product, one key and mixed keys
+    for (int mix = 0; mix < 2; ++mix) {
+      qfec::AeadArgs a = as, r = as_ref;
+      uint32_t* kmix = mix ? up(kidx_mix) : nullptr;
+      if (mix) a.key_idx = r.key_idx = kmix;
+      CK(hipMemset(d_out_ref, 0xFF, n * (L + 12)));
+      seal_new(a);
+      hipLaunchKernelGGL((qfec::aes128gcm_kernel<4, false, 4, 768, 3, true>),
+                         dim3((uint32_t)((n + 767) / 768)), dim3(768), 0, 0, r);
+      CK(hipDeviceSynchronize());
+      const auto x = down(d_out, n * (L + 12)), y = down(d_out_ref, n * (L + 12));
+      const bool same = x == y;
+      std::printf("seal 768/wpe3 variant %s == product: %s\n", mix ? "mixed-key" : "one-key",
+                  same ? "yes" : "NO");
+      bad |= !same;
+      if (kmix) CK(hipFree(kmix));
+    }
+  }
+  {  // random lengths (payload 0..1452, header 0..59), 69 keys / 5 keys / 1 key:
+     // every variant against the first kernel
+    const uint64_t rn = 4096;
+    std::vector<uint64_t> r_ad_off(rn), r_in_off(rn), r_out_off(rn);
+    std::vector<uint16_t> r_ad_len(rn), r_in_len(rn);
+    uint64_t pos = 0, opos = 0, st = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint64_t m) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st % m; };
+    for (uint64_t p = 0; p < rn; ++p) {
+      r_ad_len[p] = (uint16_t)rnd(60);
+      r_in_len[p] = (uint16_t)rnd(1453);
+      r_ad_off[p] = pos;
+      pos += r_ad_len[p] + rnd(9);
+      r_in_off[p] = pos;
+      pos += r_in_len[p] + rnd(9);
+      r_out_off[p] = opos;
+      opos += r_in_len[p] + 12;
+    }
+    qfec::AeadArgs ra = as;
+    ra.io.ad_off = up(r_ad_off);
+    ra.io.ad_len = up(r_ad_len);
+    ra.io.in_off = up(r_in_off);
+    ra.io.in_len = up(r_in_len);
+    ra.io.out_off = up(r_out_off);
+    ra.io.n = rn;
+    for (uint32_t nk : {1u, 5u, 7u}) {
+      std::vector<uint32_t> kk(rn);
+      for (uint64_t p = 0; p < rn; ++p) kk[p] = nk == 1 ? 0u : (uint32_t)rnd(nk);
+      uint32_t* dk = up(kk);
+      ra.key_idx = dk;
+      qfec::AeadArgs rr = ra;
+      rr.io.out = d_out_ref;
+      CK(hipMemset(d_out_ref, 0xFF, opos));
+      hipLaunchKernelGGL((qfec::gcm_v1::aes128gcm_kernel<8, false>), dim3((uint32_t)((rn + 255) / 256)),
+                         dim3(256), 0, 0, rr);
+      CK(hipDeviceSynchronize());
+      const auto want = down(d_out_ref, opos);
+      struct RV { const char* name; std::function<void()> run; };
+      std::vector<RV> rvs = {
+          {"product", [&] { seal_new(ra); }},
+          {"SC8 512 wpe2 uni", [&] { hipLaunchKernelGGL((qfec::aes128gcm_kernel<8, false, 4, 512, 2, true>), dim3((uint32_t)((rn + 511) / 512)), dim3(512), 0, 0, ra); }},
+          {"SC8 512 wpe2 lane", [&] { hipLaunchKernelGGL((qfec::aes128gcm_kernel<8, false, 4, 512, 2, false>), dim3((uint32_t)((rn + 511) / 512)), dim3(512), 0, 0, ra); }},
+          {"SC4 512 wpe2 uni", [&] { hipLaunchKernelGGL((qfec::aes128gcm_kernel<4, false, 4, 512, 2, true>), dim3((uint32_t)((rn + 511) / 512)), dim3(512), 0, 0, ra); }},
+          {"SC4 768 wpe3 lane", [&] { hipLaunchKernelGGL((qfec::aes128gcm_kernel<4, false, 4, 768, 3, false>), dim3((uint32_t)((rn + 767) / 768)), dim3(768), 0, 0, ra); }},
+          {"SC4 768 wpe3 NB2", [&] { hipLaunchKernelGGL((qfec::aes128gcm_kernel<4, false, 2, 768, 3, true>), dim3((uint32_t)((rn + 767) / 768)), dim3(768), 0, 0, ra); }},
+      };
+      for (auto& v : rvs) {
+        CK(hipMemset(d_out, 0, opos));
+        v.run();
+        CK(hipDeviceSynchronize());
+        const auto got = down(d_out, opos);
+        uint64_t diff = 0, ctdiff = 0, shown = 0;
+        for (uint64_t p = 0; p < rn; ++p)
+          if (std::memcmp(&got[r_out_off[p]], &want[r_out_off[p]], r_in_len[p] + 12) != 0) {
+            ++diff;
+            uint32_t j = 0;
+            while (got[r_out_off[p] + j] == want[r_out_off[p] + j]) ++j;
+            if (j < r_in_len[p]) ++ctdiff;
+            if (shown++ < 3)
+              std::printf("   packet %llu len %u (nfull %u): first differing byte %u\n",
+                          (unsigned long long)p, r_in_len[p], r_in_len[p] / 16u, j);
+          }
+        if (diff) std::printf("   %llu of them differ in the ciphertext\n", (unsigned long long)ctdiff);
+        std::printf("random batch %u keys, %-20s differing packets: %llu / %llu\n", nk, v.name,
+                    (unsigned long long)diff, (unsigned long long)rn);
+      }
+      CK(hipFree(dk));
+    }
+  }
   // d_cat now holds the mixed-key ciphertexts: rebuild it for the one-key timing
   seal_new(as);
   CK(hipMemcpy2D(d_cat + H, H + L + 12, d_out, L + 12, L + 12, n, hipMemcpyDeviceToDevice));
@@ -167,11 +253,20 @@ int main(int argc, char** argv) {
     std::function<void()> run;
   };
   const double enc_b = (double)n * (H + L + L + 12), dec_b = (double)n * (H + L + 12 + L);
+#define GCMV(NAME, BYTES, ARGS, SCV, OPENV, NBV, BLK, WPE, UNI)                             \
+  {NAME, BYTES, [&] {                                                                      \
+     hipLaunchKernelGGL((qfec::aes128gcm_kernel<SCV, OPENV, NBV, BLK, WPE, UNI>),          \
+                        dim3((uint32_t)((n + BLK - 1) / BLK)), dim3(BLK), 0, 0, ARGS);     \
+   }}
   std::vector<V> vs = {
       {"seal product", enc_b, [&] { seal_new(as); }},
       {"seal first kernel", enc_b, [&] { seal_old(as); }},
       {"open product", dec_b, [&] { open_new(ao); }},
       {"open first kernel", dec_b, [&] { open_old(ao); }},
+      GCMV("seal SC8 512 wpe2 per-lane keys", enc_b, as, 8, false, 4, 512, 2, false),
+      GCMV("seal SC4 768 wpe3 uniform keys", enc_b, as, 4, false, 4, 768, 3, true),
+      GCMV("seal SC4 768 wpe3 NB2", enc_b, as, 4, false, 2, 768, 3, true),
+      GCMV("open SC4 768 wpe3 uniform keys", dec_b, ao, 4, true, 4, 768, 3, true),
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
