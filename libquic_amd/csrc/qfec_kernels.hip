@@ -264,6 +264,16 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// The group's LDS state (accumulator, start mask, packet table) passes data
+// between lanes of one wave.  The LDS executes a wave's accesses in program
+// order; wavefront-scope fences around a wave barrier keep the compiler from
+// moving one lane's access across another lane's (no s_waitcnt emitted).
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Inclusive prefix sum over the wave.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 #pragma unroll
@@ -437,12 +447,15 @@ __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, ui
     const uint32_t S = incl - n;
     const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t nit = (W + 63u) >> 6;
+    wave_lds_order();  // accumulator initialised / previous chunk's table reads done
     for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
+    wave_lds_order();
     if (r < kr) {
       meta[lane] = u32x4{offlo, offhi, len, S};
       __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
+    wave_lds_order();  // packet table and start mask complete
     const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
     const uint32_t last = min(kr - c, 64u) - 1u;
     uint32_t before = 0;  // packet starts in earlier wave-iterations
@@ -500,6 +513,7 @@ __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, ui
     plen = wave_max11(mx);
     if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
   }
+  wave_lds_order();  // every lane's XORs into the accumulator done
   uint8_t* dst = a.out + f.dst_off;
   if (plen >= 16u) {
     const uint32_t nw = (plen + 15u) >> 4;
