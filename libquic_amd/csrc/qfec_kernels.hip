@@ -77,17 +77,25 @@ __device__ __forceinline__ uint32_t wave_max11(uint32_t v) {
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
+// XCD-aware workgroup order (MI355X_MICROARCH.md, workgroup dispatch: blocks
+// b, b + 8, b + 16, ... share an XCD and its L2): maps those blocks onto one
+// contiguous share of the grid, bijectively for any n (q = n / 8, r = n % 8).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+  const uint32_t q = n >> 3, r = n & 7u, x = b & 7u;
+  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
+}
+
 // ---------------------------------------------------------------------------
 // Fixed shape, L >= 16.
 // ---------------------------------------------------------------------------
 // SM (recover, gpb <= 8): lost-slot indices by scalar loads, see below.
-template <int KC, bool RECOVER, bool NT, bool SM>
+template <int KC, bool RECOVER, bool NT, bool SM, bool XCD = false>
 __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t C,
                                                            uint32_t gpb) {
   const uint32_t tid = threadIdx.x;
   const uint32_t gl = tid / C;  // group within the workgroup
   const uint32_t t = tid - gl * C;
-  const uint64_t gb = (uint64_t)blockIdx.x * gpb;
+  const uint64_t gb = (uint64_t)(XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) * gpb;
   const uint64_t g = gb + gl;
   uint64_t mw0 = 0, mw1 = 0;
   if constexpr (RECOVER) {
@@ -298,6 +306,13 @@ template <int ACC>
 __device__ __forceinline__ uint32_t acc_idx(uint32_t t, uint32_t c) {
   return ACC == 1 ? c * (uint32_t)kParWin + t : 4u * t + c;
 }
+__device__ __forceinline__ void lds_xor_u32(uint32_t* p, uint32_t v) {
+#ifdef QFEC_TUNE_PLAIN_LDS  // timing experiment only (tools/tune): plain store, WRONG results
+  *p = v;
+#else
+  __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
+}
 template <int ACC>
 __device__ __forceinline__ void lds_xor16(uint32_t* acc, uint32_t t, u32x4 v) {
   if constexpr (ACC == 2) {
@@ -307,14 +322,10 @@ __device__ __forceinline__ void lds_xor16(uint32_t* acc, uint32_t t, u32x4 v) {
     __hip_atomic_fetch_xor(p + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
   } else {
-    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 0), v.x, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 1), v.y, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 2), v.z, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_xor(acc + acc_idx<ACC>(t, 3), v.w, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    lds_xor_u32(acc + acc_idx<ACC>(t, 0), v.x);
+    lds_xor_u32(acc + acc_idx<ACC>(t, 1), v.y);
+    lds_xor_u32(acc + acc_idx<ACC>(t, 2), v.z);
+    lds_xor_u32(acc + acc_idx<ACC>(t, 3), v.w);
   }
 }
 template <int ACC>
@@ -393,7 +404,7 @@ __device__ __forceinline__ void group_vectors(const RaggedArgs& a, uint64_t g, u
 }
 
 // One group, one wave (see the flat-window description above).
-template <bool RECOVER, bool NT, int U, int ACC>
+template <bool RECOVER, bool NT, int U, int ACC, bool BF = false>
 __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
                                              const GroupPrefetch& f, uint32_t* par,
                                              uint64_t* head, u32x4* meta) {
@@ -459,7 +470,47 @@ __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, ui
     const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
     const uint32_t last = min(kr - c, 64u) - 1u;
     uint32_t before = 0;  // packet starts in earlier wave-iterations
-    if (!wave_any(r < kr && len < 16u)) {
+    if (BF && !wave_any(r < kr && len < 16u)) {
+      // Branch-free form: every lane loads and XORs on every iteration.  A
+      // lane past W loads its packet's last window and XORs ZERO into window
+      // `lane` (a no-op, conflict-free) — no exec-masked block, so the
+      // compiler cannot sink a load into one and wait on it right there.
+      for (uint32_t it = 0; it < nit; it += U) {
+        uint64_t M[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t w = head[min(it + (uint32_t)u, (uint32_t)kParWin - 1u)];
+          M[u] = it + (uint32_t)u < nit ? w : 0ull;
+        }
+        u32x4 md[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
+          before += (uint32_t)__popcll(M[u]);
+          md[u] = meta[pi];
+        }
+        u32x4 v[U];
+        uint32_t ts[U];  // window (bits 0-15) | shift (bits 16-19) | valid (bit 20)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t fl = 64u * (it + (uint32_t)u) + lane;
+          const uint32_t win = 16u * (fl - md[u].w);
+          const bool full = win + 16u <= md[u].z;
+          v[u] = ld16t<NT>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) +
+                           (full ? win : md[u].z - 16u));
+          const uint32_t sh = full ? 0u : min(win + 16u - md[u].z, 15u);
+          ts[u] = fl < W ? ((fl - md[u].w) | (sh << 16) | (1u << 20)) : lane;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          uint32_t keep = (ts[u] >> 20) ? 0xFFFFFFFFu : 0u;
+          // opaque to the optimiser: otherwise it proves the XOR of an idle
+          // lane to be 0, turns it into a branch and sinks the load into it
+          __asm__ volatile("" : "+v"(keep));
+          lds_xor16<ACC>(par, ts[u] & 0xFFFFu, shr_bytes_bf(v[u], (ts[u] >> 16) & 15u) & keep);
+        }
+      }
+    } else if (!BF && !wave_any(r < kr && len < 16u)) {
       // Every packet >= 16 B: every lane loads 16 in-packet bytes each
       // iteration (lanes past W re-read their packet's last window and drop
       // it), U iterations' loads in flight before the first XOR.
@@ -543,8 +594,223 @@ __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, ui
 }
 
 // One short-lived wave per group.
-template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1>
+template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1, bool BF = false,
+          bool XCD = false>
 __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[WAVES][4 * kParWin];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = (uint64_t)(XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) * WAVES + wv;
+  if (g >= a.n_groups) return;
+  GroupPrefetch f;
+  group_scalars<RECOVER>(a, g, f);
+  group_vectors<RECOVER, NT>(a, g, lane, f);
+  ragged_group<RECOVER, NT, U, ACC, BF>(a, g, lane, f, s_par[wv], s_head[wv], s_meta[wv]);
+}
+
+// ---------------------------------------------------------------------------
+// Ragged CSR, aligned-chunk form: one wave per group.
+// ---------------------------------------------------------------------------
+// Every load is an ALIGNED 16-byte chunk: entry e (a received packet, or for
+// recover the parity row) at address A with r = A & 15 covers the chunks
+// (A - r) + 16c, c < ceil((r + len) / 16).  Chunk c holds entry bytes
+// [16c - r, 16c - r + 16); the bytes outside [0, len) are masked to zero and
+// the rest XORed into the byte-addressed LDS accumulator at that position —
+// five dword atomics, the chunk funnel-shifted by (16c - r) mod 4 bytes.  An
+// aligned chunk holding a valid byte never crosses a page, so the extra bytes
+// it reads (neighbouring packets' edges) cannot fault; they are discarded.
+// Recover is the encode of the received packets plus the parity row (so the
+// parity row streams through the same path), cut to parity_len.
+// Measured: misaligned 16-B loads from packed packets cost ~5% of bandwidth
+// and make more loads in flight slower; aligned chunks lift both.
+
+// Bytes [b0, b1) of a 16-byte chunk kept, the rest zeroed (0 <= b0 <= b1 <= 16).
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 v, uint32_t b0, uint32_t b1) {
+  auto ones = [](uint32_t b) {  // ones in the low b bytes of a 64-bit word, b in 0..8
+    return b >= 8u ? ~0ull : ((1ull << (8u * b)) - 1ull);
+  };
+  const uint64_t mlo = ones(min(b1, 8u)) & ~ones(min(b0, 8u));
+  const uint64_t mhi = ones(b1 > 8u ? b1 - 8u : 0u) & ~ones(b0 > 8u ? b0 - 8u : 0u);
+  const uint64_t lo = ((uint64_t)v.x | ((uint64_t)v.y << 32)) & mlo;
+  const uint64_t hi = ((uint64_t)v.z | ((uint64_t)v.w << 32)) & mhi;
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// XOR 16 bytes into the accumulator at byte position 4*D + q (q in 0..3):
+// five dword atomics D .. D+4 (D may be -1 for a chunk that starts before the
+// entry; that dword's bytes are all masked, so it is folded onto dword 0).
+template <int ACC>
+__device__ __forceinline__ void lds_xor16_at(uint32_t* acc, int32_t D, uint32_t q, u32x4 v) {
+  const uint32_t s = 8u * q;
+  const uint32_t o[5] = {
+      v.x << s,
+      (uint32_t)((((uint64_t)v.y << 32) | v.x) << s >> 32),
+      (uint32_t)((((uint64_t)v.z << 32) | v.y) << s >> 32),
+      (uint32_t)((((uint64_t)v.w << 32) | v.z) << s >> 32),
+      (uint32_t)(((uint64_t)v.w << s) >> 32)};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint32_t d = (uint32_t)max(D + i, 0);
+    lds_xor_u32(acc + acc_idx<ACC>(d >> 2, d & 3u), o[i]);
+  }
+}
+
+// Accumulator bytes [0, plen) -> dst (16-B stores; tail = the 16 B ending at plen).
+template <int ACC, bool NT>
+__device__ __forceinline__ void store_acc(const uint32_t* par, uint8_t* dst, uint32_t plen,
+                                          uint32_t lane) {
+  if (plen >= 16u) {
+    const uint32_t nw = (plen + 15u) >> 4;
+    for (uint32_t t = lane; t < nw; t += 64u) {
+      if (16u * t + 16u <= plen) {
+        st16t<NT>(dst + 16u * t, lds_get16<ACC>(par, t));
+      } else {
+        const uint32_t o = plen - 16u * t;  // 1..15
+        const u32x4 lo = lds_get16<ACC>(par, t - 1u), hi = lds_get16<ACC>(par, t);
+        const uint64_t a0 = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+        const uint64_t a1 = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+        const uint64_t a2 = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+        const uint64_t a3 = (uint64_t)hi.z | ((uint64_t)hi.w << 32);
+        const uint64_t w0 = o < 8u ? a0 : a1, w1 = o < 8u ? a1 : a2, w2 = o < 8u ? a2 : a3;
+        const uint32_t s = (o & 7u) * 8u;
+        const uint64_t r0 = (w0 >> s) | ((w1 << 1) << (63u - s));
+        const uint64_t r1 = (w1 >> s) | ((w2 << 1) << (63u - s));
+        st16t<NT>(dst + plen - 16u, u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1,
+                                          (uint32_t)(r1 >> 32)});
+      }
+    }
+  } else if (lane < plen) {
+    dst[lane] = (uint8_t)(par[acc_idx<ACC>(0, lane >> 2)] >> (8u * (lane & 3u)));
+  }
+}
+
+template <bool RECOVER, bool NT, int U, int ACC>
+__device__ __forceinline__ void ragged_group_al(const RaggedArgs& a, uint64_t g, uint32_t lane,
+                                                uint32_t* par, uint64_t* head, u32x4* meta) {
+  const uint32_t p0 = a.grp_ptr[g];
+  const uint32_t k = a.grp_ptr[g + 1] - p0;
+  if (k == 0u || k > 255u) {  // grp_ptr not monotone shows up as k > 255 too
+    if (lane == 0) atomicOr(a.err, kErrGroupSize);
+    return;
+  }
+  uint32_t m = 0xFFFFFFFFu, plen = 0;
+  uint64_t dst_off;
+  const uint8_t* prow = nullptr;
+  if constexpr (RECOVER) {
+    m = a.missing[g];
+    plen = a.parity_len[g];
+    dst_off = a.out_off[g];
+    if (m >= k) {
+      if (lane == 0) atomicOr(a.err, kErrMissingIndex);
+      return;
+    }
+    if (plen == 0u || plen > kMaxPacket) {
+      if (lane == 0) atomicOr(a.err, kErrParityLength);
+      return;
+    }
+    prow = a.parity + a.parity_off[g];
+  } else {
+    dst_off = a.parity_off[g];
+  }
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(par, t, zero);
+  // entries: the received packets, then (recover) the parity row
+  const uint32_t ne = k;
+  const uint32_t lim = RECOVER ? plen : kMaxPacket;
+  uint32_t mx = 0;
+  for (uint32_t c = 0; c < ne; c += 64u) {
+    const uint32_t r = c + lane;
+    uint32_t len = 0;
+    uint64_t addr = 0;
+    if (r < ne) {
+      if (RECOVER && r == ne - 1u) {
+        addr = (uint64_t)(uintptr_t)prow;
+        len = plen;
+      } else {
+        const uint32_t p = p0 + r + (RECOVER && r >= m ? 1u : 0u);
+        len = a.pkt_len[p];
+        addr = (uint64_t)(uintptr_t)(a.bytes + a.pkt_off[p]);
+      }
+    }
+    const bool bad = r < ne && (len == 0u || len > lim);
+    if (wave_any(bad)) {
+      if (lane == 0) atomicOr(a.err, kErrPacketLength);
+      return;
+    }
+    mx = max(mx, len);
+    const uint32_t ra = (uint32_t)addr & 15u;
+    const uint32_t n = r < ne ? (ra + len + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(n, lane);
+    const uint32_t S = incl - n;
+    const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t nit = (W + 63u) >> 6;  // W <= 64 x 92
+    wave_lds_order();  // accumulator initialised / previous chunk's table reads done
+    for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
+    wave_lds_order();
+    if (r < ne) {
+      const uint64_t base = addr - ra;
+      meta[lane] = u32x4{(uint32_t)base, (uint32_t)(base >> 32), len | (ra << 16), S};
+      __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    wave_lds_order();  // packet table and start mask complete
+    const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t last = min(ne - c, 64u) - 1u;
+    uint32_t before = 0;
+    for (uint32_t it = 0; it < nit; it += U) {
+      uint64_t M[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t w = head[min(it + (uint32_t)u, (uint32_t)kParWin - 1u)];
+        M[u] = it + (uint32_t)u < nit ? w : 0ull;
+      }
+      u32x4 md[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
+        before += (uint32_t)__popcll(M[u]);
+        md[u] = meta[pi];
+      }
+      u32x4 v[U];
+      // per chunk, one register: (16c - r + 16) | valid << 12 | entry len << 16
+      uint32_t pk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t fl = 64u * (it + (uint32_t)u) + lane;
+        const uint32_t len_e = md[u].z & 0xFFFFu, ra_e = md[u].z >> 16;
+        const uint32_t nch = (ra_e + len_e + 15u) >> 4;
+        const uint32_t ch = min(fl - md[u].w, nch - 1u);  // lanes past W: the last chunk
+        v[u] = ld16t<NT>(reinterpret_cast<const uint8_t*>(
+            (uintptr_t)((((uint64_t)md[u].y << 32) | md[u].x) + 16ull * ch)));
+        pk[u] = (16u * ch + 16u - ra_e) | (fl < W ? 0x1000u : 0u) | (len_e << 16);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // opaque to the optimiser: otherwise it proves an idle lane's XOR to
+        // be 0, turns it into a branch and sinks the load into it
+        uint32_t x = pk[u];
+        __asm__ volatile("" : "+v"(x));
+        const int32_t P = (int32_t)(x & 0xFFFu) - 16;  // entry byte at the chunk's first byte
+        const bool valid = (x & 0x1000u) != 0u;
+        const uint32_t b0 = P < 0 ? (uint32_t)(-P) : 0u;
+        const uint32_t b1 = valid ? (uint32_t)min((int32_t)(x >> 16) - P, 16) : b0;
+        const int32_t D = valid ? (P >> 2) : (int32_t)(lane << 2);  // idle: spread, no conflicts
+        lds_xor16_at<ACC>(par, D, (uint32_t)P & 3u, keep_bytes(v[u], b0, b1));
+      }
+    }
+  }
+  if constexpr (!RECOVER) {
+    plen = wave_max11(mx);
+    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
+  }
+  wave_lds_order();  // every lane's XORs into the accumulator done
+  store_acc<ACC, NT>(par, a.out + dst_off, plen, lane);
+}
+
+template <bool RECOVER, bool NT, int U = 4, int WAVES = kFlatWaves, int ACC = 1>
+__global__ __launch_bounds__(64 * WAVES) void ragged_al_kernel(RaggedArgs a) {
   __shared__ uint32_t s_par[WAVES][4 * kParWin];
   __shared__ uint64_t s_head[WAVES][kParWin];
   __shared__ u32x4 s_meta[WAVES][64];
@@ -552,10 +818,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
   if (g >= a.n_groups) return;
-  GroupPrefetch f;
-  group_scalars<RECOVER>(a, g, f);
-  group_vectors<RECOVER, NT>(a, g, lane, f);
-  ragged_group<RECOVER, NT, U, ACC>(a, g, lane, f, s_par[wv], s_head[wv], s_meta[wv]);
+  ragged_group_al<RECOVER, NT, U, ACC>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
 }
 
 // ---------------------------------------------------------------------------

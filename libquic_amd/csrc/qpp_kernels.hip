@@ -17,7 +17,9 @@
 // third limb's addend) + one v_mul_lo_u32 + a shift/add for the top limb:
 // ≈12 instructions, ≈23 VALU issue slots per byte (the 64-bit mads are
 // multi-pass) — VALU-bound at ≈3.5 TB/s of hashed bytes on the chip
-// (tools/tune/tune_protect.hip, register-only microbenchmark).
+// (tools/tune/tune_protect.hip, register-only microbenchmark).  Payload
+// chunks take three bytes per multiply instead (fnv_step3: the same
+// recurrence, regrouped exactly).
 //
 // Memory: the payload bytes move by coalesced wave loads through an LDS
 // transpose (see "LDS-staged forms"); a lane loading its own packet (64
@@ -70,11 +72,66 @@ __device__ __forceinline__ void fnv_word(Fnv128& h, uint32_t w) {
   fnv_step(h, w >> 24);
 }
 
+// Three byte steps at once, equal to fnv_step(b0); fnv_step(b1); fnv_step(b2).
+// P = 2^88 + 315 is 59 mod 256, so the state's low byte runs on its own,
+// y' = 59 (y ^ b) mod 256 (`y` carries it: h.x0 & 0xFF on entry and exit),
+// and XORing b into a state whose low byte is y ADDS d = (y ^ b) - y.  So
+//     h3 = (h ^ b0) P^3 + d1 P^2 + d2 P                       (mod 2^128)
+// with P^j = 315^j + j 315^(j-1) 2^88 (2^176 = 0 mod 2^128):
+//     P^3 = 31255875 + 297675 2^88,  P^2 = 99225 + 630 2^88,  P = 315 + 2^88.
+// Per three bytes: one 128 x 25-bit multiply (3 v_mad_u64_u32 + 1 mul) and a
+// 40-bit product for the 2^88 column, plus full-rate 24-bit byte-chain ops,
+// instead of three dependent 128 x 9-bit multiplies — ~17 instead of ~23
+// VALU issue slots per byte, and one multiply instead of twelve on the
+// loop-carried limb-0 chain (the d's come from the cheap y chain).
+// d1, d2 lie in (-256, 256), yet every partial sum below is nonnegative: a
+// negative d needs a nonzero t0 (the low byte of x0), and then
+// x0 * 315^3 >= 31255875 > |99225 d1 + 315 d2| (<= 25382700), so the carries
+// are plain unsigned ones (tools/tune/fnv_r3_check.c checks it all on the host).
+__device__ __forceinline__ void fnv_step3(Fnv128& h, uint32_t& y, uint32_t b0, uint32_t b1,
+                                          uint32_t b2) {
+  constexpr uint32_t kC3 = 31255875u, kC3h = 297675u;  // 315^3, 3 * 315^2
+  const uint32_t t0 = y ^ b0;
+  const uint32_t y1 = (t0 * 59u) & 0xFFu;
+  const uint32_t t1 = y1 ^ b1;
+  const uint32_t y2 = (t1 * 59u) & 0xFFu;
+  const uint32_t t2 = y2 ^ b2;
+  y = (t2 * 59u) & 0xFFu;
+  const int32_t d1 = (int32_t)t1 - (int32_t)y1;
+  const int32_t d2 = (int32_t)t2 - (int32_t)y2;
+  const uint64_t slo = (uint64_t)(int64_t)(d1 * 99225 + d2 * 315);  // low parts of d1 P^2 + d2 P
+  const uint64_t shi = (uint64_t)(int64_t)(d1 * 630 + d2);          // their 2^88 coefficients
+  const uint32_t x0 = h.x0 ^ b0;
+  // 2^88 column mod 2^40: x * 297675 + shi, x mod 2^40 = x0 + 2^32 (x1 mod 256)
+  const uint64_t u =
+      (uint64_t)x0 * kC3h + shi + ((uint64_t)((h.x1 & 0xFFu) * (kC3h & 0xFFu)) << 32);
+  const uint64_t q0 = (uint64_t)x0 * kC3 + slo;
+  const uint64_t q1 = (uint64_t)h.x1 * kC3 + (q0 >> 32);
+  const uint64_t q2 = (uint64_t)h.x2 * kC3 + (q1 >> 32) + (u << 24);
+  h.x0 = (uint32_t)q0;
+  h.x1 = (uint32_t)q1;
+  h.x2 = (uint32_t)q2;
+  h.x3 = h.x3 * kC3 + (uint32_t)(q2 >> 32);
+}
+
+// 16 bytes.  R3 (the default): five fnv_step3 + one fnv_step; otherwise 16 fnv_step.
+template <bool R3 = true>
 __device__ __forceinline__ void fnv_chunk(Fnv128& h, u32x4 v) {
-  fnv_word(h, v.x);
-  fnv_word(h, v.y);
-  fnv_word(h, v.z);
-  fnv_word(h, v.w);
+  if constexpr (R3) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t y = h.x0 & 0xFFu;
+#pragma unroll
+    for (int i = 0; i < 15; i += 3)
+      fnv_step3(h, y, (w[i >> 2] >> (8 * (i & 3))) & 0xFFu,
+                (w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu,
+                (w[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 0xFFu);
+    fnv_step(h, v.w >> 24);
+  } else {
+    fnv_word(h, v.x);
+    fnv_word(h, v.y);
+    fnv_word(h, v.z);
+    fnv_word(h, v.w);
+  }
 }
 
 __device__ __forceinline__ uint32_t byte_of(u32x4 v, uint32_t i) {
@@ -115,6 +172,7 @@ __device__ __forceinline__ void fnv_tail(Fnv128& h, u32x4 v, uint32_t len) {
 constexpr uint32_t kBatch = 8;
 
 // Hash a span (no copy).
+template <bool R3 = true>
 __device__ __forceinline__ void fnv_span(Fnv128& h, const uint8_t* p, uint32_t len) {
   const uint32_t nfull = len >> 4;
   const u32x4 tail = load_tail(p, len);
@@ -124,7 +182,7 @@ __device__ __forceinline__ void fnv_span(Fnv128& h, const uint8_t* p, uint32_t l
     for (uint32_t u = 0; u < kBatch; ++u) v[u] = ld16(p + 16u * min(c + u, nfull - 1u));
 #pragma unroll
     for (uint32_t u = 0; u < kBatch; ++u)
-      if (c + u < nfull) fnv_chunk(h, v[u]);
+      if (c + u < nfull) fnv_chunk<R3>(h, v[u]);
   }
   fnv_tail(h, tail, len);
 }
@@ -226,7 +284,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // payloads.  In-place safe for dst == src + 12: slab s is stored only after
 // slab s+1 has been loaded AND the loads have completed (waitcnt), so no store
 // overtakes a load of the 12 bytes it overwrites.
-template <bool COPY, uint32_t SC>
+template <bool COPY, uint32_t SC, bool R3 = true>
 __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32x4* rows,
                                            uint32_t lane, uint32_t my_nfull) {
   const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
@@ -237,7 +295,7 @@ __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32
     if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, nxt);
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j)
-      if (sl * SC + j < my_nfull) fnv_chunk(h, rows[lane * (SC + 1u) + j]);
+      if (sl * SC + j < my_nfull) fnv_chunk<R3>(h, rows[lane * (SC + 1u) + j]);
     if constexpr (COPY) {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next slab's loads are done
       stage_store<SC>(meta, lane, sl, cur);
@@ -247,7 +305,7 @@ __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32
   }
 }
 
-template <uint32_t SC>
+template <uint32_t SC, bool R3 = true>
 __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -269,8 +327,8 @@ __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs
   // the payload's last len % 16 bytes, before any store (in place)
   const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
   Fnv128 h = fnv_init();
-  if (valid) fnv_span(h, ad, alen);
-  stage_hash<true, SC>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+  if (valid) fnv_span<R3>(h, ad, alen);
+  stage_hash<true, SC, R3>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
   if (!valid) return;
   fnv_tail(h, tail, plen);
   store_tail(o + kTag, tail, plen);
@@ -278,7 +336,7 @@ __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs
   __builtin_memcpy(o, tag, kTag);
 }
 
-template <uint32_t SC>
+template <uint32_t SC, bool R3 = true>
 __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -301,8 +359,8 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   s_meta[wv][lane] = StageMeta{ct + kTag, nullptr, plen >> 4};
   const u32x4 tail = valid ? load_tail(ct + kTag, plen) : u32x4{0u, 0u, 0u, 0u};
   Fnv128 h = fnv_init();
-  if (valid) fnv_span(h, ad, alen);
-  stage_hash<false, SC>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+  if (valid) fnv_span<R3>(h, ad, alen);
+  stage_hash<false, SC, R3>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
   // ComputeHash keeps the low 96 bits (null_decrypter.cc:97-106)
   bool ok = false;
   if (valid) {

@@ -40,6 +40,19 @@ __global__ void fnv_valu_kernel(uint32_t bytes, uint32_t* sink) {
   if ((h.x0 ^ h.x1 ^ h.x2 ^ h.x3) == 0x12345678u) sink[0] = h.x0;
 }
 
+// pure VALU, 16-byte chunks as the staged kernels hash them (R3 or byte-serial)
+template <bool R3>
+__global__ void fnv_valu_chunk_kernel(uint32_t bytes, uint32_t* sink) {
+  qfec::Fnv128 h = qfec::fnv_init();
+  uint32_t w = threadIdx.x * 0x9E3779B9u;
+  for (uint32_t i = 0; i < bytes; i += 16) {
+    const qfec::u32x4 v = {w, w ^ 0x5bd1e995u, w * 3u + 1u, w + 0x27d4eb2du};
+    qfec::fnv_chunk<R3>(h, v);
+    w = w * 1664525u + 1013904223u;
+  }
+  if ((h.x0 ^ h.x1 ^ h.x2 ^ h.x3) == 0x12345678u) sink[0] = h.x0;
+}
+
 int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 21);
   const uint32_t L = 1350, H = 22;
@@ -161,6 +174,14 @@ int main(int argc, char** argv) {
          hipLaunchKernelGGL(qfec::null_decrypt_direct_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
       {"FNV step VALU-only (4 KiB/lane)", 0.0, (double)vgrid * 256 * vb,
        [&] { hipLaunchKernelGGL(fnv_valu_kernel, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
+      {"FNV chunk VALU-only R3", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<true>, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
+      {"FNV chunk VALU-only serial", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<false>, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
+      {"null encrypt staged serial FNV", enc_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
+      {"null decrypt staged serial FNV", dec_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
