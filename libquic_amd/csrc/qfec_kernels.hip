@@ -611,217 +611,6 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Ragged CSR, aligned-chunk form: one wave per group.
-// ---------------------------------------------------------------------------
-// Every load is an ALIGNED 16-byte chunk: entry e (a received packet, or for
-// recover the parity row) at address A with r = A & 15 covers the chunks
-// (A - r) + 16c, c < ceil((r + len) / 16).  Chunk c holds entry bytes
-// [16c - r, 16c - r + 16); the bytes outside [0, len) are masked to zero and
-// the rest XORed into the byte-addressed LDS accumulator at that position —
-// five dword atomics, the chunk funnel-shifted by (16c - r) mod 4 bytes.  An
-// aligned chunk holding a valid byte never crosses a page, so the extra bytes
-// it reads (neighbouring packets' edges) cannot fault; they are discarded.
-// Recover is the encode of the received packets plus the parity row (so the
-// parity row streams through the same path), cut to parity_len.
-// Measured: misaligned 16-B loads from packed packets cost ~5% of bandwidth
-// and make more loads in flight slower; aligned chunks lift both.
-
-// Bytes [b0, b1) of a 16-byte chunk kept, the rest zeroed (0 <= b0 <= b1 <= 16).
-__device__ __forceinline__ u32x4 keep_bytes(u32x4 v, uint32_t b0, uint32_t b1) {
-  auto ones = [](uint32_t b) {  // ones in the low b bytes of a 64-bit word, b in 0..8
-    return b >= 8u ? ~0ull : ((1ull << (8u * b)) - 1ull);
-  };
-  const uint64_t mlo = ones(min(b1, 8u)) & ~ones(min(b0, 8u));
-  const uint64_t mhi = ones(b1 > 8u ? b1 - 8u : 0u) & ~ones(b0 > 8u ? b0 - 8u : 0u);
-  const uint64_t lo = ((uint64_t)v.x | ((uint64_t)v.y << 32)) & mlo;
-  const uint64_t hi = ((uint64_t)v.z | ((uint64_t)v.w << 32)) & mhi;
-  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-}
-
-// XOR 16 bytes into the accumulator at byte position 4*D + q (q in 0..3):
-// five dword atomics D .. D+4 (D may be -1 for a chunk that starts before the
-// entry; that dword's bytes are all masked, so it is folded onto dword 0).
-template <int ACC>
-__device__ __forceinline__ void lds_xor16_at(uint32_t* acc, int32_t D, uint32_t q, u32x4 v) {
-  const uint32_t s = 8u * q;
-  const uint32_t o[5] = {
-      v.x << s,
-      (uint32_t)((((uint64_t)v.y << 32) | v.x) << s >> 32),
-      (uint32_t)((((uint64_t)v.z << 32) | v.y) << s >> 32),
-      (uint32_t)((((uint64_t)v.w << 32) | v.z) << s >> 32),
-      (uint32_t)(((uint64_t)v.w << s) >> 32)};
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const uint32_t d = (uint32_t)max(D + i, 0);
-    lds_xor_u32(acc + acc_idx<ACC>(d >> 2, d & 3u), o[i]);
-  }
-}
-
-// Accumulator bytes [0, plen) -> dst (16-B stores; tail = the 16 B ending at plen).
-template <int ACC, bool NT>
-__device__ __forceinline__ void store_acc(const uint32_t* par, uint8_t* dst, uint32_t plen,
-                                          uint32_t lane) {
-  if (plen >= 16u) {
-    const uint32_t nw = (plen + 15u) >> 4;
-    for (uint32_t t = lane; t < nw; t += 64u) {
-      if (16u * t + 16u <= plen) {
-        st16t<NT>(dst + 16u * t, lds_get16<ACC>(par, t));
-      } else {
-        const uint32_t o = plen - 16u * t;  // 1..15
-        const u32x4 lo = lds_get16<ACC>(par, t - 1u), hi = lds_get16<ACC>(par, t);
-        const uint64_t a0 = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
-        const uint64_t a1 = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
-        const uint64_t a2 = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
-        const uint64_t a3 = (uint64_t)hi.z | ((uint64_t)hi.w << 32);
-        const uint64_t w0 = o < 8u ? a0 : a1, w1 = o < 8u ? a1 : a2, w2 = o < 8u ? a2 : a3;
-        const uint32_t s = (o & 7u) * 8u;
-        const uint64_t r0 = (w0 >> s) | ((w1 << 1) << (63u - s));
-        const uint64_t r1 = (w1 >> s) | ((w2 << 1) << (63u - s));
-        st16t<NT>(dst + plen - 16u, u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1,
-                                          (uint32_t)(r1 >> 32)});
-      }
-    }
-  } else if (lane < plen) {
-    dst[lane] = (uint8_t)(par[acc_idx<ACC>(0, lane >> 2)] >> (8u * (lane & 3u)));
-  }
-}
-
-template <bool RECOVER, bool NT, int U, int ACC>
-__device__ __forceinline__ void ragged_group_al(const RaggedArgs& a, uint64_t g, uint32_t lane,
-                                                uint32_t* par, uint64_t* head, u32x4* meta) {
-  const uint32_t p0 = a.grp_ptr[g];
-  const uint32_t k = a.grp_ptr[g + 1] - p0;
-  if (k == 0u || k > 255u) {  // grp_ptr not monotone shows up as k > 255 too
-    if (lane == 0) atomicOr(a.err, kErrGroupSize);
-    return;
-  }
-  uint32_t m = 0xFFFFFFFFu, plen = 0;
-  uint64_t dst_off;
-  const uint8_t* prow = nullptr;
-  if constexpr (RECOVER) {
-    m = a.missing[g];
-    plen = a.parity_len[g];
-    dst_off = a.out_off[g];
-    if (m >= k) {
-      if (lane == 0) atomicOr(a.err, kErrMissingIndex);
-      return;
-    }
-    if (plen == 0u || plen > kMaxPacket) {
-      if (lane == 0) atomicOr(a.err, kErrParityLength);
-      return;
-    }
-    prow = a.parity + a.parity_off[g];
-  } else {
-    dst_off = a.parity_off[g];
-  }
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(par, t, zero);
-  // entries: the received packets, then (recover) the parity row
-  const uint32_t ne = k;
-  const uint32_t lim = RECOVER ? plen : kMaxPacket;
-  uint32_t mx = 0;
-  for (uint32_t c = 0; c < ne; c += 64u) {
-    const uint32_t r = c + lane;
-    uint32_t len = 0;
-    uint64_t addr = 0;
-    if (r < ne) {
-      if (RECOVER && r == ne - 1u) {
-        addr = (uint64_t)(uintptr_t)prow;
-        len = plen;
-      } else {
-        const uint32_t p = p0 + r + (RECOVER && r >= m ? 1u : 0u);
-        len = a.pkt_len[p];
-        addr = (uint64_t)(uintptr_t)(a.bytes + a.pkt_off[p]);
-      }
-    }
-    const bool bad = r < ne && (len == 0u || len > lim);
-    if (wave_any(bad)) {
-      if (lane == 0) atomicOr(a.err, kErrPacketLength);
-      return;
-    }
-    mx = max(mx, len);
-    const uint32_t ra = (uint32_t)addr & 15u;
-    const uint32_t n = r < ne ? (ra + len + 15u) >> 4 : 0u;
-    const uint32_t incl = wave_incl_scan(n, lane);
-    const uint32_t S = incl - n;
-    const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t nit = (W + 63u) >> 6;  // W <= 64 x 92
-    wave_lds_order();  // accumulator initialised / previous chunk's table reads done
-    for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
-    wave_lds_order();
-    if (r < ne) {
-      const uint64_t base = addr - ra;
-      meta[lane] = u32x4{(uint32_t)base, (uint32_t)(base >> 32), len | (ra << 16), S};
-      __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-    wave_lds_order();  // packet table and start mask complete
-    const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
-    const uint32_t last = min(ne - c, 64u) - 1u;
-    uint32_t before = 0;
-    for (uint32_t it = 0; it < nit; it += U) {
-      uint64_t M[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t w = head[min(it + (uint32_t)u, (uint32_t)kParWin - 1u)];
-        M[u] = it + (uint32_t)u < nit ? w : 0ull;
-      }
-      u32x4 md[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
-        before += (uint32_t)__popcll(M[u]);
-        md[u] = meta[pi];
-      }
-      u32x4 v[U];
-      // per chunk, one register: (16c - r + 16) | valid << 12 | entry len << 16
-      uint32_t pk[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t fl = 64u * (it + (uint32_t)u) + lane;
-        const uint32_t len_e = md[u].z & 0xFFFFu, ra_e = md[u].z >> 16;
-        const uint32_t nch = (ra_e + len_e + 15u) >> 4;
-        const uint32_t ch = min(fl - md[u].w, nch - 1u);  // lanes past W: the last chunk
-        v[u] = ld16t<NT>(reinterpret_cast<const uint8_t*>(
-            (uintptr_t)((((uint64_t)md[u].y << 32) | md[u].x) + 16ull * ch)));
-        pk[u] = (16u * ch + 16u - ra_e) | (fl < W ? 0x1000u : 0u) | (len_e << 16);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        // opaque to the optimiser: otherwise it proves an idle lane's XOR to
-        // be 0, turns it into a branch and sinks the load into it
-        uint32_t x = pk[u];
-        __asm__ volatile("" : "+v"(x));
-        const int32_t P = (int32_t)(x & 0xFFFu) - 16;  // entry byte at the chunk's first byte
-        const bool valid = (x & 0x1000u) != 0u;
-        const uint32_t b0 = P < 0 ? (uint32_t)(-P) : 0u;
-        const uint32_t b1 = valid ? (uint32_t)min((int32_t)(x >> 16) - P, 16) : b0;
-        const int32_t D = valid ? (P >> 2) : (int32_t)(lane << 2);  // idle: spread, no conflicts
-        lds_xor16_at<ACC>(par, D, (uint32_t)P & 3u, keep_bytes(v[u], b0, b1));
-      }
-    }
-  }
-  if constexpr (!RECOVER) {
-    plen = wave_max11(mx);
-    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
-  }
-  wave_lds_order();  // every lane's XORs into the accumulator done
-  store_acc<ACC, NT>(par, a.out + dst_off, plen, lane);
-}
-
-template <bool RECOVER, bool NT, int U = 4, int WAVES = kFlatWaves, int ACC = 1>
-__global__ __launch_bounds__(64 * WAVES) void ragged_al_kernel(RaggedArgs a) {
-  __shared__ uint32_t s_par[WAVES][4 * kParWin];
-  __shared__ uint64_t s_head[WAVES][kParWin];
-  __shared__ u32x4 s_meta[WAVES][64];
-  const uint32_t lane = lane_id();
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
-  if (g >= a.n_groups) return;
-  ragged_group_al<RECOVER, NT, U, ACC>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-}
-
-// ---------------------------------------------------------------------------
 // out ^= in (XorBuffers).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void xor_into_kernel(const uint8_t* in, uint64_t n,

@@ -6,6 +6,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_multi.hip -o tools/tune/build/tune_multi
 // run:   tune_multi [reps] [rounds] [kmin] [kspan] [align16]
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
+#include "al_ragged.inc"
 #include "multi_ragged.inc"
 
 #include <algorithm>
@@ -60,12 +61,6 @@ template <bool REC, int U>
 static void launch_al(const RaggedArgs& a, uint64_t G) {
   hipLaunchKernelGGL((qfec::ragged_al_kernel<REC, true, U, 4, 1>),
                      dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
-}
-
-template <bool REC, int WPE>
-static void launch_wpe(const RaggedArgs& a, uint64_t G) {
-  hipLaunchKernelGGL((qfec::ragged_wpe_kernel<REC, WPE>), dim3((uint32_t)((G + 3) / 4)), dim3(256),
-                     0, 0, a);
 }
 
 template <bool REC>
@@ -169,8 +164,6 @@ int main(int argc, char** argv) {
   vs.push_back({"multi2 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4>(a, G); }});
   vs.push_back({"multi3 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, 4>(a, G); }});
   vs.push_back({"product XCD encode", false, [=](const RaggedArgs& a) { launch_xcd<false>(a, G); }});
-  vs.push_back({"product WPE10 encode", false, [=](const RaggedArgs& a) { launch_wpe<false, 10>(a, G); }});
-  vs.push_back({"product WPE12 encode", false, [=](const RaggedArgs& a) { launch_wpe<false, 12>(a, G); }});
   vs.push_back({"product recover", true, [](const RaggedArgs& a) { CK(qfec::launch_ragged(a, true, 0)); }});
   vs.push_back({"BF U2 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 2>(a, G); }});
   vs.push_back({"AL U2 recover", true, [=](const RaggedArgs& a) { launch_al<true, 2>(a, G); }});
@@ -183,8 +176,6 @@ int main(int argc, char** argv) {
   vs.push_back({"multi2 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4>(a, G); }});
   vs.push_back({"multi3 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, 4>(a, G); }});
   vs.push_back({"product XCD recover", true, [=](const RaggedArgs& a) { launch_xcd<true>(a, G); }});
-  vs.push_back({"product WPE10 recover", true, [=](const RaggedArgs& a) { launch_wpe<true, 10>(a, G); }});
-  vs.push_back({"product WPE12 recover", true, [=](const RaggedArgs& a) { launch_wpe<true, 12>(a, G); }});
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
