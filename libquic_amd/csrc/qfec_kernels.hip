@@ -307,11 +307,7 @@ __device__ __forceinline__ uint32_t acc_idx(uint32_t t, uint32_t c) {
   return ACC == 1 ? c * (uint32_t)kParWin + t : 4u * t + c;
 }
 __device__ __forceinline__ void lds_xor_u32(uint32_t* p, uint32_t v) {
-#ifdef QFEC_TUNE_PLAIN_LDS  // timing experiment only (tools/tune): plain store, WRONG results
-  *p = v;
-#else
   __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
 }
 template <int ACC>
 __device__ __forceinline__ void lds_xor16(uint32_t* acc, uint32_t t, u32x4 v) {
