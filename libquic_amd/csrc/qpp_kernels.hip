@@ -371,11 +371,17 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   // copy after the check (null_decrypter.cc:60-62), coalesced, verified packets only
   uint8_t* o = ok ? a.out + a.out_off[p] : nullptr;
   s_meta[wv][lane] = StageMeta{ct + kTag, o, ok ? plen >> 4 : 0u};
+  // Slab s+1's loads are in flight while slab s is stored (out of place: no
+  // load/store ordering hazard); a load-then-store loop parked the waves on
+  // every slab's round trip (SQ_WAIT_ANY 0.76 of the decrypt's wave cycles).
   const uint32_t nslab = (wave_max_u32(ok ? plen >> 4 : 0u) + SC - 1) / SC;
+  u32x4 cur[SC], nxt[SC];
+  if (nslab) stage_load<SC>(s_meta[wv], lane, 0, cur);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
-    u32x4 v[SC];
-    stage_load<SC>(s_meta[wv], lane, sl, v);
-    stage_store<SC>(s_meta[wv], lane, sl, v);
+    if (sl + 1u < nslab) stage_load<SC>(s_meta[wv], lane, sl + 1u, nxt);
+    stage_store<SC>(s_meta[wv], lane, sl, cur);
+#pragma unroll
+    for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
   }
   if (ok) store_tail(o, tail, plen);
 }

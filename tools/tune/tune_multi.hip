@@ -4,7 +4,9 @@
 // packed CSR).  Every variant's output bytes are compared with the product's.
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_multi.hip -o tools/tune/build/tune_multi
-// run:   tune_multi [reps] [rounds] [kmin] [kspan] [align16]
+// run:   tune_multi [reps] [rounds] [kmin] [kspan] [align16] [packed_out]
+//        packed_out = 1: parity / revived rows back to back (offset = running sum of
+//        parity lengths) instead of 1452-byte slots
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
 #include "al_ragged.inc"
 #include "multi_ragged.inc"
@@ -75,6 +77,8 @@ int main(int argc, char** argv) {
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
   const uint32_t kmin = argc > 3 ? atoi(argv[3]) : 5, kspan = argc > 4 ? atoi(argv[4]) : 11;
   const bool align16 = argc > 5 && atoi(argv[5]) != 0;
+  const bool packed_out = argc > 6 && atoi(argv[6]) != 0;
+  uint64_t out_pos = 0;
   const uint64_t seed = 0x51554944;
   std::vector<uint32_t> ptr{0};
   std::vector<uint16_t> len, plen_h(G);
@@ -100,7 +104,8 @@ int main(int argc, char** argv) {
     enc_alg += s + mx;
     rec_alg += sm + 2.0 * mx;
     ptr.push_back((uint32_t)len.size());
-    poff[g] = g * 1452;
+    poff[g] = packed_out ? out_pos : g * 1452;
+    out_pos += mx;
   }
   uint8_t* data;
   CK(hipMalloc(&data, bytes + 4096));
@@ -201,8 +206,8 @@ int main(int argc, char** argv) {
         if (p - ptr[g] != miss[g])
           for (uint32_t j = 0; j < len[p]; ++j) rv[j] ^= h[off[p] + j];
       const uint32_t lm = len[ptr[g] + miss[g]];
-      bad += memcmp(ref, &want_e[g * 1452], mx) != 0 || want_pl[g] != mx;
-      bad += memcmp(rv, &want_r[g * 1452], lm) != 0;
+      bad += memcmp(ref, &want_e[poff[g]], mx) != 0 || want_pl[g] != mx;
+      bad += memcmp(rv, &want_r[poff[g]], lm) != 0;
     }
     std::printf("product vs host XOR: bad groups %d\n", bad);
   }
