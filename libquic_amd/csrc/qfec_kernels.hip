@@ -606,6 +606,215 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   ragged_group<RECOVER, NT, U, ACC, BF>(a, g, lane, f, s_par[wv], s_head[wv], s_meta[wv]);
 }
 
+// Two groups per wave (the launch_ragged default): GPW consecutive groups in
+// ONE flat window space — their received packets fill the 64-lane packet
+// table together — so the per-group load chain (group pointer -> packet table
+// -> packet bytes), which parks the one-group waves for 70% of their cycles
+// (SQ_WAIT_ANY, profiles/round1/sq_stalls_fec_pq.txt), and the partially idle
+// last iteration are paid once per GPW groups.  Groups that do not fit (more
+// than 64 received packets together, a packet below 16 B, any invalid field)
+// run the per-group body above with its exact error semantics.  Measured
+// +1.0-1.6% encode and recover over one group per wave in three interleaved
+// A/B runs (tune_multi_t2.txt, ragged_slots_p*.txt, tune_multi_sp.txt);
+// three groups per wave overflow the table too often (-10%).
+constexpr int kRaggedGPW = 2;
+
+template <int N, typename T>
+__device__ __forceinline__ T sel_n(const T (&v)[N], uint32_t j) {
+  T r = v[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) r = j == (uint32_t)i ? v[i] : r;
+  return r;
+}
+
+template <bool RECOVER, bool NT, int GPW, int U = 2, int WAVES = kFlatWaves, bool BF = false>
+__global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) {
+  constexpr int ACC = 1;
+  constexpr uint32_t kAccWords = 4 * kParWin;
+  __shared__ uint32_t s_par[WAVES][GPW * kAccWords];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * WAVES + wv) * GPW;
+  if (g0 >= a.n_groups) return;
+  const uint32_t ng = (uint32_t)min<uint64_t>((uint64_t)GPW, a.n_groups - g0);
+  uint32_t* par = s_par[wv];
+  uint64_t* head = s_head[wv];
+  u32x4* meta = s_meta[wv];
+
+  // wave-uniform group scalars
+  uint32_t kb[GPW + 1], rb[GPW + 1], mm[GPW], pl[GPW];
+  uint64_t doff[GPW];
+  const uint32_t P0 = a.grp_ptr[g0];
+  bool ok = true;
+  kb[0] = rb[0] = 0;
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    uint32_t k = 0, m = 0xFFFFFFFFu, p = 0;
+    uint64_t d = 0;
+    if ((uint32_t)j < ng) {
+      k = a.grp_ptr[g0 + j + 1] - P0 - kb[j];
+      if constexpr (RECOVER) {
+        m = a.missing[g0 + j];
+        p = a.parity_len[g0 + j];
+        d = a.out_off[g0 + j];
+        ok = ok && m < k && p >= 16u && p <= kMaxPacket;
+      } else {
+        d = a.parity_off[g0 + j];
+      }
+      ok = ok && k >= 1u && k <= 255u;
+    }
+    kb[j + 1] = kb[j] + k;
+    rb[j + 1] = rb[j] + (RECOVER && k ? k - 1u : k);
+    mm[j] = m;
+    pl[j] = p;
+    doff[j] = d;
+  }
+  const uint32_t R = rb[GPW];
+  ok = ok && R <= 64u;
+
+  // lane r: received packet r of the wave's groups
+  uint32_t jl = 0, base = 0, kbase = 0, ml = 0xFFFFFFFFu, lim = kMaxPacket;
+#pragma unroll
+  for (int j = 1; j < GPW; ++j) {
+    const bool in = lane >= rb[j];
+    jl += in ? 1u : 0u;
+    base = in ? rb[j] : base;
+    kbase = in ? kb[j] : kbase;
+  }
+  ml = sel_n<GPW>(mm, jl);
+  if constexpr (RECOVER) lim = sel_n<GPW>(pl, jl);
+  uint32_t len = 0, offlo = 0, offhi = 0;
+  if (ok && lane < R) {
+    const uint32_t i = lane - base;
+    const uint32_t p = P0 + kbase + i + (RECOVER && i >= ml ? 1u : 0u);
+    len = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    offlo = (uint32_t)o;
+    offhi = (uint32_t)(o >> 32);
+  }
+  // accumulators: the parity rows (recover) or zero (encode)
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      uint32_t* acc = par + j * kAccWords;
+      if constexpr (RECOVER) {
+        const uint8_t* prow = a.parity + ((uint32_t)j < ng ? a.parity_off[g0 + j] : 0ull);
+        const uint32_t plj = (uint32_t)j < ng ? pl[j] : 0u;
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        u32x4 w0 = zero, w1 = zero;
+        if (16u * lane < plj) w0 = packet_window<NT>(prow, plj, lane);
+        if (16u * (lane + 64u) < plj) w1 = packet_window<NT>(prow, plj, lane + 64u);
+        lds_put16<ACC>(acc, lane, w0);
+        if (lane + 64u < kParWin) lds_put16<ACC>(acc, lane + 64u, w1);
+      } else {
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(acc, t, zero);
+      }
+    }
+  }
+  const bool odd = lane < R && (len < 16u || len > lim);
+  if (!ok || wave_any(odd)) {
+    // per-group body (exact error semantics of the one-group kernel)
+    for (uint32_t j = 0; j < ng; ++j) {
+      GroupPrefetch f;
+      group_scalars<RECOVER>(a, g0 + j, f);
+      group_vectors<RECOVER, NT>(a, g0 + j, lane, f);
+      wave_lds_order();
+      ragged_group<RECOVER, NT, U, ACC, BF>(a, g0 + j, lane, f, par, head, meta);
+      wave_lds_order();
+    }
+    return;
+  }
+  const uint32_t n = (len + 15u) >> 4;
+  const uint32_t incl = wave_incl_scan(n, lane);
+  const uint32_t S = incl - n;
+  const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t nit = (W + 63u) >> 6;  // W <= 64 x 91
+  for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
+  wave_lds_order();
+  if (lane < R) {
+    meta[lane] = u32x4{offlo, offhi, len | (jl << 16), S};
+    __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  wave_lds_order();  // accumulators, packet table and start mask complete
+  const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+  const uint32_t last = R - 1u;
+  uint32_t before = 0;
+  for (uint32_t it = 0; it < nit; it += U) {
+    uint64_t M[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) M[u] = it + u < nit ? head[it + u] : 0ull;
+    u32x4 md[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
+      before += (uint32_t)__popcll(M[u]);
+      md[u] = meta[pi];
+    }
+    u32x4 v[U];
+    uint32_t tt[U], sh[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t fl = 64u * (it + u) + lane;
+      const uint32_t ln = md[u].z & 0xFFFFu;
+      const uint32_t win = 16u * (fl - md[u].w);
+      const bool full = win + 16u <= ln;
+      v[u] = ld16t<NT>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) + (full ? win : ln - 16u));
+      sh[u] = full ? 0u : min(win + 16u - ln, 15u);
+      tt[u] = fl < W ? (md[u].z >> 16) * kAccWords + (fl - md[u].w) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tt[u] != 0xFFFFFFFFu) lds_xor16<ACC>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+  }
+  if constexpr (!RECOVER) {
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      pl[j] = wave_max11(lane < R && jl == (uint32_t)j ? len : 0u);
+      if (lane == 0 && (uint32_t)j < ng) a.parity_len_out[g0 + j] = (uint16_t)pl[j];
+    }
+  }
+  wave_lds_order();  // every lane's XORs done
+  // write-out, flattened over the groups' output windows
+  uint32_t ob[GPW + 1];
+  ob[0] = 0;
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) ob[j + 1] = ob[j] + ((uint32_t)j < ng ? (pl[j] + 15u) >> 4 : 0u);
+  const uint32_t NW = ob[GPW];
+  for (uint32_t q = lane; q < NW; q += 64u) {
+    uint32_t jq = 0, qb = 0;
+#pragma unroll
+    for (int j = 1; j < GPW; ++j) {
+      const bool in = q >= ob[j];
+      jq += in ? 1u : 0u;
+      qb = in ? ob[j] : qb;
+    }
+    const uint32_t t = q - qb;
+    const uint32_t plen = sel_n<GPW>(pl, jq);
+    uint8_t* dst = a.out + sel_n<GPW>(doff, jq);
+    const uint32_t* acc = par + jq * kAccWords;
+    if (16u * t + 16u <= plen) {
+      st16t<NT>(dst + 16u * t, lds_get16<ACC>(acc, t));
+    } else {
+      const uint32_t o = plen - 16u * t;  // 1..15
+      const u32x4 lo = lds_get16<ACC>(acc, t - 1u), hi = lds_get16<ACC>(acc, t);
+      const uint64_t a0 = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+      const uint64_t a1 = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+      const uint64_t a2 = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+      const uint64_t a3 = (uint64_t)hi.z | ((uint64_t)hi.w << 32);
+      const uint64_t w0 = o < 8u ? a0 : a1, w1 = o < 8u ? a1 : a2, w2 = o < 8u ? a2 : a3;
+      const uint32_t s = (o & 7u) * 8u;
+      const uint64_t r0 = (w0 >> s) | ((w1 << 1) << (63u - s));
+      const uint64_t r1 = (w1 >> s) | ((w2 << 1) << (63u - s));
+      st16t<NT>(dst + plen - 16u, u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1,
+                                        (uint32_t)(r1 >> 32)});
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // out ^= in (XorBuffers).
 // ---------------------------------------------------------------------------
@@ -787,7 +996,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
 
 hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
   if (a0.n_groups == 0) return hipSuccess;
-  const uint64_t gpb = kBlock / 64;  // one wave per group
+  const uint64_t gpb = (kBlock / 64) * kRaggedGPW;  // kRaggedGPW groups per wave
   const uint64_t maxg = 0x7FFFFFFFull * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     RaggedArgs a = a0;
@@ -804,11 +1013,11 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
     }
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
     if (recover)
-      hipLaunchKernelGGL((ragged_xor_kernel<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0,
-                         s, a);
+      hipLaunchKernelGGL((ragged_multi_kernel<true, true, kRaggedGPW>), dim3((uint32_t)blocks),
+                         dim3(kBlock), 0, s, a);
     else
-      hipLaunchKernelGGL((ragged_xor_kernel<false, true>), dim3((uint32_t)blocks), dim3(kBlock),
-                         0, s, a);
+      hipLaunchKernelGGL((ragged_multi_kernel<false, true, kRaggedGPW>), dim3((uint32_t)blocks),
+                         dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -1,5 +1,6 @@
-// tune_multi.hip — A/B of the ragged kernel with GPW groups per wave
-// (multi_ragged.inc) against the product one-group-per-wave kernel, encode and
+// tune_multi.hip — A/B of the ragged kernels: GPW groups per wave
+// (ragged_multi_kernel; the product runs GPW = 2) against one group per wave
+// (ragged_xor_kernel), branch-free / aligned-chunk / XCD variants, encode and
 // recover on the BASELINE configs[3] batch (2^20 groups, k 5-15, 64-1350 B,
 // packed CSR).  Every variant's output bytes are compared with the product's.
 //
@@ -9,7 +10,6 @@
 //        parity lengths) instead of 1452-byte slots
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
 #include "al_ragged.inc"
-#include "multi_ragged.inc"
 
 #include <algorithm>
 #include <cstdio>
@@ -63,6 +63,12 @@ template <bool REC, int U>
 static void launch_al(const RaggedArgs& a, uint64_t G) {
   hipLaunchKernelGGL((qfec::ragged_al_kernel<REC, true, U, 4, 1>),
                      dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
+}
+
+template <bool REC>
+static void launch_1g(const RaggedArgs& a, uint64_t G) {
+  hipLaunchKernelGGL((qfec::ragged_xor_kernel<REC, true>), dim3((uint32_t)((G + 3) / 4)), dim3(256),
+                     0, 0, a);
 }
 
 template <bool REC>
@@ -167,6 +173,7 @@ int main(int argc, char** argv) {
   vs.push_back({"BF U4 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 4>(a, G); }});
   vs.push_back({"BF U6 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 6>(a, G); }});
   vs.push_back({"multi2 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4>(a, G); }});
+  vs.push_back({"1 group/wave encode", false, [=](const RaggedArgs& a) { launch_1g<false>(a, G); }});
   vs.push_back({"multi3 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, 4>(a, G); }});
   vs.push_back({"product XCD encode", false, [=](const RaggedArgs& a) { launch_xcd<false>(a, G); }});
   vs.push_back({"product recover", true, [](const RaggedArgs& a) { CK(qfec::launch_ragged(a, true, 0)); }});
@@ -179,6 +186,7 @@ int main(int argc, char** argv) {
   vs.push_back({"BF U4 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 4>(a, G); }});
   vs.push_back({"BF U6 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 6>(a, G); }});
   vs.push_back({"multi2 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4>(a, G); }});
+  vs.push_back({"1 group/wave recover", true, [=](const RaggedArgs& a) { launch_1g<true>(a, G); }});
   vs.push_back({"multi3 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, 4>(a, G); }});
   vs.push_back({"product XCD recover", true, [=](const RaggedArgs& a) { launch_xcd<true>(a, G); }});
 
