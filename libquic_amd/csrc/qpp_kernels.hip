@@ -440,7 +440,39 @@ struct Poly1305 {
   uint32_t r0, r1, r2, r3, r4;
   uint32_t h0, h1, h2, h3, h4;
   uint32_t pad[4];
+  uint32_t q0, q1, q2, q3, q4;  // r^2 mod 2^130 - 5 (poly_block2)
 };
+
+// Unreduced product of 26-bit limbs a (each < 2^27) and r (r^2 or r), into d.
+__device__ __forceinline__ void poly_mul_acc(uint64_t (&d)[5], const uint32_t (&a)[5], uint32_t r0,
+                                             uint32_t r1, uint32_t r2, uint32_t r3, uint32_t r4) {
+  const uint32_t s1 = r1 * 5u, s2 = r2 * 5u, s3 = r3 * 5u, s4 = r4 * 5u;
+  d[0] += (uint64_t)a[0] * r0 + (uint64_t)a[1] * s4 + (uint64_t)a[2] * s3 + (uint64_t)a[3] * s2 +
+          (uint64_t)a[4] * s1;
+  d[1] += (uint64_t)a[0] * r1 + (uint64_t)a[1] * r0 + (uint64_t)a[2] * s4 + (uint64_t)a[3] * s3 +
+          (uint64_t)a[4] * s2;
+  d[2] += (uint64_t)a[0] * r2 + (uint64_t)a[1] * r1 + (uint64_t)a[2] * r0 + (uint64_t)a[3] * s4 +
+          (uint64_t)a[4] * s3;
+  d[3] += (uint64_t)a[0] * r3 + (uint64_t)a[1] * r2 + (uint64_t)a[2] * r1 + (uint64_t)a[3] * r0 +
+          (uint64_t)a[4] * s4;
+  d[4] += (uint64_t)a[0] * r4 + (uint64_t)a[1] * r3 + (uint64_t)a[2] * r2 + (uint64_t)a[3] * r1 +
+          (uint64_t)a[4] * r0;
+}
+
+// d (limb sums < 2^60) -> 26-bit limbs: h0..h4 with h1 < 2^26 + 2^10.
+__device__ __forceinline__ void poly_carry(const uint64_t (&d0)[5], uint32_t (&h)[5]) {
+  uint64_t d1 = d0[1] + (d0[0] >> 26), d2 = d0[2], d3 = d0[3], d4 = d0[4];
+  d2 += d1 >> 26;
+  d3 += d2 >> 26;
+  d4 += d3 >> 26;
+  const uint64_t c = d4 >> 26;
+  const uint64_t h0 = (d0[0] & 0x3ffffffu) + c * 5u;
+  h[1] = (uint32_t)(d1 & 0x3ffffffu) + (uint32_t)(h0 >> 26);
+  h[0] = (uint32_t)(h0 & 0x3ffffffu);
+  h[2] = (uint32_t)(d2 & 0x3ffffffu);
+  h[3] = (uint32_t)(d3 & 0x3ffffffu);
+  h[4] = (uint32_t)(d4 & 0x3ffffffu);
+}
 
 __device__ __forceinline__ void poly_init(Poly1305& p, const uint32_t (&k)[16]) {
   // r clamp (RFC 7539 §2.5) in 26-bit limbs
@@ -454,6 +486,50 @@ __device__ __forceinline__ void poly_init(Poly1305& p, const uint32_t (&k)[16]) 
   p.pad[1] = k[5];
   p.pad[2] = k[6];
   p.pad[3] = k[7];
+  // r^2 for two blocks per step (poly_block2)
+  const uint32_t r[5] = {p.r0, p.r1, p.r2, p.r3, p.r4};
+  uint64_t d[5] = {0u, 0u, 0u, 0u, 0u};
+  poly_mul_acc(d, r, p.r0, p.r1, p.r2, p.r3, p.r4);
+  uint32_t q[5];
+  poly_carry(d, q);
+  p.q0 = q[0];
+  p.q1 = q[1];
+  p.q2 = q[2];
+  p.q3 = q[3];
+  p.q4 = q[4];
+}
+
+__device__ __forceinline__ void poly_limbs(u32x4 m, uint32_t (&a)[5]) {  // block + 2^128
+  a[0] = m.x & 0x3ffffffu;
+  a[1] = ((m.x >> 26) | (m.y << 6)) & 0x3ffffffu;
+  a[2] = ((m.y >> 20) | (m.z << 12)) & 0x3ffffffu;
+  a[3] = ((m.z >> 14) | (m.w << 18)) & 0x3ffffffu;
+  a[4] = (m.w >> 8) | (1u << 24);
+}
+
+// Two blocks at once: h = ((h + m1) r + m2) r = (h + m1) r^2 + m2 r — two
+// independent products and one carry chain, where poly_block twice is two
+// products and two carry chains in series.  Limb sums stay below 2^59
+// (a < 2^27, 5 r^2 < 2^28.4; the m2 r products below 2^57).
+__device__ __forceinline__ void poly_block2(Poly1305& p, u32x4 m1, u32x4 m2) {
+  uint32_t a[5], b[5];
+  poly_limbs(m1, a);
+  a[0] += p.h0;
+  a[1] += p.h1;
+  a[2] += p.h2;
+  a[3] += p.h3;
+  a[4] += p.h4;
+  poly_limbs(m2, b);
+  uint64_t d[5] = {0u, 0u, 0u, 0u, 0u};
+  poly_mul_acc(d, a, p.q0, p.q1, p.q2, p.q3, p.q4);
+  poly_mul_acc(d, b, p.r0, p.r1, p.r2, p.r3, p.r4);
+  uint32_t h[5];
+  poly_carry(d, h);
+  p.h0 = h[0];
+  p.h1 = h[1];
+  p.h2 = h[2];
+  p.h3 = h[3];
+  p.h4 = h[4];
 }
 
 // h = (h + m + 2^128) * r mod 2^130 - 5 for one full 16-byte block.
@@ -607,17 +683,27 @@ __device__ __forceinline__ void aead_pass(const ChachaKey& key, Poly1305& poly,
       if (c0 >= my_nfull) break;
       uint32_t ks[16];
       if constexpr (XOR) chacha_block(key, 1u + c0 / 4u, ks);
+      // the MAC takes the chunks in pairs (poly_block2); a lone last chunk
+      // of the packet goes through poly_block
+      u32x4 mac[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
-        if (c0 + j < my_nfull) {
-          u32x4& slot = rows[lane * (SC + 1u) + 4u * b + j];
-          u32x4 v = slot;
-          if constexpr (MAC_IN) poly_block(poly, v);
-          if constexpr (XOR) {
-            v ^= ks_chunk(ks, j);
-            slot = v;
-          }
-          if constexpr (MAC_OUT) poly_block(poly, v);
+        u32x4& slot = rows[lane * (SC + 1u) + 4u * b + j];
+        u32x4 v = slot;
+        if constexpr (MAC_IN) mac[j] = v;
+        if constexpr (XOR) {
+          v ^= ks_chunk(ks, j);
+          if (c0 + j < my_nfull) slot = v;
+        }
+        if constexpr (MAC_OUT) mac[j] = v;
+      }
+      if constexpr (MAC_IN || MAC_OUT) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; j += 2u) {
+          if (c0 + j + 1u < my_nfull)
+            poly_block2(poly, mac[j], mac[j + 1u]);
+          else if (c0 + j < my_nfull)
+            poly_block(poly, mac[j]);
         }
       }
     }
