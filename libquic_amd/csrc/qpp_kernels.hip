@@ -1210,8 +1210,9 @@ __device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, ui
 // 768-thread blocks: the 64 KiB table is shared by 12 waves with 64-B slabs
 // (SC = 4): LDS 154 KiB per block = one block per CU = 3 waves/SIMD, which the
 // key-uniform path's SGPR round keys make fit in 168 VGPRs (148 used).
-// Measured vs 512 threads / SC = 8 / 2 waves: seal +6.5%, open +1.3%
-// (profiles/round1/tune_gcm_g8.txt).
+// Measured vs 512 threads / SC = 8 / 2 waves at 2^21 packets: seal +6.5%,
+// open +1.3% (profiles/round1/tune_gcm_g8.txt); smaller batches and open run
+// the 512-thread shape instead (launch_aes128gcm picks by batch size).
 constexpr int kGcmBlock = 768;
 constexpr int kGcmSC = 4;   // 16-B chunks per packet per slab
 constexpr int kGcmWPE = 3;  // waves per SIMD
@@ -1432,10 +1433,21 @@ hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t
 
 namespace qfec {
 
-// AES-128-GCM: 64-B slabs at 3 waves/SIMD (see kGcmBlock).
-hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
-  constexpr uint32_t SC = kGcmSC;
-  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kGcmBlock;
+// AES-128-GCM block shape by batch: both shapes fill the LDS (one block per
+// CU), so a grid of blocks/256 rounds leaves its last round partly idle.
+// Measured seal / open (tools/tune/tune_gcm.hip, profiles/round1/tune_gcm_gq_*.txt):
+// 512 threads / 128-B slabs / 2 waves per SIMD against the 768-thread shape
+// (64-B slabs, 3 waves): 1.30x / 1.30x at 2^16 packets, 1.27x / 1.30x at
+// 2^18, 1.04x / 1.05x at 2^20, 1.00x / 1.04x at 2^22.  Seal keeps the
+// 768-thread shape from 2^22 packets on (+3% at 2^21 measured earlier,
+// tune_gcm_g12.txt); open always takes 512.
+constexpr uint64_t kGcmSeal768From = 1ull << 22;
+
+template <bool OPEN, int BLOCK>
+hipError_t launch_gcm_shape(const AeadArgs& a0, hipStream_t s) {
+  constexpr uint32_t SC = BLOCK == 768 ? 4u : 8u;
+  constexpr int WPE = BLOCK == 768 ? 3 : 2;
+  const uint64_t chunk = (uint64_t)0x7FFFFFFF * BLOCK;
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;
     a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;
@@ -1444,19 +1456,23 @@ hipError_t launch_aes128gcm(const AeadArgs& a0, bool decrypt, hipStream_t s) {
     a.io.in_off += p;
     a.io.in_len += p;
     a.io.out_off += p;
-    if (decrypt) a.io.ok += p;
+    if (OPEN) a.io.ok += p;
     a.key_idx += p;
     a.packet_number += p;
     if (a.path_id) a.path_id += p;
-    const uint32_t blocks = (uint32_t)((a.io.n + kGcmBlock - 1) / kGcmBlock);
-    if (decrypt)
-      hipLaunchKernelGGL((aes128gcm_kernel<SC, true>), dim3(blocks), dim3(kGcmBlock), 0, s, a);
-    else
-      hipLaunchKernelGGL((aes128gcm_kernel<SC, false>), dim3(blocks), dim3(kGcmBlock), 0, s, a);
+    const uint32_t blocks = (uint32_t)((a.io.n + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL((aes128gcm_kernel<SC, OPEN, kGcmNB, BLOCK, WPE>), dim3(blocks), dim3(BLOCK),
+                       0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_aes128gcm(const AeadArgs& a, bool decrypt, hipStream_t s) {
+  if (decrypt) return launch_gcm_shape<true, 512>(a, s);
+  return a.io.n >= kGcmSeal768From ? launch_gcm_shape<false, 768>(a, s)
+                                   : launch_gcm_shape<false, 512>(a, s);
 }
 
 }  // namespace qfec

@@ -264,6 +264,9 @@ int main(int argc, char** argv) {
       {"open product", dec_b, [&] { open_new(ao); }},
       {"open first kernel", dec_b, [&] { open_old(ao); }},
       GCMV("seal SC8 512 wpe2 per-lane keys", enc_b, as, 8, false, 4, 512, 2, false),
+      GCMV("seal SC8 512 wpe2 uniform keys", enc_b, as, 8, false, 4, 512, 2, true),
+      GCMV("open SC8 512 wpe2 uniform keys", dec_b, ao, 8, true, 4, 512, 2, true),
+      GCMV("open SC8 512 wpe2 per-lane keys", dec_b, ao, 8, true, 4, 512, 2, false),
       GCMV("seal SC4 768 wpe3 uniform keys", enc_b, as, 4, false, 4, 768, 3, true),
       GCMV("seal SC4 768 wpe3 NB2", enc_b, as, 4, false, 2, 768, 3, true),
       GCMV("open SC4 768 wpe3 uniform keys", dec_b, ao, 4, true, 4, 768, 3, true),
