@@ -147,3 +147,49 @@ def test_seal_open_random_vs_oracle(ctx, nkeys, lmax):
     good = np.repeat(ok.astype(bool), in_len.astype(np.int64))
     assert np.array_equal(out[:good.size][good], w_out[:good.size][good])
     assert (out[:good.size][~good] == 0xA5).all()
+
+
+
+def test_block_shapes_agree_on_large_batch(ctx):
+    """launch_aes128gcm seals batches of >= 2^22 packets with the 768-thread
+    shape and smaller ones with the 512-thread shape: the same 2^22 packets
+    sealed in one call and in two halves (in place, [header | payload | 12
+    spare] records) must give the same bytes, and the (512-thread) open must
+    verify every one of them.  Device-side compare."""
+    n = 1 << 22
+    rng = np.random.default_rng(41)
+    hdr = 13
+    pt_len = rng.integers(0, 81, n).astype(np.uint16)
+    rec = hdr + pt_len.astype(np.uint64) + TAG
+    ad_off = offsets(rec)
+    in_off = ad_off + np.uint64(hdr)
+    ad_len = np.full(n, hdr, np.uint16)
+    total = int(ad_off[-1] + rec[-1])
+    nkeys = 5
+    keys = rng.integers(0, 256, 16 * nkeys, dtype=np.uint8)
+    pre = rng.integers(0, 256, 4 * nkeys, dtype=np.uint8)
+    kidx = (np.arange(n, dtype=np.uint32) // 192) % nkeys  # mostly key-uniform waves
+    pn = np.arange(1, n + 1, dtype=np.uint64)
+    d = {k: dv(v) for k, v in dict(ad_off=ad_off, ad_len=ad_len, in_off=in_off, in_len=pt_len,
+                                     keys=keys, pre=pre, kidx=kidx, pn=pn).items()}
+    base = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    whole, halves = base.clone(), base.clone()
+    ctx.aes128gcm_seal(d["keys"], d["pre"], d["kidx"], d["pn"], None, whole, d["ad_off"],
+                       d["ad_len"], d["in_off"], d["in_len"], n, whole, d["in_off"])
+    h = n // 2
+    for lo in (0, h):
+        sl = slice(lo, lo + h)
+        ctx.aes128gcm_seal(d["keys"], d["pre"], d["kidx"][sl], d["pn"][sl], None, halves,
+                           d["ad_off"][sl], d["ad_len"][sl], d["in_off"][sl], d["in_len"][sl], h,
+                           halves, d["in_off"][sl])
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert torch.equal(whole, halves)
+    ok = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    pout = torch.zeros(int(pt_len.astype(np.int64).sum()) + 1, dtype=torch.uint8, device=DEV)
+    ctx.aes128gcm_open(d["keys"], d["pre"], d["kidx"], d["pn"], None, whole, d["ad_off"],
+                       d["ad_len"], d["in_off"], dv((pt_len.astype(np.uint32) + TAG).astype(np.uint16)),
+                       n, pout, dv(offsets(pt_len.astype(np.uint64))), ok)
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert bool(ok.all())
