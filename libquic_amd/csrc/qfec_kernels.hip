@@ -22,7 +22,8 @@
 //    L2/TA handle the line crossing.
 //  * Recover reads the parity row *in place of* the lost row: k loads per lane,
 //    every one unconditional — the lost slot is never read and no lane idles.
-//  * Ragged CSR batches: one wave per group, lanes own 16-byte windows of the
+//  * Ragged CSR batches: two groups per wave (ragged_multi_kernel; the
+//    one-group body below is its exact fallback), lanes own 16-byte windows of the
 //    parity; a packet shorter than the window is loaded as the 16 bytes that
 //    end at its last byte and shifted down (zero fill), so again no load leaves
 //    the packet.
@@ -198,7 +199,8 @@ __global__ __launch_bounds__(kBlock) void fixed_small_kernel(FixedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Ragged CSR: one wave per group.
+// Ragged CSR: the per-group body (one wave per group) and, below it, the
+// two-groups-per-wave product kernel.
 // ---------------------------------------------------------------------------
 // Right shift of a 16-byte vector by sh bytes (0..15), zero fill, branch-free:
 // one 64-bit select for the 8-byte step, then 64-bit funnel shifts
@@ -589,7 +591,8 @@ __device__ __forceinline__ void ragged_group(const RaggedArgs& a, uint64_t g, ui
   }
 }
 
-// One short-lived wave per group.
+// One short-lived wave per group (the A/B reference; launch_ragged runs
+// ragged_multi_kernel).
 template <bool RECOVER, bool NT, int U = 2, int WAVES = kFlatWaves, int ACC = 1, bool BF = false,
           bool XCD = false>
 __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
