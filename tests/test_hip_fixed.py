@@ -219,7 +219,9 @@ def test_torch_stream(ctx):
         ctx.set_stream(s)
         ctx.encode(d_rows, k, L, n, par)
         res = par.cpu()  # ordered on s
-    ctx.set_stream(None)
+    # back to the session's setting (conftest: torch's current stream), so later
+    # tests' torch fills stay ordered with the context's launches
+    ctx.set_stream(torch.cuda.current_stream())
     s.synchronize()
     assert np.array_equal(res.numpy(), want_p)
 

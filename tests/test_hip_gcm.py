@@ -174,6 +174,7 @@ def test_block_shapes_agree_on_large_batch(ctx):
                                      keys=keys, pre=pre, kidx=kidx, pn=pn).items()}
     base = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
     whole, halves = base.clone(), base.clone()
+    torch.cuda.synchronize()  # the context may run on a stream of its own
     ctx.aes128gcm_seal(d["keys"], d["pre"], d["kidx"], d["pn"], None, whole, d["ad_off"],
                        d["ad_len"], d["in_off"], d["in_len"], n, whole, d["in_off"])
     h = n // 2
