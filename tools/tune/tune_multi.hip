@@ -46,10 +46,10 @@ static T* up(const std::vector<T>& v) {
 
 using qfec::RaggedArgs;
 
-template <bool REC, int GPW, int WAVES>
+template <bool REC, int GPW, int WAVES, int U = 2>
 static void launch_multi(const RaggedArgs& a, uint64_t G) {
   const uint64_t per = (uint64_t)GPW * WAVES;
-  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, true, GPW, 2, WAVES>),
+  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, true, GPW, U, WAVES>),
                      dim3((uint32_t)((G + per - 1) / per)), dim3(64 * WAVES), 0, 0, a);
 }
 
@@ -173,6 +173,10 @@ int main(int argc, char** argv) {
   vs.push_back({"BF U4 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 4>(a, G); }});
   vs.push_back({"BF U6 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 6>(a, G); }});
   vs.push_back({"multi2 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4>(a, G); }});
+  vs.push_back({"multi2 w4 U1 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4, 1>(a, G); }});
+  vs.push_back({"multi2 w4 U3 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4, 3>(a, G); }});
+  vs.push_back({"multi2 w2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 2>(a, G); }});
+  vs.push_back({"multi2 w8 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 8>(a, G); }});
   vs.push_back({"1 group/wave encode", false, [=](const RaggedArgs& a) { launch_1g<false>(a, G); }});
   vs.push_back({"multi3 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, 4>(a, G); }});
   vs.push_back({"product XCD encode", false, [=](const RaggedArgs& a) { launch_xcd<false>(a, G); }});
@@ -186,6 +190,10 @@ int main(int argc, char** argv) {
   vs.push_back({"BF U4 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 4>(a, G); }});
   vs.push_back({"BF U6 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 6>(a, G); }});
   vs.push_back({"multi2 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4>(a, G); }});
+  vs.push_back({"multi2 w4 U1 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4, 1>(a, G); }});
+  vs.push_back({"multi2 w4 U3 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4, 3>(a, G); }});
+  vs.push_back({"multi2 w2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 2>(a, G); }});
+  vs.push_back({"multi2 w8 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 8>(a, G); }});
   vs.push_back({"1 group/wave recover", true, [=](const RaggedArgs& a) { launch_1g<true>(a, G); }});
   vs.push_back({"multi3 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, 4>(a, G); }});
   vs.push_back({"product XCD recover", true, [=](const RaggedArgs& a) { launch_xcd<true>(a, G); }});
