@@ -281,6 +281,9 @@ def main():
 
     if not args.profile_only and rank == 0 and world == 1 and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
+        if line["roofline"]:  # the encode kernel against this box's measured streaming read
+            line["ceilings"]["encode_frac_of_read_ceiling"] = round(
+                line["roofline"]["achieved"] / line["ceilings"]["read_GBps"], 4)
     if not args.profile_only and rank == 0 and world == 1:
         work.release()
         ctx, stream = work.ctx, work.stream
