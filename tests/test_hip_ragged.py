@@ -190,3 +190,47 @@ def test_cpp_quic_fec_group():
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stderr
     assert " 0 failures" in r.stdout
+
+
+@pytest.mark.parametrize("host", [False, True])
+def test_ragged_pair_boundaries(ctx, host):
+    """launch_ragged runs two consecutive groups per wave (groups 2w, 2w+1) in
+    one flat window space when their received packets fit the 64-lane table,
+    all are >= 16 B and every field is valid; otherwise the per-group body.
+    Pairs straddling each switch: 63 / 64 / 65 received packets (encode: k;
+    recover: k - 1), a packet below 16 B in one group, a redundancy shorter
+    than 16 B, k = 1 next to k = 255, and an odd group count (the last wave
+    holds one group).  Against the oracle, bit-exact."""
+    rng = np.random.default_rng(11)
+
+    def grp(k, lo=16, hi=1452):
+        return list(rng.integers(lo, hi + 1, k))
+    groups = [grp(32), grp(31),          # 63 received (encode), 61 (recover)
+              grp(32), grp(32),          # 64 / 62
+              grp(32), grp(33),          # 65 / 63
+              grp(33), grp(33),          # 66 / 64: recover fits, encode falls back
+              grp(33), grp(34),          # 67 / 65
+              grp(5) + [15], grp(6),     # a packet below 16 B: both fall back
+              [10, 12], grp(3),          # redundancy below 16 B (recover fallback)
+              grp(1), grp(255, 1, 1452),  # k = 1 next to k = 255
+              grp(7)]                    # odd count: one group in the last wave
+    ln = np.array([l for g in groups for l in g], np.uint16)
+    ptr = np.zeros(len(groups) + 1, np.uint32)
+    ptr[1:] = np.cumsum([len(g) for g in groups])
+    gap = rng.integers(0, 9, ln.size).astype(np.uint64)
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gap[:-1])
+    data = rng.integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    n = len(groups)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1460) + np.uint64(5)
+    miss = np.array([rng.integers(0, len(g)) for g in groups], np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1460 + 5)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1460 + 5)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged(ctx, z, host=host)
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
