@@ -1438,7 +1438,8 @@ namespace qfec {
 // Measured seal / open (tools/tune/tune_gcm.hip, profiles/round1/tune_gcm_gq_*.txt):
 // 512 threads / 128-B slabs / 2 waves per SIMD against the 768-thread shape
 // (64-B slabs, 3 waves): 1.30x / 1.30x at 2^16 packets, 1.27x / 1.30x at
-// 2^18, 1.04x / 1.05x at 2^20, 1.00x / 1.04x at 2^22.  Seal keeps the
+// 2^18, 1.04x / 1.05x at 2^20, 1.00x / 1.04x at 2^22, 0.95x / 1.01x at
+// 2^23.  Seal keeps the
 // 768-thread shape from 2^22 packets on (+3% at 2^21 measured earlier,
 // tune_gcm_g12.txt); open always takes 512.
 constexpr uint64_t kGcmSeal768From = 1ull << 22;
