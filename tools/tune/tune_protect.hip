@@ -162,6 +162,10 @@ int main(int argc, char** argv) {
          hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<16>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
       {"chacha20poly1305 open SC=16", dec_b, hashed, [&] {
          hipLaunchKernelGGL(qfec::c20p1305_open_kernel<16>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, ao); }},
+      {"chacha20poly1305 seal SC=8", enc_b, hashed, [&] {
+         hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<8>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
+      {"chacha20poly1305 open SC=8", dec_b, hashed, [&] {
+         hipLaunchKernelGGL(qfec::c20p1305_open_kernel<8>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, ao); }},
       {"chacha20poly1305 seal SC=4", enc_b, hashed, [&] {
          hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<4>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
       {"null encrypt staged SC=4", enc_b, hashed, [&] {
