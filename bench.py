@@ -34,9 +34,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md (spec 8.0 TB/s)
 SEED_FIXED, SEED_RAGGED, SEED_DROP = 0x51554943, 0x51554944, 0x51554945
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one process per GPU); without WORLD_SIZE in the environment "
+                        "bench.py starts them itself")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--groups", type=int, default=1 << 20, help="FEC groups per GPU")
@@ -49,12 +51,19 @@ def parse():
     p.add_argument("--no-ragged", action="store_true")
     p.add_argument("--no-protect", action="store_true")
     p.add_argument("--no-entropy", action="store_true")
+    p.add_argument("--no-connection", action="store_true")
+    p.add_argument("--no-fused", action="store_true")
     p.add_argument("--no-ceilings", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU-baseline threads (default: every host CPU)")
+    p.add_argument("--cpu-workload", action="store_true",
+                   help="test switch: numpy stand-in for the GPU step over gloo (no GPU); "
+                        "exercises the rank launch / shard / timing / JSON path on a CPU box")
     p.add_argument("--profile-only", action="store_true",
                    help="only the device-resident steps (for rocprofv3 runs)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def drop_indices(g0, n, k):
@@ -62,48 +71,58 @@ def drop_indices(g0, n, k):
     return synth.drop_indices(SEED_DROP, np.arange(g0, g0 + n, dtype=np.uint64), k).astype(np.uint8)
 
 
-def cpu_baseline(k, L, seconds):
-    """Oracle (C restatement) on the host cores, bounded sample (rank 0, N=1)."""
-    from oracle import oracle_c as OC
-    lib = OC.lib()
-    threads = min(16, os.cpu_count() or 1)
-    n = 1 << 16  # 65,536 groups = 885 MB of rows
-    rows = OC.synth_fixed(SEED_FIXED, 0, n, k, L)
-    par = np.zeros(n * L, np.uint8)
-    out = np.zeros(n * L, np.uint8)
-    miss = drop_indices(0, n, k)
-    bytes_per_pass = 2 * n * (k * L + L)  # encode + recover algorithmic bytes
-
-    def run(th):
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            lib.qo_encode_fixed_mt(OC._p(rows), k, L, n, OC._p(par), th)
-            lib.qo_recover_fixed_mt(OC._p(rows), OC._p(par), OC._p(miss), k, L, n, OC._p(out), th)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 2:
-                return reps * bytes_per_pass / el / 2**30, reps
-
-    mt, reps_mt = run(threads)
-    st, reps_st = run(1)
-    # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
-    ns_group = lib.qo_time_single_group_ns(k, L, 200000)
-    cpu_model = ""
+def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return ""
+
+
+def cpu_baseline(rows, G, k, L, seconds, threads=0):
+    """The CPU FEC path (the oracle's C restatement: word-wise uint64 XOR +
+    byte tail, contiguous group split over pthreads) on the host cores, over
+    the SAME workload the GPU step runs — G groups x k x L, encode + recover —
+    timed on every host CPU and on one core, plus configs[0] (one group).
+    `rows` is the step's input copied to host memory."""
+    from oracle import oracle_c as OC
+    lib = OC.lib()
+    threads = threads or min(256, os.cpu_count() or 1)
+    par = np.zeros(G * L, np.uint8)
+    out = np.zeros(G * L, np.uint8)
+    miss = drop_indices(0, G, k)
+    bytes_per_pass = G * (k * L + L) + G * ((k - 1) * L + 2 * L)
+
+    def one(th):
+        assert lib.qo_encode_fixed_mt(OC._p(rows), k, L, G, OC._p(par), th) == 0
+        assert lib.qo_recover_fixed_mt(OC._p(rows), OC._p(par), OC._p(miss), k, L, G,
+                                       OC._p(out), th) == 0
+
+    def run(th, budget):
+        one(th)  # untimed: faults the output pages in
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            one(th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return reps * bytes_per_pass / el / 2**30, reps, el
+
+    mt, reps_mt, el_mt = run(threads, seconds / 2)
+    st, reps_st, el_st = run(1, seconds / 2)
+    # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
+    ns_group = lib.qo_time_single_group_ns(k, L, 200000)
     return {
         "value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"oracle encode+recover of {n} groups x {k} x {L} B, {reps_mt} passes "
-                  f"(~{seconds / 2:.0f} s) on {threads} threads",
+        "sample": f"oracle encode+recover of the bench workload itself ({G} groups x {k} x {L} B,"
+                  f" {bytes_per_pass / 1e9:.1f} GB per pass): {reps_mt} passes in {el_mt:.1f} s on "
+                  f"{threads} threads; {reps_st} passes in {el_st:.1f} s on 1 core",
         "single_core_value": round(st, 3),
         "configs0_ns_per_group_1core": round(ns_group, 1),
-        "cpu_model": cpu_model, "nproc": os.cpu_count(),
+        "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
     }
 
 
@@ -142,6 +161,13 @@ class HipFixedWorkload:
         if ev:
             ev[2].record(self.stream)
 
+    def poison(self):
+        """Overwrite the outputs (untimed) so verify() can only pass on what the
+        timed steps wrote."""
+        self.par.fill_(0xA5)
+        self.out.fill_(0x5A)
+        self.synchronize()
+
     def synchronize(self):
         self.ctx.sync()
         self.torch.cuda.synchronize()
@@ -152,7 +178,8 @@ class HipFixedWorkload:
         return float(enc), float(rec)
 
     def verify(self):
-        """Round trip on every group + parity XOR all rows == 0 (device, untimed).
+        """On the LAST timed step's outputs (device, untimed): the revived row of
+        every group equals the lost row, and parity XOR all k rows == 0.
         Bit-exactness against the oracle is tests/test_hip_fixed.py's job."""
         torch, G, k, L = self.torch, self.G, self.k, self.L
         r3 = self.rows.view(G, k, L)
@@ -163,17 +190,84 @@ class HipFixedWorkload:
             acc ^= r3[:, i]
         return bool(ok) and not bool(acc.any())
 
+    def digests(self):
+        import hashlib
+        return [hashlib.sha256(self.par.cpu().numpy().tobytes()).hexdigest()[:32],
+                hashlib.sha256(self.out.cpu().numpy().tobytes()).hexdigest()[:32]]
+
+    def host_rows(self):
+        return self.rows.cpu().numpy()
+
     def release(self):
         del self.rows
         self.torch.cuda.empty_cache()
 
 
+class CpuStandInWorkload:
+    """`--cpu-workload` (tests only): the same shard, step and verification
+    structure as HipFixedWorkload with a numpy XOR in place of the kernels, so
+    the rank launch, shard assignment, timing contract and JSON line run on a
+    CPU box under gloo.  Never the measured path (the line says so)."""
+
+    def __init__(self, g0, G, k, L):
+        from libquic_amd import synth
+        self.g0, self.G, self.k, self.L = g0, G, k, L
+        self.rows = synth.synth_fixed_host(SEED_FIXED, g0, G, k, L)
+        self.miss = drop_indices(g0, G, k)
+        self.par = np.zeros(G * L, np.uint8)
+        self.out = np.zeros(G * L, np.uint8)
+        self.bytes_encode = G * (k * L + L)
+        self.bytes_recover = G * ((k - 1) * L + 2 * L)
+        self.steps = 0
+
+    def new_events(self):
+        return None
+
+    def step(self, ev=None):
+        r3 = self.rows.reshape(self.G, self.k, self.L)
+        par = np.bitwise_xor.reduce(r3, axis=1)
+        self.par[:] = par.reshape(-1)
+        keep = r3.copy()
+        keep[np.arange(self.G), self.miss] = 0
+        self.out[:] = (np.bitwise_xor.reduce(keep, axis=1) ^ par).reshape(-1)
+        self.steps += 1
+
+    def poison(self):
+        self.par[:] = 0xA5
+        self.out[:] = 0x5A
+
+    def synchronize(self):
+        pass
+
+    def kernel_seconds(self, events):
+        return None, None
+
+    def verify(self):
+        r3 = self.rows.reshape(self.G, self.k, self.L)
+        return bool(np.array_equal(self.out.reshape(self.G, self.L),
+                                   r3[np.arange(self.G), self.miss]))
+
+    def digests(self):
+        import hashlib
+        return [hashlib.sha256(self.par.tobytes()).hexdigest()[:32],
+                hashlib.sha256(self.out.tobytes()).hexdigest()[:32]]
+
+    def host_rows(self):
+        return self.rows
+
+    def release(self):
+        pass
+
+
 def timed_steps(work, steps, warmup, barrier, reduce_max):
     """The measurement contract: W untimed steps, then exactly K steps bracketed
-    by barrier + synchronize on both sides; elapsed = max over ranks."""
+    by barrier + synchronize on both sides; elapsed = max over ranks.  The
+    outputs are poisoned before the timed steps, so the verification that
+    follows checks what the timed steps wrote."""
     for _ in range(warmup):
         work.step()
     work.synchronize()
+    work.poison()
     events = [work.new_events() for _ in range(steps)]
     barrier()
     work.synchronize()
@@ -188,7 +282,8 @@ def timed_steps(work, steps, warmup, barrier, reduce_max):
 
 def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_recover,
                 enc_s=None, rec_s=None, traffic=None, verified=None):
-    """The JSON line (rank 0).  value = algorithmic bytes of ALL ranks / max time."""
+    """The JSON line (rank 0).  value = algorithmic bytes of ALL ranks / max time.
+    enc_s / rec_s: the slowest rank's mean encode / recover launch (seconds)."""
     total = world * steps * (bytes_encode + bytes_recover)
     line = {
         "metric": "FEC XOR encode+recover GiB/s (device-resident) on batched 1350B packet groups",
@@ -242,21 +337,83 @@ def measured_traffic(G, k, L):
     return None
 
 
-def main():
-    args = parse()
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of
+    this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set), one per GPU,
+    and return the worst exit code.  This parent process never imports torch
+    and never touches a GPU; rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:  # a dead rank leaves the others in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            return launch_ranks(args.gpus, argv)
+        world = 1
+    else:
+        world = int(env_world)
+        if world != args.gpus:
+            print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+            return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.groups < 1 or not 1 <= args.k <= 255 or not 1 <= args.L <= 1452 or args.steps < 1:
+        print(f"bench.py[rank {rank}]: invalid workload groups={args.groups} k={args.k} "
+              f"L={args.L} steps={args.steps}", file=sys.stderr)
+        return 2
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = args.cpu_workload
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif not cpu:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = None if cpu else torch.device("cuda", torch.cuda.current_device())
 
     def barrier():
         if world > 1:
@@ -269,22 +426,52 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
     k, L, G = args.k, args.L, args.groups
-    work = HipFixedWorkload(torch, dev, rank * G, G, k, L, cached=args.cached)
-    work.step()
-    work.synchronize()
-    verified = None if args.no_verify else work.verify()
+    g0 = rank * G  # contiguous group shard per rank: no collective on the data path
+    if cpu:
+        work = CpuStandInWorkload(g0, G, k, L)
+    else:
+        work = HipFixedWorkload(torch, dev, g0, G, k, L, cached=args.cached)
     elapsed, events = timed_steps(work, args.steps, args.warmup, barrier, reduce_max)
     enc_s, rec_s = work.kernel_seconds(events)
+    verified = None if args.no_verify else work.verify()
+    per_rank = gather({"rank": rank, "g0": g0, "groups": G, "enc_s": enc_s, "rec_s": rec_s,
+                       "verified": verified, "digests": work.digests() if cpu else None})
+    if enc_s:  # the roofline of the slowest rank's encode launch
+        enc_s = max(r["enc_s"] for r in per_rank)
+        rec_s = max(r["rec_s"] for r in per_rank)
+    if verified is not None:
+        verified = all(r["verified"] for r in per_rank)
     line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
                        work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified)
+    if world > 1 and line["roofline"]:
+        fr = [work.bytes_encode / r["enc_s"] / 1e9 / HBM_PEAK_GBS for r in per_rank]
+        line["roofline"]["per_rank_frac"] = {"min": round(min(fr), 4), "max": round(max(fr), 4)}
+    if cpu:
+        line["data"] = "synthetic; --cpu-workload numpy stand-in (test of the rank path, not a measurement)"
+        line["dtype"] = "u8"
+        line["shards"] = [{"rank": r["rank"], "g0": r["g0"], "groups": r["groups"],
+                           "digests": r["digests"]} for r in per_rank]
 
-    if not args.profile_only and rank == 0 and world == 1 and not args.no_ceilings:
+    extras = rank == 0 and world == 1 and not cpu and not args.profile_only
+    if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
         if line["roofline"]:  # the encode kernel against this box's measured streaming read
             line["ceilings"]["encode_frac_of_read_ceiling"] = round(
                 line["roofline"]["achieved"] / line["ceilings"]["read_GBps"], 4)
-    if not args.profile_only and rank == 0 and world == 1:
+    # The CPU baseline: rank 0 only, after every rank's timed region (the other
+    # ranks wait at the final barrier), over rank 0's shard of the same workload.
+    host_rows = None
+    if rank == 0 and not args.no_cpu_baseline and not args.profile_only:
+        host_rows = work.host_rows()
+    if extras:
         work.release()
         ctx, stream = work.ctx, work.stream
         if not args.no_ragged:
@@ -297,14 +484,24 @@ def main():
                                             cpu=not args.no_cpu_baseline)
         if not args.no_e2e:
             line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(k, L, args.cpu_seconds)
+        if not args.no_fused:
+            line["e2e_fec_gcm"] = bench_fused(ctx, torch, dev, stream, k, L,
+                                              cpu=not args.no_cpu_baseline)
+        if not args.no_connection:
+            line["connection"] = bench_connection(cpu=not args.no_cpu_baseline)
+    if host_rows is not None:
+        line["cpu_baseline"] = cpu_baseline(host_rows, G, k, L, args.cpu_seconds,
+                                            args.cpu_threads)
+        del host_rows
     line.setdefault("cpu_baseline", None)
+    barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    work.ctx.close()
+    if not cpu:
+        work.ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
@@ -337,19 +534,11 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
         if ev:
             ev[2].record(stream)
 
-    run()
+    run()  # warm
     ctx.sync()
-    # verify: parity lengths and the round trip of a sample of groups
-    ok = np.array_equal(plen.cpu().numpy().view(np.uint16), plen_max)
-    out_h = out.cpu().numpy()
-    data_h = None
-    for g in np.random.default_rng(0).choice(G, 256, replace=False):
-        p = int(ptr[g]) + int(miss[g])
-        o, l_ = int(off[p]), int(ln[p])
-        if data_h is None:
-            data_h = data.cpu().numpy()
-        seg = out_h[g * 1452: g * 1452 + int(plen_max[g])]
-        ok = ok and np.array_equal(seg[:l_], data_h[o:o + l_]) and not seg[l_:].any()
+    par.fill_(0xA5)  # poison: the check below sees only what the timed steps wrote
+    out.fill_(0x5A)
+    plen.fill_(0)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     torch.cuda.synchronize()
     for s in range(steps):
@@ -357,6 +546,22 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
     torch.cuda.synchronize()
     enc = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
     rec = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
+    # verify the last timed step: parity lengths, the revived packet of a
+    # sample of groups (zero tail to parity_len), parity XOR rows == 0 there
+    ok = np.array_equal(plen.cpu().numpy().view(np.uint16), plen_max)
+    out_h = out.cpu().numpy()
+    par_h = par.cpu().numpy()
+    data_h = data.cpu().numpy()
+    for g in np.random.default_rng(0).choice(G, 256, replace=False):
+        p = int(ptr[g]) + int(miss[g])
+        o, l_ = int(off[p]), int(ln[p])
+        pl = int(plen_max[g])
+        seg = out_h[g * 1452: g * 1452 + pl]
+        ok = ok and np.array_equal(seg[:l_], data_h[o:o + l_]) and not seg[l_:].any()
+        acc = par_h[g * 1452: g * 1452 + pl].copy()
+        for q in range(int(ptr[g]), int(ptr[g + 1])):
+            acc[:int(ln[q])] ^= data_h[int(off[q]):int(off[q]) + int(ln[q])]
+        ok = ok and not acc.any()
     lens_sum = float(ln.astype(np.float64).sum())
     pl_sum = float(plen_max.astype(np.float64).sum())
     miss_len = float(ln[ptr[:-1].astype(np.int64) + miss.astype(np.int64)].astype(np.float64).sum())
@@ -711,4 +916,4 @@ def bench_e2e(ctx, torch, k, L, G=1 << 18):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -427,13 +427,48 @@ int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity
 // ---- ragged ---------------------------------------------------------------
 namespace {
 
-// Host-pointer ragged path: stage the whole batch through one device
-// allocation (ragged batches in the host path are bounded by the caller's
-// batch; the device-pointer path is the throughput path).
-struct DevBuf {
+// Host-pointer ragged path (QuicFecGroup::PayloadParity/Revive and the
+// connection batches' Flush run through it).  Chunks of whole groups are
+// GATHERED on the host into one slot's pinned staging buffer — received
+// packets packed back to back, then the chunk's CSR tables rebased to the
+// staging layout — moved by ONE H2D, XORed by one ragged launch, and the
+// packed outputs come back by one D2H and are scattered to the caller's
+// offsets.  Chunks rotate over the context's kSlots streams, so the host
+// gathers chunk c+1 while chunk c is on the device.  Nothing is allocated per
+// call: the slots' device and pinned buffers (ensure_staging) are reused.
+// Only exactly what the device path writes is written: parity_len[g] bytes
+// per group (+ parity_len_out on encode).
+struct DevBuf {  // scoped device allocation (the protection / entropy host paths)
   void* p = nullptr;
   ~DevBuf() {
     if (p) (void)hipFree(p);
+  }
+};
+
+struct RaggedChunk {
+  uint64_t g0 = 0, n = 0;
+  uint64_t np = 0, nbytes = 0, nout = 0, npar = 0;  // staged packets, bytes, output, parity bytes
+  bool live = false;
+};
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct RaggedLayout {  // byte offsets inside a slot's d_in / h_in (and d_out / h_out)
+  uint64_t bytes, off, len, ptr, poff, par, plen, miss, ooff, in_total;
+  uint64_t out_plen, out_total;
+  RaggedLayout(const RaggedChunk& c, bool recover) {
+    bytes = 0;
+    off = align_up(c.nbytes, 16);
+    len = off + c.np * 8;
+    ptr = align_up(len + c.np * 2, 8);
+    poff = align_up(ptr + (c.n + 1) * 4, 8);
+    par = align_up(poff + c.n * 8, 16);
+    plen = align_up(par + (recover ? c.npar : 0), 8);
+    miss = plen + (recover ? c.n * 2 : 0);
+    ooff = align_up(miss + (recover ? c.n : 0), 8);
+    in_total = ooff + (recover ? c.n * 8 : 0);
+    out_plen = align_up(c.nout, 8);
+    out_total = out_plen + (recover ? 0 : c.n * 2);
   }
 };
 
@@ -442,102 +477,154 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
                 const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
                 const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
                 uint8_t* out, const uint64_t* out_off) {
-  const uint32_t np = grp_ptr[n] - grp_ptr[0];
-  const uint32_t pb = grp_ptr[0];
-  // byte span of the packets and of the output region
-  uint64_t lo = UINT64_MAX, hi = 0;
+  int rc = ensure_staging(ctx);
+  if (rc) return rc;
+  // Host-side validation of what the staging depends on (the same error
+  // words the kernel latches; the kernel re-checks everything else).
+  uint32_t bits = 0;
   for (uint64_t g = 0; g < n; ++g) {
-    if (grp_ptr[g + 1] < grp_ptr[g])
-      return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "grp_ptr not monotone at group %llu",
-                  (unsigned long long)g);
+    if (grp_ptr[g + 1] < grp_ptr[g] || grp_ptr[g + 1] - grp_ptr[g] > QFEC_MAX_GROUP_PACKETS ||
+        grp_ptr[g + 1] == grp_ptr[g]) {
+      bits |= qfec::kErrGroupSize;
+      continue;
+    }
+    if (recover) {
+      if (missing[g] >= grp_ptr[g + 1] - grp_ptr[g]) bits |= qfec::kErrMissingIndex;
+      if (parity_len[g] == 0 || parity_len[g] > QFEC_MAX_PACKET_SIZE) bits |= qfec::kErrParityLength;
+    }
     for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) {
       if (recover && p - grp_ptr[g] == missing[g]) continue;
-      lo = std::min(lo, pkt_off[p]);
-      hi = std::max(hi, pkt_off[p] + pkt_len[p]);
+      if (pkt_len[p] == 0 || pkt_len[p] > QFEC_MAX_PACKET_SIZE ||
+          (recover && pkt_len[p] > parity_len[g]))
+        bits |= qfec::kErrPacketLength;
     }
   }
-  if (lo == UINT64_MAX) lo = hi = 0;
-  uint64_t olo = UINT64_MAX, ohi = 0, plo = UINT64_MAX, phi = 0;
-  for (uint64_t g = 0; g < n; ++g) {
-    const uint64_t o = recover ? out_off[g] : parity_off[g];
-    olo = std::min(olo, o);
-    ohi = std::max(ohi, o + QFEC_MAX_PACKET_SIZE);
-    if (recover) {
-      plo = std::min(plo, parity_off[g]);
-      phi = std::max(phi, parity_off[g] + parity_len[g]);
+  if (bits) return latch_error(ctx, bits);
+
+  const uint64_t in_cap = kStageBytes, out_cap = kStageBytes / 4;
+  RaggedChunk chunk[kSlots];
+
+  auto finish = [&](int si) -> int {
+    RaggedChunk& c = chunk[si];
+    if (!c.live) return QFEC_OK;
+    Slot& s = ctx->slots[si];
+    QFEC_HIP(ctx, hipEventSynchronize(s.done));
+    const RaggedLayout lay(c, recover);
+    const uint16_t* h_plen = reinterpret_cast<const uint16_t*>(s.h_out + lay.out_plen);
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < c.n; ++i) {
+      const uint64_t g = c.g0 + i;
+      if (recover) {
+        std::memcpy(out + out_off[g], s.h_out + o, parity_len[g]);
+        o += parity_len[g];
+      } else {
+        std::memcpy(parity_out + parity_off[g], s.h_out + o, h_plen[i]);
+        parity_len_out[g] = h_plen[i];
+        uint16_t mx = 0;
+        for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) mx = std::max(mx, pkt_len[p]);
+        o += mx;
+      }
     }
-  }
-  // The output span may not be fully written (gaps between groups): seed the
-  // device copy with the caller's bytes so the D2H leaves gaps unchanged.  The
-  // upper bound is clipped to the last byte any group can write.
-  uint64_t owrite_hi = 0;
-  for (uint64_t g = 0; g < n; ++g) {
-    uint32_t mx = 0;
+    c.live = false;
+    return QFEC_OK;
+  };
+
+  int slot = 0;
+  uint64_t g = 0;
+  while (g < n) {
+    // plan the chunk: whole groups while both staging budgets hold
+    RaggedChunk c;
+    c.g0 = g;
+    for (; g < n; ++g) {
+      const uint32_t k = grp_ptr[g + 1] - grp_ptr[g];
+      uint64_t gb = 0, mx = 0;
+      for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) {
+        if (recover && p - grp_ptr[g] == missing[g]) continue;
+        gb += pkt_len[p];
+        mx = std::max<uint64_t>(mx, pkt_len[p]);
+      }
+      const uint64_t gout = recover ? parity_len[g] : mx;
+      RaggedChunk t = c;
+      t.n += 1;
+      t.np += k;
+      t.nbytes += gb;
+      t.nout += gout;
+      t.npar += recover ? parity_len[g] : 0;
+      const RaggedLayout lay(t, recover);
+      if (c.n > 0 && (lay.in_total > in_cap || lay.out_total > out_cap)) break;
+      c = t;
+    }
+    if ((rc = finish(slot))) return rc;
+    Slot& s = ctx->slots[slot];
+    const RaggedLayout lay(c, recover);
+    uint8_t* h = s.h_in;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(h + lay.off);
+    uint16_t* h_len = reinterpret_cast<uint16_t*>(h + lay.len);
+    uint32_t* h_ptr = reinterpret_cast<uint32_t*>(h + lay.ptr);
+    uint64_t* h_poff = reinterpret_cast<uint64_t*>(h + lay.poff);
+    uint16_t* h_plen = reinterpret_cast<uint16_t*>(h + lay.plen);
+    uint64_t* h_ooff = reinterpret_cast<uint64_t*>(h + lay.ooff);
+    uint64_t b = 0, pb = 0, ob = 0;
+    uint32_t q = 0;
+    for (uint64_t i = 0; i < c.n; ++i) {
+      const uint64_t gg = c.g0 + i;
+      h_ptr[i] = q;
+      uint16_t mx = 0;
+      for (uint32_t p = grp_ptr[gg]; p < grp_ptr[gg + 1]; ++p, ++q) {
+        h_len[q] = pkt_len[p];
+        if (recover && p - grp_ptr[gg] == missing[gg]) {
+          h_off[q] = 0;  // the lost packet's entry is never read
+          continue;
+        }
+        std::memcpy(h + b, bytes + pkt_off[p], pkt_len[p]);
+        h_off[q] = b;
+        b += pkt_len[p];
+        mx = std::max(mx, pkt_len[p]);
+      }
+      if (recover) {
+        std::memcpy(h + lay.par + pb, parity + parity_off[gg], parity_len[gg]);
+        h_poff[i] = lay.par + pb;
+        pb += parity_len[gg];
+        h_plen[i] = parity_len[gg];
+        h[lay.miss + i] = missing[gg];
+        h_ooff[i] = ob;
+        ob += parity_len[gg];
+      } else {
+        h_poff[i] = ob;
+        ob += mx;
+      }
+    }
+    h_ptr[c.n] = q;
+    QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, s.h_in, lay.in_total, hipMemcpyHostToDevice, s.stream));
+    qfec::RaggedArgs a{};
+    a.bytes = s.d_in;
+    a.pkt_off = reinterpret_cast<const uint64_t*>(s.d_in + lay.off);
+    a.pkt_len = reinterpret_cast<const uint16_t*>(s.d_in + lay.len);
+    a.grp_ptr = reinterpret_cast<const uint32_t*>(s.d_in + lay.ptr);
+    a.n_groups = c.n;
+    a.err = ctx->d_err;
+    a.out = s.d_out;
     if (recover) {
-      mx = parity_len[g];
+      a.parity = s.d_in;  // parity_off is relative to the staging base
+      a.parity_off = reinterpret_cast<const uint64_t*>(s.d_in + lay.poff);
+      a.parity_len = reinterpret_cast<const uint16_t*>(s.d_in + lay.plen);
+      a.missing = s.d_in + lay.miss;
+      a.out_off = reinterpret_cast<const uint64_t*>(s.d_in + lay.ooff);
     } else {
-      for (uint32_t p = grp_ptr[g]; p < grp_ptr[g + 1]; ++p) mx = std::max<uint32_t>(mx, pkt_len[p]);
+      a.parity_off = reinterpret_cast<const uint64_t*>(s.d_in + lay.poff);
+      a.parity_len_out = reinterpret_cast<uint16_t*>(s.d_out + lay.out_plen);
     }
-    owrite_hi = std::max(owrite_hi, (recover ? out_off[g] : parity_off[g]) + mx);
+    QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+    QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, lay.out_total, hipMemcpyDeviceToHost,
+                                 s.stream));
+    QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    c.live = true;
+    chunk[slot] = c;
+    slot = (slot + 1) % kSlots;
   }
-  ohi = std::min(ohi, owrite_hi);
-  if (olo > ohi) olo = ohi;
-  DevBuf d_bytes, d_off, d_len, d_ptr, d_par, d_poff, d_plen, d_miss, d_out, d_ooff;
-  std::vector<uint32_t> ptr(grp_ptr, grp_ptr + n + 1);
-  for (auto& v : ptr) v -= pb;
-  std::vector<uint64_t> off(pkt_off + pb, pkt_off + pb + np);
-  for (auto& v : off) v -= (v >= lo ? lo : v);  // the lost packet's entry is never read
-  std::vector<uint64_t> ooff(n);
-  for (uint64_t g = 0; g < n; ++g) ooff[g] = (recover ? out_off[g] : parity_off[g]) - olo;
-  hipStream_t st = ctx->stream;
-  QFEC_HIP(ctx, hipMalloc(&d_bytes.p, std::max<uint64_t>(hi - lo, 1)));
-  QFEC_HIP(ctx, hipMalloc(&d_off.p, std::max<size_t>(np, 1) * 8));
-  QFEC_HIP(ctx, hipMalloc(&d_len.p, std::max<size_t>(np, 1) * 2));
-  QFEC_HIP(ctx, hipMalloc(&d_ptr.p, (n + 1) * 4));
-  QFEC_HIP(ctx, hipMalloc(&d_out.p, std::max<uint64_t>(ohi - olo, 1)));
-  QFEC_HIP(ctx, hipMalloc(&d_ooff.p, n * 8));
-  QFEC_HIP(ctx, hipMalloc(&d_plen.p, n * 2));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_bytes.p, bytes + lo, hi - lo, hipMemcpyHostToDevice, st));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_off.p, off.data(), np * 8, hipMemcpyHostToDevice, st));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_len.p, pkt_len + pb, np * 2, hipMemcpyHostToDevice, st));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_ptr.p, ptr.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, (recover ? out : parity_out) + olo, ohi - olo,
-                               hipMemcpyHostToDevice, st));
-  QFEC_HIP(ctx, hipMemcpyAsync(d_ooff.p, ooff.data(), n * 8, hipMemcpyHostToDevice, st));
-  qfec::RaggedArgs a{};
-  a.bytes = static_cast<const uint8_t*>(d_bytes.p);
-  a.pkt_off = static_cast<const uint64_t*>(d_off.p);
-  a.pkt_len = static_cast<const uint16_t*>(d_len.p);
-  a.grp_ptr = static_cast<const uint32_t*>(d_ptr.p);
-  a.n_groups = n;
-  a.err = ctx->d_err;
-  a.out = static_cast<uint8_t*>(d_out.p);
-  std::vector<uint64_t> poff;
-  if (recover) {
-    poff.resize(n);
-    for (uint64_t g = 0; g < n; ++g) poff[g] = parity_off[g] - plo;
-    QFEC_HIP(ctx, hipMalloc(&d_par.p, std::max<uint64_t>(phi - plo, 1)));
-    QFEC_HIP(ctx, hipMalloc(&d_poff.p, n * 8));
-    QFEC_HIP(ctx, hipMalloc(&d_miss.p, n));
-    QFEC_HIP(ctx, hipMemcpyAsync(d_par.p, parity + plo, phi - plo, hipMemcpyHostToDevice, st));
-    QFEC_HIP(ctx, hipMemcpyAsync(d_poff.p, poff.data(), n * 8, hipMemcpyHostToDevice, st));
-    QFEC_HIP(ctx, hipMemcpyAsync(d_miss.p, missing, n, hipMemcpyHostToDevice, st));
-    QFEC_HIP(ctx, hipMemcpyAsync(d_plen.p, parity_len, n * 2, hipMemcpyHostToDevice, st));
-    a.parity = static_cast<const uint8_t*>(d_par.p);
-    a.parity_off = static_cast<const uint64_t*>(d_poff.p);
-    a.parity_len = static_cast<const uint16_t*>(d_plen.p);
-    a.missing = static_cast<const uint8_t*>(d_miss.p);
-    a.out_off = static_cast<const uint64_t*>(d_ooff.p);
-  } else {
-    a.parity_off = static_cast<const uint64_t*>(d_ooff.p);
-    a.parity_len_out = static_cast<uint16_t*>(d_plen.p);
-  }
-  QFEC_HIP(ctx, qfec::launch_ragged(a, recover, st));
-  QFEC_HIP(ctx, hipMemcpyAsync((recover ? out : parity_out) + olo, d_out.p, ohi - olo,
-                               hipMemcpyDeviceToHost, st));
-  if (!recover)
-    QFEC_HIP(ctx, hipMemcpyAsync(parity_len_out, d_plen.p, n * 2, hipMemcpyDeviceToHost, st));
-  return collect_error(ctx, st);
+  for (int i = 0; i < kSlots; ++i)
+    if ((rc = finish((slot + i) % kSlots))) return rc;
+  return collect_error(ctx, ctx->slots[0].stream);
 }
 
 }  // namespace

@@ -33,8 +33,11 @@ bool QuicFecSender::OnDataPacket(QuicPacketNumber packet_number, StringPiece pay
   if (fec_protect_) {
     if (!group_) group_.reset(new QuicFecGroup(packet_number));
     const QuicPacketNumber offset = packet_number - group_->FecGroupNumber();
-    if (offset > 0xFF) {  // uint8 first_fec_protected_packet_offset
-      detailed_error_ = "packet beyond the FEC group's uint8 offset range";
+    // uint8 first_fec_protected_packet_offset: the FEC packet needs an offset
+    // above every data packet's, so data packets stop at offset 254.
+    if (offset >= 0xFF) {
+      detailed_error_ = "data packet at FEC group offset " + std::to_string(offset) +
+                        ": no room left for the FEC packet (close the group first)";
       return false;
     }
     QuicPacketHeader h;

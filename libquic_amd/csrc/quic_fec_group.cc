@@ -35,13 +35,20 @@ QuicFecGroup::~QuicFecGroup() = default;
 
 qfec_ctx* QuicFecGroup::context() const { return ctx_ ? ctx_ : thread_default_ctx(); }
 
-bool QuicFecGroup::Fold(StringPiece payload) {
+bool QuicFecGroup::Fold(StringPiece payload, bool completes_group) {
   if (payload.size() > kMaxPacketSize) {
     detailed_error_ = "Illegal payload size: " + std::to_string(payload.size());
     return false;
   }
   if (payload.empty()) return true;  // XOR of nothing
   if (lens_.size() >= QFEC_MAX_GROUP_PACKETS) {
+    // A group spans 256 packet numbers (uint8 offset 0..255): 255 data
+    // packets + the FEC packet.  The 256th payload can only arrive when it
+    // completes the group, which then has nothing to revive; it is not kept.
+    if (completes_group) {
+      unkept_payload_ = true;
+      return true;
+    }
     detailed_error_ = "FEC group holds more than 255 payloads";
     return false;
   }
@@ -62,7 +69,10 @@ bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHead
                       std::to_string(header.packet_number);
     return false;
   }
-  if (!Fold(decrypted_payload)) return false;
+  const bool completes = min_protected_packet_ != kInvalidPacketNumber &&
+                         received_packets_.size() + 1 ==
+                             max_protected_packet_ - min_protected_packet_ + 1;
+  if (!Fold(decrypted_payload, completes)) return false;
   received_packets_.insert(header.packet_number);
   if (encryption_level < effective_encryption_level_)
     effective_encryption_level_ = encryption_level;
@@ -84,7 +94,8 @@ bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketH
       return false;
     }
   }
-  if (!Fold(redundancy)) return false;
+  const bool completes = received_packets_.size() == fec_packet_number - fec_group_number_;
+  if (!Fold(redundancy, completes)) return false;
   min_protected_packet_ = fec_group_number_;
   max_protected_packet_ = fec_packet_number - 1;
   if (encryption_level < effective_encryption_level_)
@@ -117,6 +128,10 @@ int QuicFecGroup::EnsureParity() const {
 }
 
 StringPiece QuicFecGroup::PayloadParity() const {
+  if (unkept_payload_) {
+    detailed_error_ = "finished group of 256 payloads: its accumulator was not kept";
+    return StringPiece();
+  }
   if (EnsureParity() != QFEC_OK) return StringPiece();
   return StringPiece(reinterpret_cast<const char*>(parity_.data()), payload_parity_len_);
 }

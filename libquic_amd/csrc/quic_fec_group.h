@@ -33,12 +33,26 @@
 
 #include "../../include/qfec.h"
 
+#ifdef QFEC_WITH_LIBQUIC
+// Built inside libquic, with integration/libquic_fec.patch applied: the
+// reference's own types.  The patch restores the v<=31 group fields of
+// QuicPacketHeader (is_in_fec_group, fec_group) and the QuicFecGroupNumber /
+// InFecGroup declarations in quic_protocol.h.
+#include "base/strings/string_piece.h"
+#include "net/quic/core/quic_bandwidth.h"
+#include "net/quic/core/quic_protocol.h"
+
+namespace net {
+using base::StringPiece;
+#else
 namespace net {
 
-// quic_protocol.h mirrors (the reference's own types, same values).
+// Standalone build (no libquic headers): mirrors of the reference's types in
+// quic_protocol.h, same names and values.  Never compiled together with the
+// reference headers — a libquic build defines QFEC_WITH_LIBQUIC instead.
 typedef uint64_t QuicPacketNumber;                 // quic_protocol.h:44
 typedef QuicPacketNumber QuicFecGroupNumber;       // historical v<=31 header field
-typedef uint64_t QuicPacketCount;
+typedef uint64_t QuicPacketCount;                  // quic_bandwidth.h:21
 const QuicPacketNumber kInvalidPacketNumber = 0;   // quic_protocol.h:752-753
 const size_t kMaxPacketSize = QFEC_MAX_PACKET_SIZE;  // quic_protocol.h:66
 
@@ -73,6 +87,7 @@ struct StringPiece {
   size_t size() const { return len; }
   bool empty() const { return len == 0; }
 };
+#endif  // QFEC_WITH_LIBQUIC
 
 class QuicFecGroup {
  public:
@@ -116,7 +131,7 @@ class QuicFecGroup {
   const std::string& detailed_error() const { return detailed_error_; }
 
  private:
-  bool Fold(StringPiece payload);
+  bool Fold(StringPiece payload, bool completes_group);
   int EnsureParity() const;
   QuicPacketCount NumMissingPackets() const;
   qfec_ctx* context() const;
@@ -134,6 +149,7 @@ class QuicFecGroup {
   mutable std::vector<uint8_t> parity_;
   mutable size_t payload_parity_len_ = 0;
   mutable bool dirty_ = false;
+  bool unkept_payload_ = false;  // a 256th payload completed the group (Fold)
   mutable std::string detailed_error_;
 };
 

@@ -17,9 +17,15 @@
 #include <vector>
 
 #include "quic_fec_group.h"
+#ifdef QFEC_WITH_LIBQUIC
+#include "net/quic/core/quic_framer.h"
+#endif
 
 namespace net {
 
+#ifndef QFEC_WITH_LIBQUIC
+// Standalone build: the reference's values (a libquic build takes them from
+// quic_protocol.h / quic_framer.h).
 enum QuicPacketPrivateFlags : uint8_t {  // quic_protocol.h:343-358
   PACKET_PRIVATE_FLAGS_NONE = 0,
   PACKET_PRIVATE_FLAGS_ENTROPY = 1 << 0,
@@ -29,8 +35,10 @@ enum QuicPacketPrivateFlags : uint8_t {  // quic_protocol.h:343-358
   PACKET_PRIVATE_FLAGS_MAX_VERSION_32 = (1 << 1) - 1,
 };
 
-const int kQuicVersion31 = 31;                 // last version with FEC (quic_protocol.h:371-373)
 const size_t kNumberOfRevivedPacketsSize = 1;  // quic_framer.h:64-65
+#endif
+
+const int kQuicVersion31 = 31;  // last version with FEC (quic_protocol.h:371-373)
 
 struct FecHeaderFields {
   bool entropy_flag = false;

@@ -110,3 +110,19 @@ def entropy_batch(rng, n_conns, max_packets=300, acks_per_conn=3, max_ranges=4,
             "largest": np.array(largest, np.uint64), "claimed": np.array(claimed, np.uint8),
             "range_ptr": np.array(rptr, np.uint32), "range_lo": np.array(lo, np.uint64),
             "range_hi": np.array(hi, np.uint64), "full": full}
+
+
+def synth_fixed_host(seed, g0, n, k, L):
+    """rows[n*k*L] of the counter-based generator on the host (the formula of
+    the device's qfec_synth_fixed: word w of row (g, i) = splitmix64(seed ^
+    (g*256 + i) << 32 ^ w), little-endian).  Plumbing for bench.py's CPU
+    stand-in workload (multi-rank tests without a GPU); small n only."""
+    g = np.arange(g0, g0 + n, dtype=np.uint64)[:, None, None]
+    i = np.arange(k, dtype=np.uint64)[None, :, None]
+    nw = (L + 7) // 8
+    w = np.arange(nw, dtype=np.uint64)[None, None, :]
+    with np.errstate(over="ignore"):
+        key = np.uint64(seed) ^ ((g * np.uint64(256) + i) << np.uint64(32))
+    words = splitmix64(key ^ w)
+    return np.ascontiguousarray(
+        words.astype("<u8").view(np.uint8).reshape(n, k, nw * 8)[:, :, :L]).reshape(-1)

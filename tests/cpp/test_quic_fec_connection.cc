@@ -86,9 +86,12 @@ static void SenderBookkeeping() {
   // a group cannot span more than 255 packet numbers
   QuicFecSender t(255);
   EXPECT(t.OnDataPacket(1, Payload(2, 1, 10), false, &f));
-  EXPECT(t.OnDataPacket(256, Payload(2, 256, 10), false, &f) && f.fec_group_offset == 255);
-  EXPECT(!t.OnDataPacket(257, Payload(2, 257, 10), false, &f));
-  EXPECT(!t.CloseFecGroup(300, &batch));
+  // offset 255 is the FEC packet's: a data packet there would leave the group
+  // unclosable, so it is refused and the group stays usable
+  EXPECT(!t.OnDataPacket(256, Payload(2, 256, 10), false, &f));
+  EXPECT(t.OnDataPacket(255, Payload(2, 255, 10), false, &f) && f.fec_group_offset == 254);
+  EXPECT(!t.CloseFecGroup(257, &batch));  // offset 256: beyond uint8
+  EXPECT(t.CloseFecGroup(256, &batch) && !t.IsFecGroupOpen());
 }
 
 static void ReceiverBookkeeping() {
@@ -150,6 +153,48 @@ struct GroupTruth {
   std::map<QuicPacketNumber, bool> lost;
   bool fec_lost = false;
 };
+
+// A full-width group: 255 data packets (offsets 0..254) + the FEC packet at
+// offset 255 = 256 payloads.  Lossless, the receiver takes every packet and the
+// group finishes (the 256th payload completes it and is not kept); with one
+// loss it folds 255 payloads and can revive.
+static void FullWidthGroup() {
+  QuicFecSender s(1000);  // clamps to 255
+  EXPECT(s.max_packets_per_fec_group() == 255);
+  FecHeaderFields f;
+  for (QuicPacketNumber pn = 1; pn <= 255; ++pn)
+    EXPECT(s.OnDataPacket(pn, Payload(7, pn, 40 + pn % 50), false, &f) &&
+           f.fec_group_offset == pn - 1);
+  EXPECT(s.ShouldSendFec(false));
+  QuicFecEncodeBatch batch;
+  EXPECT(s.CloseFecGroup(256, &batch));
+  for (int lost : {-1, 0, 254}) {
+    QuicFecReceiver r;
+    for (QuicPacketNumber pn = 1; pn <= 255; ++pn) {
+      if ((int)pn - 1 == lost) continue;
+      EXPECT(r.OnPacket(ENCRYPTION_FORWARD_SECURE, DataHeader(pn, 1),
+                        Payload(7, pn, 40 + pn % 50)));
+    }
+    QuicPacketHeader fh = DataHeader(256, 1);
+    fh.fec_flag = true;
+    EXPECT(r.OnPacket(ENCRYPTION_FORWARD_SECURE, fh, std::string(90, 'r')));
+    const QuicFecGroup* g = r.GetGroup(1);
+    if (lost < 0) {
+      EXPECT(g == nullptr || g->IsFinished());  // finished groups leave the map
+    } else {
+      EXPECT(g != nullptr && g->CanRevive());
+    }
+  }
+  // the group object itself: 256 payloads only when the last one completes it
+  QuicFecGroup grp(1);
+  for (QuicPacketNumber pn = 1; pn <= 255; ++pn)
+    EXPECT(grp.Update(ENCRYPTION_NONE, DataHeader(pn, 1), Payload(8, pn, 30)));
+  QuicPacketHeader fh = DataHeader(256, 1);
+  fh.fec_flag = true;
+  EXPECT(grp.UpdateFec(ENCRYPTION_NONE, fh, std::string(30, 'z')));
+  EXPECT(grp.IsFinished() && !grp.CanRevive());
+  EXPECT(grp.PayloadParity().empty() && !grp.detailed_error().empty());
+}
 
 static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double loss,
                        uint64_t seed) {
@@ -300,6 +345,7 @@ int main(int argc, char** argv) {
   const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
   SenderBookkeeping();
   ReceiverBookkeeping();
+  FullWidthGroup();
   if (!cpu_only) {
     qfec_ctx* ctx = qfec_create(0);
     EXPECT(ctx != nullptr);

@@ -1,123 +1,49 @@
-"""CPU multi-rank test of bench.py's N>1 path (gloo, world_size 2).
+"""CPU multi-rank tests of bench.py's N>1 path (gloo, world_size 2).
 
 The FEC groups are independent, so the multi-GPU design is a contiguous group
 shard per rank (g0 = rank * G) with no collective on the data path; the only
-collectives are the timing barrier and the max-over-ranks of the elapsed time.
-This test runs exactly that skeleton (bench.timed_steps / bench.result_line)
-in two gloo processes, with the oracle standing in for the GPU (test
-infrastructure), and checks that the shards tile the global group range and
-reproduce the single-process result group for group.
+collectives are the timing barrier, the max-over-ranks of the elapsed time and
+the gather of per-rank results.  These tests run `python bench.py --gpus 2`
+exactly as a user would, without a launcher: bench.main() starts the ranks
+itself; `--cpu-workload` swaps the kernels for a numpy XOR (gloo backend), and
+each shard's outputs are compared with the oracle (test infrastructure) over
+its group range.
 """
 import json
 import os
-import socket
 import subprocess
 import sys
-import textwrap
 
 import numpy as np
 
 from conftest import ROOT
 
-WORKER = textwrap.dedent(r"""
-    import json, os, sys
-    sys.path.insert(0, os.environ["QFEC_ROOT"])
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    import bench
-    from oracle import oracle_c as OC
-
-    class CpuOracleWorkload:
-        # same shard assignment and step structure as bench.HipFixedWorkload
-        def __init__(self, g0, G, k, L):
-            self.g0, self.G, self.k, self.L = g0, G, k, L
-            self.rows = OC.synth_fixed(bench.SEED_FIXED, g0, G, k, L)
-            self.miss = bench.drop_indices(g0, G, k)
-            self.par = np.zeros(G * L, np.uint8)
-            self.out = np.zeros(G * L, np.uint8)
-            self.bytes_encode = G * (k * L + L)
-            self.bytes_recover = G * ((k - 1) * L + 2 * L)
-            self.steps = 0
-        def new_events(self):
-            return None
-        def step(self, ev=None):
-            lib = OC.lib()
-            assert lib.qo_encode_fixed_mt(OC._p(self.rows), self.k, self.L, self.G,
-                                          OC._p(self.par), 1) == 0
-            assert lib.qo_recover_fixed_mt(OC._p(self.rows), OC._p(self.par), OC._p(self.miss),
-                                           self.k, self.L, self.G, OC._p(self.out), 1) == 0
-            self.steps += 1
-        def synchronize(self):
-            pass
-
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
-    G, k, L = int(os.environ["QFEC_G"]), 10, 1350
-    work = CpuOracleWorkload(rank * G, G, k, L)
-
-    def barrier():
-        dist.barrier()
-
-    def reduce_max(x):
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    local = []
-    def reduce_max_record(x):
-        local.append(x)
-        return reduce_max(x)
-
-    elapsed, _ = bench.timed_steps(work, 3, 1, barrier, reduce_max_record)
-    d = torch.tensor([OC.group_digest(work.par, G, L, L), OC.group_digest(work.out, G, L, L)],
-                     dtype=torch.float64)  # carried as raw bits below
-    digests = [int(OC.group_digest(work.par, G, L, L)), int(OC.group_digest(work.out, G, L, L))]
-    gathered = [None] * world
-    dist.all_gather_object(gathered, {"rank": rank, "g0": work.g0, "G": G, "digests": digests,
-                                      "local_elapsed": local[0], "steps": work.steps})
-    if rank == 0:
-        line = bench.result_line(world, 3, 1, elapsed, G, k, L, work.bytes_encode,
-                                 work.bytes_recover)
-        print("RESULT " + json.dumps({"line": line, "ranks": gathered, "elapsed": elapsed}))
-    dist.destroy_process_group()
-""")
+def _bench_cli(args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=timeout, cwd=ROOT)
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def test_two_rank_gloo_shards():
-    G = 256
-    port = _free_port()
-    procs = []
-    for r in range(2):
-        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2",
-                   RANK=str(r), LOCAL_RANK=str(r), QFEC_ROOT=ROOT, QFEC_G=str(G),
-                   OMP_NUM_THREADS="1")
-        procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
-    outs = []
-    for p in procs:
-        o, e = p.communicate(timeout=300)
-        assert p.returncode == 0, e
-        outs.append(o)
-    res = json.loads([l for l in outs[0].splitlines() if l.startswith("RESULT ")][0][7:])
-    ranks = sorted(res["ranks"], key=lambda r: r["rank"])
-    # shards tile [0, 2G) contiguously, every rank ran warmup + K steps
-    assert [r["g0"] for r in ranks] == [0, G]
-    assert all(r["steps"] == 4 for r in ranks)
-    # elapsed is the max over ranks
-    assert abs(res["elapsed"] - max(r["local_elapsed"] for r in ranks)) < 1e-9
-    # the JSON line aggregates all ranks' bytes over the max time
-    line = res["line"]
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    want = 2 * 3 * G * 14850 * 2 / 2**30 / res["elapsed"]
-    assert abs(line["value"] - round(want, 2)) < 0.02
-    # each shard reproduces the single-process computation of its group range
+def test_bench_cli_spawns_ranks_cpu_workload():
+    """`python bench.py --gpus 2` with no launcher: bench.main() starts the two
+    ranks itself (gloo with --cpu-workload); the line says n_gpus 2 and each
+    shard's outputs equal the single-process oracle result for its range."""
+    G = 64
+    p = _bench_cli(["--gpus", "2", "--cpu-workload", "--groups", str(G), "--steps", "2",
+                    "--warmup", "1", "--no-cpu-baseline"])
+    assert p.returncode == 0, p.stderr
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["warmup"] == 1
+    assert line["verified"] is True
+    assert line["scaling"] == "weak"
+    total = 2 * 2 * G * 14850 * 2
+    assert abs(line["value"] - total / 2**30 / (line["ms_per_step"] * 2 / 1e3)) / line["value"] < 0.01
+    import hashlib
     from oracle import oracle_c as OC
     import bench
     k, L = 10, 1350
@@ -126,10 +52,40 @@ def test_two_rank_gloo_shards():
     miss = bench.drop_indices(0, 2 * G, k)
     rc2, out = OC.recover_fixed(rows, par, miss, k, L, 2 * G)
     assert rc == 0 and rc2 == 0
-    for r in ranks:
-        sl = slice(r["g0"] * L, (r["g0"] + G) * L)
-        assert r["digests"][0] == OC.group_digest(np.ascontiguousarray(par[sl]), G, L, L)
-        assert r["digests"][1] == OC.group_digest(np.ascontiguousarray(out[sl]), G, L, L)
+    shards = sorted(line["shards"], key=lambda s: s["rank"])
+    assert [s["g0"] for s in shards] == [0, G]
+    for s in shards:
+        sl = slice(s["g0"] * L, (s["g0"] + G) * L)
+        assert s["digests"][0] == hashlib.sha256(par[sl].tobytes()).hexdigest()[:32]
+        assert s["digests"][1] == hashlib.sha256(out[sl].tobytes()).hexdigest()[:32]
+
+
+def test_bench_cli_one_rank_matches_two_rank_shard0():
+    G = 32
+    p1 = _bench_cli(["--gpus", "1", "--cpu-workload", "--groups", str(G), "--steps", "1",
+                     "--warmup", "0", "--no-cpu-baseline"])
+    assert p1.returncode == 0, p1.stderr
+    l1 = json.loads([l for l in p1.stdout.splitlines() if l.startswith("{")][0])
+    assert l1["n_gpus"] == 1
+    p2 = _bench_cli(["--gpus", "2", "--cpu-workload", "--groups", str(G), "--steps", "1",
+                     "--warmup", "0", "--no-cpu-baseline"])
+    assert p2.returncode == 0, p2.stderr
+    l2 = json.loads([l for l in p2.stdout.splitlines() if l.startswith("{")][0])
+    s0 = [s for s in l2["shards"] if s["rank"] == 0][0]
+    assert s0["digests"] == l1["shards"][0]["digests"]
+
+
+def test_bench_cli_refuses_world_size_mismatch():
+    p = _bench_cli(["--gpus", "4", "--cpu-workload", "--groups", "8"],
+                   env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 4" in p.stderr
+
+
+def test_bench_cli_failed_rank_fails_the_run():
+    # an invalid shape makes every rank fail: the launcher must return non-zero
+    p = _bench_cli(["--gpus", "2", "--cpu-workload", "--groups", "0", "--steps", "1"])
+    assert p.returncode != 0
 
 
 def test_shard_ranges_disjoint_for_8_ranks():
