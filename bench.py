@@ -337,6 +337,11 @@ def measured_traffic(G, k, L):
     return None
 
 
+def _progress(msg):
+    """One stderr line per leg (a long default run keeps producing output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -474,22 +479,29 @@ def main(argv=None):
     if extras:
         work.release()
         ctx, stream = work.ctx, work.stream
+        _progress("fixed-shape timed steps done")
         if not args.no_ragged:
             line["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
+        _progress("ragged done")
         if not args.no_protect:
             line["protect"] = bench_protect(ctx, torch, dev, stream, G, k, L,
                                             cpu=not args.no_cpu_baseline)
+        _progress("protect done")
         if not args.no_entropy:
             line["entropy"] = bench_entropy(ctx, torch, dev, stream,
                                             cpu=not args.no_cpu_baseline)
+        _progress("entropy done")
         if not args.no_e2e:
             line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
+        _progress("e2e done")
         if not args.no_fused:
             line["e2e_fec_gcm"] = bench_fused(ctx, torch, dev, stream, k, L,
                                               cpu=not args.no_cpu_baseline)
+        _progress("fused e2e done")
         if not args.no_connection:
             line["connection"] = bench_connection(cpu=not args.no_cpu_baseline)
     if host_rows is not None:
+        _progress("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(host_rows, G, k, L, args.cpu_seconds,
                                             args.cpu_threads)
         del host_rows
@@ -882,6 +894,186 @@ def _cpu_entropy_baseline(d, C, n=1 << 16, seconds=3.0):
             "sample": f"oracle over {n} connections x {W} packets + {n} acks, {reps} passes "
                       f"(restatement pinned against the reference's QuicSentEntropyManager; "
                       f"the reference runs it per connection on the connection thread)"}
+
+
+def bench_connection(cpu=True):
+    """Connection layer (QuicFecEncodeBatch / QuicFecReviveBatch::Flush through
+    the host-pointer ragged path): us per Flush and groups/s at 1, 64, 4096,
+    65536 groups of 10 x 1350 B, beside the reference's per-connection CPU
+    accumulate on one core (tests/cpp/bench_connection.cc)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "bench_connection")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} not built"}
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["note"] = ("one Flush = CSR build + gather into pinned staging + H2D + one ragged launch "
+                   "+ D2H + scatter + FEC body / revived copies (wall, median); cpu_1core = the "
+                   "oracle's per-group XorBuffers accumulate (the reference's connection-thread "
+                   "path), one core" + ("" if cpu else "; cpu legs requested off but always run"))
+    return res
+
+
+def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=8192, slots=3, cpu=True):
+    """Host memory in, host memory out, FEC + packet protection on the device
+    with ONE PCIe crossing each way:
+    per chunk of cg groups, H2D of the plaintext payloads + headers, FEC encode
+    (qfec_encode_batch) into the slot, AES-128-GCM-12 seal of every data packet
+    AND every FEC packet (qfec_aes128gcm_seal_batch), D2H of the ciphertexts;
+    chunks rotate over `slots` streams so copies overlap compute.  Rate =
+    plaintext payload bytes / wall time (pinned host buffers)."""
+    from libquic_amd import qfec
+    assert G % cg == 0
+    nchunk = G // cg
+    npk = cg * (k + 1)                      # packets per chunk: data, then FEC
+    rows_b, par_b, hdr_b = cg * k * L, cg * L, npk * hdr
+    host_rows = torch.empty(G * k * L, dtype=torch.uint8).pin_memory()
+    d = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
+    ctx0.synth_fixed(d, k, L, 0, G, SEED_FIXED)
+    ctx0.sync()
+    host_rows.copy_(d)
+    del d
+    torch.cuda.empty_cache()
+    ar = torch.arange(G * (k + 1), dtype=torch.int64)
+    host_hdr = ((ar.view(-1, 1) * 131 + torch.arange(hdr)) & 0xFF).to(torch.uint8).reshape(-1)
+    host_hdr = host_hdr.pin_memory()
+    host_out = torch.empty(G * (k + 1) * (L + 12), dtype=torch.uint8).pin_memory()
+    # per-chunk packet tables (identical for every chunk), device-resident
+    q = torch.arange(npk, dtype=torch.int64, device=dev)
+    in_off = torch.where(q < cg * k, q * L, rows_b + (q - cg * k) * L)
+    ad_off = rows_b + par_b + q * hdr
+    ad_len = torch.full((npk,), hdr, dtype=torch.int16, device=dev)
+    in_len = torch.full((npk,), L, dtype=torch.int16, device=dev)
+    out_off = q * (L + 12)
+    kidx = torch.zeros(npk, dtype=torch.int32, device=dev)
+    grp = torch.where(q < cg * k, q // k, q - cg * k)
+    idx = torch.where(q < cg * k, q % k, torch.full_like(q, k))
+    key = torch.arange(16, dtype=torch.uint8, device=dev) * 11 + 3
+    pre = torch.tensor([0xA0, 0xA1, 0xA2, 0xA3], dtype=torch.uint8, device=dev)
+    pn = [((c * cg + grp) * (k + 1) + idx + 1) for c in range(nchunk)]  # per chunk
+    S = []
+    for s in range(slots):
+        st = torch.cuda.Stream(device=dev)
+        c = qfec.Context(dev.index)
+        c.set_stream(st)
+        S.append({"stream": st, "ctx": c,
+                  "buf": torch.empty(rows_b + par_b + hdr_b, dtype=torch.uint8, device=dev),
+                  "out": torch.empty(npk * (L + 12), dtype=torch.uint8, device=dev)})
+
+    def chunk(c):
+        s = S[c % slots]
+        buf, out = s["buf"], s["out"]
+        with torch.cuda.stream(s["stream"]):
+            buf[:rows_b].copy_(host_rows[c * rows_b:(c + 1) * rows_b], non_blocking=True)
+            buf[rows_b + par_b:].copy_(host_hdr[c * hdr_b:(c + 1) * hdr_b], non_blocking=True)
+            s["ctx"].encode(buf[:rows_b], k, L, cg, buf[rows_b:rows_b + par_b])
+            s["ctx"].aes128gcm_seal(key, pre, kidx, pn[c], None, buf, ad_off, ad_len, in_off,
+                                    in_len, npk, out, out_off)
+            ob = npk * (L + 12)
+            host_out[c * ob:(c + 1) * ob].copy_(out, non_blocking=True)
+
+    for c in range(min(slots, nchunk)):  # warm (contexts, kernels)
+        chunk(c)
+    torch.cuda.synchronize()
+    host_out.fill_(0)
+    reps = 2
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for c in range(nchunk):
+            chunk(c)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    # verify chunk 0 and the last chunk: open on the device, plaintext == rows,
+    # FEC plaintext == XOR of the group's rows
+    ok = True
+    vs = S[0]
+    for c in (0, nchunk - 1):
+        ob = npk * (L + 12)
+        ct = host_out[c * ob:(c + 1) * ob].to(dev)
+        vb = vs["buf"]
+        vb[rows_b + par_b:].copy_(host_hdr[c * hdr_b:(c + 1) * hdr_b])
+        cat = torch.empty(hdr_b + ob, dtype=torch.uint8, device=dev)
+        cat[:hdr_b] = vb[rows_b + par_b:]
+        cat[hdr_b:] = ct
+        pt = torch.empty(npk * L, dtype=torch.uint8, device=dev)
+        okv = torch.zeros(npk, dtype=torch.uint8, device=dev)
+        vs["ctx"].aes128gcm_open(key, pre, kidx, pn[c], None, cat, q * hdr, ad_len,
+                                 hdr_b + q * (L + 12), (in_len + 12).to(torch.int16), npk, pt,
+                                 q * L, okv)
+        vs["ctx"].sync()
+        rows_c = host_rows[c * rows_b:(c + 1) * rows_b].to(dev)
+        par_c = rows_c.view(cg, k, L)[:, 0].clone()
+        for i in range(1, k):
+            par_c ^= rows_c.view(cg, k, L)[:, i]
+        ok = ok and bool(okv.all()) and torch.equal(pt[:rows_b], rows_c) and \
+            torch.equal(pt[rows_b:], par_c.reshape(-1))
+    for s in S:
+        s["ctx"].close()
+    payload = G * k * L
+    res = {"groups": G, "chunk_groups": cg, "slots": slots, "header": hdr,
+           "payload_GiBps": round(payload / wall / 2**30, 2),
+           "wall_ms": round(wall * 1e3, 2),
+           "pcie_h2d_bytes": G * k * L + G * (k + 1) * hdr,
+           "pcie_d2h_bytes": G * (k + 1) * (L + 12),
+           "verified": bool(ok),
+           "note": "pinned host plaintext -> H2D -> FEC encode + AES-128-GCM-12 seal of data and "
+                   "FEC packets -> D2H ciphertext; one PCIe crossing each way, 3 streams"}
+    del host_rows, host_out, host_hdr, S
+    torch.cuda.empty_cache()
+    if cpu:
+        res["cpu_baseline"] = _cpu_fused_baseline(k, L, hdr)
+    return res
+
+
+def _cpu_fused_baseline(k, L, hdr, n=4096, seconds=4.0):
+    """The same work on the host cores: FEC encode (oracle, word-wise XOR) +
+    AES-128-GCM-12 seal of every data and FEC packet (the reference's own
+    BoringSSL aes.c + gcm.c from oracle/_ref when present, else the port)."""
+    from oracle import oracle_c as OC
+    from oracle import ref_quic
+    threads = min(256, os.cpu_count() or 1)
+    npk = n * (k + 1)
+    rows_b, par_b = n * k * L, n * L
+    buf = np.zeros(rows_b + par_b + npk * hdr, np.uint8)
+    buf[:rows_b] = OC.synth_fixed(SEED_FIXED, 0, n, k, L)
+    q = np.arange(npk, dtype=np.uint64)
+    in_off = np.where(q < n * k, q * np.uint64(L), np.uint64(rows_b) + (q - np.uint64(n * k)) * np.uint64(L)).astype(np.uint64)
+    ad_off = np.uint64(rows_b + par_b) + q * np.uint64(hdr)
+    ad_len = np.full(npk, hdr, np.uint16)
+    in_len = np.full(npk, L, np.uint16)
+    out_off = q * np.uint64(L + 12)
+    keys = np.arange(16, dtype=np.uint8)
+    pre = np.arange(4, dtype=np.uint8)
+    kidx = np.zeros(npk, np.uint32)
+    pn = q + np.uint64(1)
+    obuf = np.zeros(npk * (L + 12), np.uint8)
+    kind, what = "port", "oracle FEC + scalar C AES-GCM restatement"
+    seal = OC.quic_aes128gcm_encrypt_batch
+    if ref_quic.available():
+        kind, what = "reference", "oracle FEC + the reference's BoringSSL aes.c + gcm.c (C build)"
+
+        def seal(keys, pre, kidx, pn, path, *rest, threads, out):
+            return ref_quic.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, *rest,
+                                                         threads=threads, out=out)
+    lib = OC.lib()
+
+    def once():
+        assert lib.qo_encode_fixed_mt(OC._p(buf), k, L, n, OC._p(buf[rows_b:]), threads) == 0
+        seal(keys, pre, kidx, pn, None, buf, ad_off, ad_len, in_off, in_len, out_off,
+             npk * (L + 12), threads=threads, out=obuf)
+    once()
+    t0, reps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        once()
+        reps += 1
+    el = time.perf_counter() - t0
+    return {"value": round(reps * n * k * L / el / 2**30, 3), "unit": "GiB/s of payload",
+            "cores": threads, "kind": kind,
+            "sample": f"{n} groups x {k} x {L} B: FEC encode + seal of {npk} packets, {reps} "
+                      f"passes on {threads} threads ({what}; BoringSSL's AES-NI/PCLMUL assembly "
+                      f"is not buildable here and would be faster)"}
 
 
 def bench_e2e(ctx, torch, k, L, G=1 << 18):

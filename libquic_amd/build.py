@@ -74,7 +74,7 @@ def build_lib(force: bool = False, extra_flags=()) -> str:
     return LIB
 
 
-CPP_TESTS = ["test_quic_fec_group", "test_quic_fec_connection"]
+CPP_TESTS = ["test_quic_fec_group", "test_quic_fec_connection", "bench_connection"]
 
 
 def build_cpp_tests(force: bool = False) -> list:

@@ -171,21 +171,16 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
     for (QuicFecGroup* g : work) g->detailed_error_ = qfec_last_error(nullptr);
     return QFEC_ERR_INTERNAL;
   }
-  // Ragged CSR over every folded payload of every group.
-  size_t total = 0, npk = 0;
-  for (QuicFecGroup* g : work) {
-    total += g->bytes_.size();
-    npk += g->lens_.size();
-  }
-  std::vector<uint8_t> bytes;
-  bytes.reserve(total);
-  std::vector<uint64_t> pkt_off;
-  pkt_off.reserve(npk);
-  std::vector<uint16_t> pkt_len;
-  pkt_len.reserve(npk);
-  std::vector<uint32_t> grp_ptr(1, 0);
-  std::vector<uint64_t> parity_off;
+  // Ragged CSR over every folded payload of every group, addressed IN PLACE:
+  // the C-ABI takes one base pointer plus 64-bit offsets, so the base is the
+  // lowest of the groups' payload buffers and each packet's offset is its
+  // distance from it (likewise for the parity accumulators).  The host path
+  // of qfec_encode_ragged gathers straight from the groups into its pinned
+  // staging — no intermediate copy here.
+  size_t npk = 0;
   std::vector<QuicFecGroup*> launched;
+  launched.reserve(work.size());
+  uintptr_t in_base = UINTPTR_MAX, out_base = UINTPTR_MAX;
   for (QuicFecGroup* g : work) {
     if (g->lens_.empty()) {  // only empty payloads folded: parity is empty
       g->payload_parity_len_ = 0;
@@ -193,23 +188,36 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
       g->dirty_ = false;
       continue;
     }
-    uint64_t o = bytes.size();
-    bytes.insert(bytes.end(), g->bytes_.begin(), g->bytes_.end());
+    g->parity_.resize(kMaxPacketSize);
+    in_base = std::min(in_base, reinterpret_cast<uintptr_t>(g->bytes_.data()));
+    out_base = std::min(out_base, reinterpret_cast<uintptr_t>(g->parity_.data()));
+    npk += g->lens_.size();
+    launched.push_back(g);
+  }
+  if (launched.empty()) return QFEC_OK;
+  std::vector<uint64_t> pkt_off;
+  pkt_off.reserve(npk);
+  std::vector<uint16_t> pkt_len;
+  pkt_len.reserve(npk);
+  std::vector<uint32_t> grp_ptr(1, 0);
+  grp_ptr.reserve(launched.size() + 1);
+  std::vector<uint64_t> parity_off;
+  parity_off.reserve(launched.size());
+  for (QuicFecGroup* g : launched) {
+    uint64_t o = reinterpret_cast<uintptr_t>(g->bytes_.data()) - in_base;
     for (uint16_t l : g->lens_) {
       pkt_off.push_back(o);
       pkt_len.push_back(l);
       o += l;
     }
     grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));
-    parity_off.push_back(launched.size() * kMaxPacketSize);
-    launched.push_back(g);
+    parity_off.push_back(reinterpret_cast<uintptr_t>(g->parity_.data()) - out_base);
   }
-  if (launched.empty()) return QFEC_OK;
-  std::vector<uint8_t> parity(launched.size() * kMaxPacketSize, 0);
   std::vector<uint16_t> plen(launched.size(), 0);
-  int rc = qfec_encode_ragged(ctx, bytes.data(), pkt_off.data(), pkt_len.data(), grp_ptr.data(),
-                              launched.size(), parity.data(), parity_off.data(), plen.data(),
-                              QFEC_PTR_HOST);
+  int rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
+                              pkt_len.data(), grp_ptr.data(), launched.size(),
+                              reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
+                              plen.data(), QFEC_PTR_HOST);
   if (rc != QFEC_OK) {
     for (QuicFecGroup* g : launched) g->detailed_error_ = qfec_last_error(ctx);
     return rc;
@@ -217,7 +225,7 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   for (size_t i = 0; i < launched.size(); ++i) {
     QuicFecGroup* g = launched[i];
     g->payload_parity_len_ = plen[i];
-    g->parity_.assign(parity.begin() + parity_off[i], parity.begin() + parity_off[i] + plen[i]);
+    g->parity_.resize(plen[i]);
     g->dirty_ = false;
   }
   return QFEC_OK;
