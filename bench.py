@@ -81,6 +81,19 @@ def _cpu_model():
     return ""
 
 
+def _cpu_share():
+    """CPUs this process may actually use: affinity mask, capped by a cgroup v2
+    CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n or 1
+
+
 def cpu_baseline(rows, G, k, L, seconds, threads=0):
     """The CPU FEC path (the oracle's C restatement: word-wise uint64 XOR +
     byte tail, contiguous group split over pthreads) on the host cores, over
@@ -111,15 +124,26 @@ def cpu_baseline(rows, G, k, L, seconds, threads=0):
             if el >= budget:
                 return reps * bytes_per_pass / el / 2**30, reps, el
 
-    mt, reps_mt, el_mt = run(threads, seconds / 2)
+    # thread sweep: the box's CPU share (affinity / cgroup quota) can be far
+    # below nproc, where nproc threads only oversubscribe it
+    share = _cpu_share()
+    cands = sorted({t for t in (share, 16, 32, 64, threads) if 1 <= t <= threads})
+    sweep = {}
+    for th in cands:
+        v, reps, el = run(th, max(1.0, seconds / 2 / len(cands)))
+        sweep[th] = round(v, 3)
+    best = max(sweep, key=sweep.get)
+    mt, reps_mt, el_mt = sweep[best], None, None
     st, reps_st, el_st = run(1, seconds / 2)
     # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
     ns_group = lib.qo_time_single_group_ns(k, L, 200000)
     return {
-        "value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "value": round(mt, 3), "unit": "GiB/s", "cores": best, "kind": "port",
         "sample": f"oracle encode+recover of the bench workload itself ({G} groups x {k} x {L} B,"
-                  f" {bytes_per_pass / 1e9:.1f} GB per pass): {reps_mt} passes in {el_mt:.1f} s on "
-                  f"{threads} threads; {reps_st} passes in {el_st:.1f} s on 1 core",
+                  f" {bytes_per_pass / 1e9:.1f} GB per pass): best of a thread sweep "
+                  f"{sweep} (GiB/s by threads; box CPU share {share} of nproc "
+                  f"{os.cpu_count()}); {reps_st} passes in {el_st:.1f} s on 1 core",
+        "threads_sweep": sweep, "cpu_share": share,
         "single_core_value": round(st, 3),
         "configs0_ns_per_group_1core": round(ns_group, 1),
         "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
@@ -719,7 +743,7 @@ def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
 def _cpu_aead_baseline(aead, hdr, L, n, seconds):
     """Oracle (vector-pinned scalar C) AEAD seal on the host cores."""
     from oracle import oracle_c as OC
-    threads = min(16, os.cpu_count() or 1)
+    threads = _cpu_share()
     rec = hdr + L
     rng = np.random.default_rng(2)
     data = rng.integers(0, 256, n * rec, dtype=np.uint8)
@@ -769,7 +793,7 @@ def _cpu_null_baseline(hdr, L, n, seconds):
     if ref_quic.available():
         enc, kind, what = ref_quic.null_encrypt_batch, "reference", \
             "the reference's NullEncrypter compiled from its sources"
-    threads = min(16, os.cpu_count() or 1)
+    threads = _cpu_share()
     rec = hdr + L
     rng = np.random.default_rng(1)
     data = rng.integers(0, 256, n * rec, dtype=np.uint8)
@@ -1033,7 +1057,7 @@ def _cpu_fused_baseline(k, L, hdr, n=4096, seconds=4.0):
     BoringSSL aes.c + gcm.c from oracle/_ref when present, else the port)."""
     from oracle import oracle_c as OC
     from oracle import ref_quic
-    threads = min(256, os.cpu_count() or 1)
+    threads = _cpu_share()
     npk = n * (k + 1)
     rows_b, par_b = n * k * L, n * L
     buf = np.zeros(rows_b + par_b + npk * hdr, np.uint8)

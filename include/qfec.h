@@ -147,6 +147,38 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
 /* out[j] ^= in[j] for j < n (QuicFecGroupInterface::XorBuffers). */
 int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, uint32_t flags);
 
+/* ---- v<=31 FEC wire format (host memory; no device involved) ----------- */
+/* What an FFI user (e.g. a cgo binding) needs around the parity bytes:
+ *   private flags byte + 1-byte first_fec_protected_packet_offset, with the
+ *   checks of QuicFramer::ProcessAuthenticatedHeader (quic_framer.cc:1102-1141:
+ *   flags above the version's maximum are illegal — v > 31 allows only the
+ *   entropy bit, quic_protocol.h:343-358 — and the offset must be below the
+ *   packet number; the group is packet_number - offset);
+ *   the ack frame's revived-packets list (count byte + N packet numbers of the
+ *   largest-observed length, little-endian: quic_framer.cc:1477-1493 read,
+ *   :2307-2317 write, kNumberOfRevivedPacketsSize quic_framer.h:64-65);
+ *   an FEC packet body: private header (FEC | FEC_GROUP, offset) + redundancy.
+ * Each returns the bytes written / consumed, or 0 on failure with the
+ * framer's detailed error string in qfec_last_error(NULL). */
+typedef struct qfec_fec_header {
+  uint8_t entropy_flag;     /* PACKET_PRIVATE_FLAGS_ENTROPY */
+  uint8_t fec_flag;         /* PACKET_PRIVATE_FLAGS_FEC: the payload is redundancy */
+  uint8_t in_fec_group;     /* PACKET_PRIVATE_FLAGS_FEC_GROUP: offset byte follows */
+  uint8_t fec_group_offset; /* packet_number - first protected packet number */
+} qfec_fec_header;
+
+size_t qfec_wire_write_private_header(const qfec_fec_header* h, uint8_t* buf, size_t cap);
+size_t qfec_wire_parse_private_header(const uint8_t* buf, size_t len, int quic_version,
+                                      uint64_t packet_number, qfec_fec_header* out);
+size_t qfec_wire_write_revived(const uint64_t* revived, size_t n, size_t packet_number_length,
+                               uint8_t* buf, size_t cap);
+/* Parses into revived[0 .. *n_out) (at most 255 entries: size the array so). */
+size_t qfec_wire_parse_revived(const uint8_t* buf, size_t len, size_t packet_number_length,
+                               uint64_t* revived, size_t* n_out);
+size_t qfec_wire_fec_packet_body(uint64_t packet_number, uint64_t fec_group, int entropy_flag,
+                                 const uint8_t* redundancy, size_t redundancy_len, uint8_t* buf,
+                                 size_t cap);
+
 /* ---- packet protection around FEC (ENCRYPTION_NONE) -------------------- */
 /* The NULL packet protection libquic applies before the handshake completes:
  * a 12-byte FNV-1a-128 tag of header || payload written in front of the

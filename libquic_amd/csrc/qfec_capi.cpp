@@ -12,10 +12,12 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/qfec.h"
 #include "qfec_internal.h"
+#include "quic_fec_wire.h"
 
 namespace {
 
@@ -283,6 +285,73 @@ const char* qfec_strerror(int code) {
 }
 
 const char* qfec_last_error(const qfec_ctx* ctx) { return ctx ? ctx->last_error : g_tls_error; }
+
+// ---- v<=31 wire format: C wrappers over quic_fec_wire.h ---------------------
+size_t qfec_wire_write_private_header(const qfec_fec_header* h, uint8_t* buf, size_t cap) {
+  if (!h || !buf) return fail(nullptr, 0, "null buffer"), 0;
+  net::FecHeaderFields f;
+  f.entropy_flag = h->entropy_flag != 0;
+  f.fec_flag = h->fec_flag != 0;
+  f.in_fec_group = h->in_fec_group != 0;
+  f.fec_group_offset = h->fec_group_offset;
+  const size_t n = net::WriteFecPrivateHeader(f, buf, cap);
+  if (n == 0) fail(nullptr, 0, "private header does not fit or FEC flag without a group");
+  return n;
+}
+
+size_t qfec_wire_parse_private_header(const uint8_t* buf, size_t len, int quic_version,
+                                      uint64_t packet_number, qfec_fec_header* out) {
+  if ((!buf && len) || !out) return fail(nullptr, 0, "null buffer"), 0;
+  net::FecHeaderFields f;
+  std::string err;
+  const size_t n = net::ParseFecPrivateHeader(buf, len, quic_version, packet_number, &f, &err);
+  if (n == 0) {
+    fail(nullptr, 0, "%s", err.c_str());
+    return 0;
+  }
+  out->entropy_flag = f.entropy_flag;
+  out->fec_flag = f.fec_flag;
+  out->in_fec_group = f.in_fec_group;
+  out->fec_group_offset = f.fec_group_offset;
+  return n;
+}
+
+size_t qfec_wire_write_revived(const uint64_t* revived, size_t n, size_t packet_number_length,
+                               uint8_t* buf, size_t cap) {
+  if ((!revived && n) || !buf) return fail(nullptr, 0, "null buffer"), 0;
+  std::vector<net::QuicPacketNumber> v(revived, revived + n);
+  const size_t w = net::WriteRevivedPackets(v, packet_number_length, buf, cap);
+  if (w == 0) fail(nullptr, 0, "revived list does not fit (count > 255, length or capacity)");
+  return w;
+}
+
+size_t qfec_wire_parse_revived(const uint8_t* buf, size_t len, size_t packet_number_length,
+                               uint64_t* revived, size_t* n_out) {
+  if ((!buf && len) || !revived || !n_out) return fail(nullptr, 0, "null buffer"), 0;
+  std::vector<net::QuicPacketNumber> v;
+  std::string err;
+  const size_t n = net::ParseRevivedPackets(buf, len, packet_number_length, &v, &err);
+  if (n == 0) {
+    fail(nullptr, 0, "%s", err.c_str());
+    return 0;
+  }
+  std::copy(v.begin(), v.end(), revived);
+  *n_out = v.size();
+  return n;
+}
+
+size_t qfec_wire_fec_packet_body(uint64_t packet_number, uint64_t fec_group, int entropy_flag,
+                                 const uint8_t* redundancy, size_t redundancy_len, uint8_t* buf,
+                                 size_t cap) {
+  if ((!redundancy && redundancy_len) || !buf) return fail(nullptr, 0, "null buffer"), 0;
+  const size_t n = net::SerializeFecPacketBody(
+      packet_number, fec_group, entropy_flag != 0,
+      net::StringPiece(reinterpret_cast<const char*>(redundancy), redundancy_len), buf, cap);
+  if (n == 0)
+    fail(nullptr, 0, "FEC packet body: group outside the uint8 offset range, redundancy above "
+                     "kMaxPacketSize or capacity too small");
+  return n;
+}
 
 qfec_ctx* qfec_create(int device) {
   int count = 0;

@@ -53,6 +53,13 @@ SIGNATURES = [
     ("qfec_recover_ragged", C.c_int,
      [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _vp, _u8p, _u8p, _vp, C.c_uint32]),
     ("qfec_xor_into", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_wire_write_private_header", C.c_size_t, [_vp, _u8p, C.c_size_t]),
+    ("qfec_wire_parse_private_header", C.c_size_t,
+     [_u8p, C.c_size_t, C.c_int, C.c_uint64, _vp]),
+    ("qfec_wire_write_revived", C.c_size_t, [_vp, C.c_size_t, C.c_size_t, _u8p, C.c_size_t]),
+    ("qfec_wire_parse_revived", C.c_size_t, [_u8p, C.c_size_t, C.c_size_t, _vp, _vp]),
+    ("qfec_wire_fec_packet_body", C.c_size_t,
+     [C.c_uint64, C.c_uint64, C.c_int, _u8p, C.c_size_t, _u8p, C.c_size_t]),
     ("qfec_null_encrypt_batch", C.c_int,
      [_vp, _u8p, _vp, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, C.c_uint32]),
     ("qfec_null_decrypt_batch", C.c_int,
@@ -297,3 +304,59 @@ class Context:
         return self._check(self.lib.qfec_synth_ragged(self.ctx, _ptr(data), _ptr(pkt_off),
                                                       _ptr(pkt_len), _ptr(grp_ptr), g0,
                                                       n_groups, seed))
+
+
+# -- v<=31 wire format (host-only C-ABI: no device, no context) -------------------
+class FecHeader(C.Structure):
+    """qfec_fec_header"""
+    _fields_ = [("entropy_flag", C.c_uint8), ("fec_flag", C.c_uint8),
+                ("in_fec_group", C.c_uint8), ("fec_group_offset", C.c_uint8)]
+
+
+def _last_error():
+    return load().qfec_last_error(None).decode()
+
+
+def wire_write_private_header(entropy=False, fec=False, in_group=False, offset=0):
+    """bytes written by qfec_wire_write_private_header (b"" on failure)."""
+    h = FecHeader(int(entropy), int(fec), int(in_group), offset)
+    buf = (C.c_uint8 * 4)()
+    n = load().qfec_wire_write_private_header(C.byref(h), C.addressof(buf), 4)
+    return bytes(buf[:n])
+
+
+def wire_parse_private_header(data: bytes, version: int, packet_number: int):
+    """(consumed, FecHeader) or (0, detailed_error)."""
+    h = FecHeader()
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    n = load().qfec_wire_parse_private_header(C.addressof(buf), len(data), version,
+                                              packet_number, C.byref(h))
+    return (n, h) if n else (0, _last_error())
+
+
+def wire_write_revived(revived, packet_number_length):
+    arr = (C.c_uint64 * max(1, len(revived)))(*revived)
+    cap = 1 + len(revived) * 8
+    buf = (C.c_uint8 * cap)()
+    n = load().qfec_wire_write_revived(C.addressof(arr), len(revived), packet_number_length,
+                                       C.addressof(buf), cap)
+    return bytes(buf[:n])
+
+
+def wire_parse_revived(data: bytes, packet_number_length):
+    """(consumed, [packet numbers]) or (0, detailed_error)."""
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    out = (C.c_uint64 * 256)()
+    cnt = C.c_size_t(0)
+    n = load().qfec_wire_parse_revived(C.addressof(buf), len(data), packet_number_length,
+                                       C.addressof(out), C.byref(cnt))
+    return (n, list(out[:cnt.value])) if n else (0, _last_error())
+
+
+def wire_fec_packet_body(packet_number, fec_group, entropy, redundancy: bytes):
+    red = (C.c_uint8 * max(1, len(redundancy))).from_buffer_copy(redundancy or b"\0")
+    cap = 2 + len(redundancy)
+    buf = (C.c_uint8 * cap)()
+    n = load().qfec_wire_fec_packet_body(packet_number, fec_group, int(entropy),
+                                         C.addressof(red), len(redundancy), C.addressof(buf), cap)
+    return bytes(buf[:n])

@@ -23,7 +23,7 @@ _lib = None
 def build() -> bool:
     """Build from /root/reference when it exists (this container only)."""
     if os.path.isdir(REF):
-        subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "ref"), f"REF={REF}"], check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "ref"), f"REF={REF}"], check=True)
     return os.path.exists(SO)
 
 
