@@ -1,0 +1,230 @@
+// patched_shim.cc — end-to-end drop-in check of integration/libquic_fec.patch:
+// the REFERENCE's QuicPacketCreator and QuicFramer, patched, sending and
+// receiving a FEC-protected QUIC_VERSION_31 stream through the MI355X FEC path.
+//
+// Built by integration/build.py into integration/_build/libquic_fec_patched.so
+// together with the patched reference sources and the FEC host code
+// (-DQFEC_WITH_LIBQUIC); the XOR runs in libqfec.so on the GPU.
+//
+//   send:    QuicPacketCreator (patched SerializePacket: FEC encode hook,
+//            MaybeSendFecPacketAndCloseGroup: FEC packets via BuildFecPacket)
+//            with a QuicFecSender, NULL encryption, a delegate that keeps the
+//            encrypted packets;
+//   channel: one data packet in `drop_every` dropped (never an FEC packet);
+//   receive: QuicFramer (patched ProcessAuthenticatedHeader / ProcessDataPacket
+//            -> OnFecProtectedPayload / OnFecData) with a visitor that feeds a
+//            QuicFecReceiver, as the patched QuicConnection does; after every
+//            packet, revivable groups are revived in one launch and re-injected
+//            through QuicFramer::ProcessRevivedPacket; the visitor reassembles
+//            the stream from received AND revived stream frames.
+// The stream must come out byte-identical with every dropped packet revived.
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "net/quic/core/crypto/quic_random.h"
+#include "net/quic/core/quic_fec_connection.h"
+#include "net/quic/core/quic_framer.h"
+#include "net/quic/core/quic_packet_creator.h"
+#include "net/quic/core/quic_simple_buffer_allocator.h"
+#include "net/quic/core/quic_utils.h"
+
+using namespace net;
+
+extern "C" {
+struct fec_e2e_result {
+  uint64_t data_packets_sent;
+  uint64_t fec_packets_sent;
+  uint64_t dropped;
+  uint64_t revived;
+  uint64_t stream_bytes;
+  int32_t stream_ok;      // reassembled stream == sent stream
+  int32_t framer_errors;  // packets the receiving framer refused
+  int32_t fec_header_ok;  // every received data packet carried in_fec_group + group
+  int32_t status;         // 0 ok, else a failure code
+  char detail[256];
+};
+}
+
+namespace {
+
+class CollectingDelegate : public QuicPacketCreator::DelegateInterface {
+ public:
+  struct Sent {
+    QuicPacketNumber number;
+    std::string bytes;
+  };
+  void OnSerializedPacket(SerializedPacket* p) override {
+    sent.push_back({p->packet_number, std::string(p->encrypted_buffer, p->encrypted_length)});
+    QuicUtils::DeleteFrames(&p->retransmittable_frames);
+  }
+  void OnUnrecoverableError(QuicErrorCode error, const std::string& details,
+                            ConnectionCloseSource) override {
+    this->error = details.empty() ? "unrecoverable error" : details;
+  }
+  std::vector<Sent> sent;
+  std::string error;
+};
+
+class ReceiverVisitor : public QuicFramerVisitorInterface {
+ public:
+  explicit ReceiverVisitor(size_t stream_len) : stream(stream_len, '\0'), have(stream_len, 0) {}
+  void OnError(QuicFramer*) override {}
+  bool OnProtocolVersionMismatch(QuicVersion) override { return false; }
+  void OnPacket() override {}
+  void OnPublicResetPacket(const QuicPublicResetPacket&) override {}
+  void OnVersionNegotiationPacket(const QuicVersionNegotiationPacket&) override {}
+  bool OnUnauthenticatedPublicHeader(const QuicPacketPublicHeader&) override { return true; }
+  bool OnUnauthenticatedHeader(const QuicPacketHeader&) override { return true; }
+  void OnDecryptedPacket(EncryptionLevel level) override { level_ = level; }
+  bool OnPacketHeader(const QuicPacketHeader& h) override {
+    last_header = h;
+    if (!h.fec_flag && h.is_in_fec_group != IN_FEC_GROUP) header_ok = false;
+    return true;
+  }
+  bool OnStreamFrame(const QuicStreamFrame& f) override {
+    if (f.offset + f.data_length > stream.size()) return false;
+    std::memcpy(&stream[f.offset], f.data_buffer, f.data_length);
+    std::memset(&have[f.offset], 1, f.data_length);
+    return true;
+  }
+  bool OnAckFrame(const QuicAckFrame&) override { return true; }
+  bool OnStopWaitingFrame(const QuicStopWaitingFrame&) override { return true; }
+  bool OnPaddingFrame(const QuicPaddingFrame&) override { return true; }
+  bool OnPingFrame(const QuicPingFrame&) override { return true; }
+  bool OnRstStreamFrame(const QuicRstStreamFrame&) override { return true; }
+  bool OnConnectionCloseFrame(const QuicConnectionCloseFrame&) override { return true; }
+  bool OnGoAwayFrame(const QuicGoAwayFrame&) override { return true; }
+  bool OnWindowUpdateFrame(const QuicWindowUpdateFrame&) override { return true; }
+  bool OnBlockedFrame(const QuicBlockedFrame&) override { return true; }
+  bool OnPathCloseFrame(const QuicPathCloseFrame&) override { return true; }
+  void OnPacketComplete() override {}
+  // the patched framer's FEC callbacks -> the receiver's group map
+  void OnFecProtectedPayload(base::StringPiece payload) override {
+    fec_receiver.OnPacket(level_, last_header, payload);
+  }
+  bool OnFecData(base::StringPiece redundancy) override {
+    fec_receiver.OnPacket(level_, last_header, redundancy);
+    return true;
+  }
+
+  QuicFecReceiver fec_receiver;
+  QuicPacketHeader last_header;
+  std::string stream;
+  std::vector<uint8_t> have;
+  bool header_ok = true;
+
+ private:
+  EncryptionLevel level_ = ENCRYPTION_NONE;
+};
+
+}  // namespace
+
+#define SHIM_API extern "C" __attribute__((visibility("default")))
+
+SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int drop_every,
+                         fec_e2e_result* r) {
+  std::memset(r, 0, sizeof(*r));
+  const QuicVersion v = static_cast<QuicVersion>(version);
+  const QuicStreamId kStream = 5;
+  // the stream: counter bytes
+  std::string data(stream_len, '\0');
+  for (uint64_t i = 0; i < stream_len; ++i)
+    data[i] = static_cast<char>((i * 2654435761u) >> 13);
+
+  // ---- send
+  QuicFramer client(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_CLIENT);
+  client.set_version(v);
+  SimpleBufferAllocator allocator;
+  CollectingDelegate delegate;
+  QuicPacketCreator creator(0x1122334455667788ull, &client, QuicRandom::GetInstance(), &allocator,
+                            &delegate);
+  creator.StopSendingVersion();
+  QuicFecSender fec_sender(group_size);
+  creator.set_fec_sender(&fec_sender);
+  struct iovec iov;
+  QuicIOVector io = MakeIOVector(data, &iov);
+  uint64_t off = 0;
+  while (off < stream_len) {
+    QuicFrame frame;
+    if (!creator.ConsumeData(kStream, io, off, off, false, false, &frame)) {
+      std::snprintf(r->detail, sizeof(r->detail), "ConsumeData failed at %llu",
+                    (unsigned long long)off);
+      r->status = 1;
+      return r->status;
+    }
+    off += frame.stream_frame->data_length;
+    creator.Flush();  // one stream frame per packet; FEC packet when a group fills
+  }
+  creator.MaybeSendFecPacketAndCloseGroup(/*force_close=*/true);
+  if (!delegate.error.empty()) {
+    std::snprintf(r->detail, sizeof(r->detail), "sender: %s", delegate.error.c_str());
+    r->status = 2;
+    return r->status;
+  }
+
+  // ---- receive (drop one data packet in drop_every)
+  QuicFramer server(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_SERVER);
+  server.set_version(v);
+  ReceiverVisitor visitor(stream_len);
+  server.set_visitor(&visitor);
+  qfec_ctx* ctx = qfec_create(0);
+  if (!ctx) {
+    std::snprintf(r->detail, sizeof(r->detail), "qfec_create: %s", qfec_last_error(nullptr));
+    r->status = 3;
+    return r->status;
+  }
+  uint64_t data_index = 0;
+  for (const auto& p : delegate.sent) {
+    // an FEC packet's private flags carry PACKET_PRIVATE_FLAGS_FEC; the
+    // sender knows which it sent: FEC packets are those the creator emitted
+    // right after closing a group — recognised here by parsing
+    QuicEncryptedPacket pkt(p.bytes.data(), p.bytes.size(), false);
+    const bool is_fec = [&] {
+      QuicFramer probe(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_SERVER);
+      probe.set_version(v);
+      ReceiverVisitor pv(stream_len);
+      probe.set_visitor(&pv);
+      probe.ProcessPacket(pkt);
+      return pv.last_header.fec_flag;
+    }();
+    if (is_fec) {
+      ++r->fec_packets_sent;
+    } else {
+      ++r->data_packets_sent;
+      if (drop_every > 0 && data_index++ % drop_every == static_cast<uint64_t>(drop_every / 2)) {
+        ++r->dropped;
+        continue;
+      }
+    }
+    if (!server.ProcessPacket(pkt)) ++r->framer_errors;
+    // the patched QuicConnection's MaybeProcessRevivedPackets
+    QuicFecReviveBatch batch;
+    if (visitor.fec_receiver.CollectRevivable(&batch) > 0) {
+      std::vector<QuicFecReviveBatch::Revived> revived;
+      if (batch.Flush(ctx, &revived) != QFEC_OK) {
+        std::snprintf(r->detail, sizeof(r->detail), "revive flush: %s", qfec_last_error(ctx));
+        r->status = 4;
+        break;
+      }
+      for (auto& rv : revived) {
+        QuicPacketHeader h(visitor.last_header.public_header);
+        h.packet_number = rv.header.packet_number;
+        h.is_in_fec_group = IN_FEC_GROUP;
+        h.fec_group = rv.header.fec_group;
+        if (server.ProcessRevivedPacket(&h, rv.payload))
+          ++r->revived;
+        else
+          ++r->framer_errors;
+      }
+    }
+  }
+  qfec_destroy(ctx);
+  r->stream_bytes = stream_len;
+  bool all = true;
+  for (uint8_t b : visitor.have) all &= b != 0;
+  r->stream_ok = all && visitor.stream == data;
+  r->fec_header_ok = visitor.header_ok;
+  return r->status;
+}

@@ -77,6 +77,8 @@ class QuicFecSender {
                     FecHeaderFields* fields);
 
   bool IsFecGroupOpen() const { return group_ != nullptr; }
+  // The open group's number (its first packet), 0 when none is open.
+  QuicFecGroupNumber FecGroupNumber() const { return group_ ? group_->FecGroupNumber() : 0; }
   size_t NumPacketsInGroup() const { return group_ ? group_->NumReceivedPackets() : 0; }
   // The open group is full, or force_close and it holds at least one packet.
   bool ShouldSendFec(bool force_close) const;

@@ -31,7 +31,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/qfec.h"
+#include "qfec.h"  // include/qfec.h
 
 #ifdef QFEC_WITH_LIBQUIC
 // Built inside libquic, with integration/libquic_fec.patch applied: the
