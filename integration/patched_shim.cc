@@ -23,6 +23,7 @@
 #include <string>
 #include <vector>
 
+#include "net/quic/core/crypto/null_encrypter.h"
 #include "net/quic/core/crypto/quic_random.h"
 #include "net/quic/core/quic_fec_connection.h"
 #include "net/quic/core/quic_framer.h"
@@ -141,6 +142,11 @@ SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int d
   QuicPacketCreator creator(0x1122334455667788ull, &client, QuicRandom::GetInstance(), &allocator,
                             &delegate);
   creator.StopSendingVersion();
+  // stream data needs a non-NONE encryption level (QuicPacketCreator::AddFrame
+  // refuses it otherwise); NullEncrypter at FORWARD_SECURE keeps the bytes
+  // readable by the server framer's default NullDecrypter
+  client.SetEncrypter(ENCRYPTION_FORWARD_SECURE, new NullEncrypter());
+  creator.set_encryption_level(ENCRYPTION_FORWARD_SECURE);
   QuicFecSender fec_sender(group_size);
   creator.set_fec_sender(&fec_sender);
   struct iovec iov;
@@ -157,7 +163,12 @@ SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int d
     off += frame.stream_frame->data_length;
     creator.Flush();  // one stream frame per packet; FEC packet when a group fills
   }
+  const size_t sent_before_close = delegate.sent.size();
+  const bool open_before_close = fec_sender.IsFecGroupOpen();
   creator.MaybeSendFecPacketAndCloseGroup(/*force_close=*/true);
+  std::snprintf(r->detail, sizeof(r->detail),
+                "sent %zu packets before the final close (group open: %d), %zu after",
+                sent_before_close, (int)open_before_close, delegate.sent.size());
   if (!delegate.error.empty()) {
     std::snprintf(r->detail, sizeof(r->detail), "sender: %s", delegate.error.c_str());
     r->status = 2;
@@ -176,19 +187,19 @@ SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int d
     return r->status;
   }
   uint64_t data_index = 0;
+  // The sender knows which packets it sent as FEC packets; here they are
+  // recognised by parsing every sent packet, in send order, with one probe
+  // framer (it must see the whole sequence: a 1-byte packet number is
+  // expanded against the last one it saw).
+  QuicFramer probe(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_SERVER);
+  probe.set_version(v);
+  ReceiverVisitor pv(stream_len);
+  probe.set_visitor(&pv);
   for (const auto& p : delegate.sent) {
-    // an FEC packet's private flags carry PACKET_PRIVATE_FLAGS_FEC; the
-    // sender knows which it sent: FEC packets are those the creator emitted
-    // right after closing a group — recognised here by parsing
     QuicEncryptedPacket pkt(p.bytes.data(), p.bytes.size(), false);
-    const bool is_fec = [&] {
-      QuicFramer probe(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_SERVER);
-      probe.set_version(v);
-      ReceiverVisitor pv(stream_len);
-      probe.set_visitor(&pv);
-      probe.ProcessPacket(pkt);
-      return pv.last_header.fec_flag;
-    }();
+    pv.last_header = QuicPacketHeader();
+    probe.ProcessPacket(pkt);
+    const bool is_fec = pv.last_header.fec_flag;
     if (is_fec) {
       ++r->fec_packets_sent;
     } else {

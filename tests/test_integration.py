@@ -92,7 +92,7 @@ def test_patched_libquic_end_to_end(group_size, stream_len, drop_every):
     r = _run(group_size, stream_len, drop_every)
     assert r.framer_errors == 0
     assert r.fec_header_ok == 1
-    assert r.fec_packets_sent == -(-r.data_packets_sent // group_size)
+    assert r.fec_packets_sent == -(-r.data_packets_sent // group_size), r.detail.decode()
     if drop_every:
         assert r.dropped > 0
     # a group revives iff it lost exactly one packet

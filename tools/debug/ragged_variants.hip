@@ -5,7 +5,7 @@
 // groups, nondeterministically (root cause not found; the product uses b32).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/debug/ragged_variants.hip -o tools/debug/build/ragged_variants
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
-#include "../tune/pipe_ragged.inc"
+
 
 #include <cstdio>
 #include <cstdlib>
@@ -122,14 +122,6 @@ int main(int argc, char** argv) {
    }}
   std::vector<V> vs = {
       {"product", [&](bool r) { CK(launch_ragged(r ? ar : ae, r, 0)); }},
-      {"pipe grid 2048", [&](bool r) {
-         if (r) hipLaunchKernelGGL((ragged_pipe_kernel<true, true>), dim3(2048), blk, 0, 0, ar);
-         else hipLaunchKernelGGL((ragged_pipe_kernel<false, true>), dim3(2048), blk, 0, 0, ae);
-       }},
-      {"pipe grid 37", [&](bool r) {
-         if (r) hipLaunchKernelGGL((ragged_pipe_kernel<true, true>), dim3(37), blk, 0, 0, ar);
-         else hipLaunchKernelGGL((ragged_pipe_kernel<false, true>), dim3(37), blk, 0, 0, ae);
-       }},
       QV("nt U2 b32", true, 2, 0),    QV("nt U4 b32", true, 4, 0),
       QV("nt U8 b32", true, 8, 0),    QV("def U4 b32", false, 4, 0),
       QV("nt U2 b32cm", true, 2, 1),  QV("nt U4 b32cm", true, 4, 1),

@@ -1,0 +1,2 @@
+mkdir -p gpurun_out
+timeout -k 10 300 tools/tune/build/tune_rw 2 1 > gpurun_out/tune_rw_h.txt 2>&1

@@ -1,15 +1,14 @@
-// tune_multi.hip — A/B of the ragged kernels: GPW groups per wave
-// (ragged_multi_kernel; the product runs GPW = 2) against one group per wave
-// (ragged_xor_kernel), branch-free / aligned-chunk / XCD variants, encode and
-// recover on the BASELINE configs[3] batch (2^20 groups, k 5-15, 64-1350 B,
-// packed CSR).  Every variant's output bytes are compared with the product's.
+// tune_rw.hip — A/B of the ragged kernels: the parity-window form
+// (ragged_window_kernel, PB load slots in flight) against the flat-window
+// two-groups-per-wave kernel (ragged_multi_kernel), encode and recover on the
+// BASELINE configs[3] batch (2^20 groups, k 5-15, 64-1350 B, packed CSR) or
+// another k / length range.  Every variant's output bytes are compared with
+// the multi kernel's, which is checked against a host XOR on a sample.
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_multi.hip -o tools/tune/build/tune_multi
-// run:   tune_multi [reps] [rounds] [kmin] [kspan] [align16] [packed_out]
-//        packed_out = 1: parity / revived rows back to back (offset = running sum of
-//        parity lengths) instead of 1452-byte slots
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rw.hip -o tools/tune/build/tune_rw
+// run:   tune_rw [reps] [rounds] [kmin] [kspan] [lmin] [lspan] [packed_out]
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
-#include "al_ragged.inc"
+#include "ragged_exp.inc"
 
 #include <algorithm>
 #include <cstdio>
@@ -46,35 +45,23 @@ static T* up(const std::vector<T>& v) {
 
 using qfec::RaggedArgs;
 
-template <bool REC, int GPW, int WAVES, int U = 2>
+template <bool REC, int GPW, bool NT = true>
 static void launch_multi(const RaggedArgs& a, uint64_t G) {
-  const uint64_t per = (uint64_t)GPW * WAVES;
-  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, true, GPW, U, WAVES>),
-                     dim3((uint32_t)((G + per - 1) / per)), dim3(64 * WAVES), 0, 0, a);
+  const uint64_t per = (uint64_t)GPW * 4;
+  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, NT, GPW>),
+                     dim3((uint32_t)((G + per - 1) / per)), dim3(256), 0, 0, a);
 }
 
-template <bool REC, int U>
-static void launch_bf(const RaggedArgs& a, uint64_t G) {
-  hipLaunchKernelGGL((qfec::ragged_xor_kernel<REC, true, U, 4, 1, true>),
-                     dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
+template <bool REC, int B, bool GATE, int FENCE = 0, int DBG = 0>
+static void launch_flat(const RaggedArgs& a, uint64_t G) {
+  hipLaunchKernelGGL((qfec::ragged_flat_kernel<REC, true, B, GATE, FENCE, DBG>), dim3((uint32_t)((G + 3) / 4)),
+                     dim3(256), 0, 0, a);
 }
 
-template <bool REC, int U>
-static void launch_al(const RaggedArgs& a, uint64_t G) {
-  hipLaunchKernelGGL((qfec::ragged_al_kernel<REC, true, U, 4, 1>),
-                     dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
-}
-
-template <bool REC>
-static void launch_1g(const RaggedArgs& a, uint64_t G) {
-  hipLaunchKernelGGL((qfec::ragged_xor_kernel<REC, true>), dim3((uint32_t)((G + 3) / 4)), dim3(256),
-                     0, 0, a);
-}
-
-template <bool REC>
-static void launch_xcd(const RaggedArgs& a, uint64_t G) {
-  hipLaunchKernelGGL((qfec::ragged_xor_kernel<REC, true, 2, 4, 1, false, true>),
-                     dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, 0, a);
+template <bool REC, int PB, bool NT = true>
+static void launch_win(const RaggedArgs& a, uint64_t G) {
+  hipLaunchKernelGGL((qfec::ragged_window_kernel<REC, NT, PB>), dim3((uint32_t)((G + 3) / 4)),
+                     dim3(256), 0, 0, a);
 }
 
 int main(int argc, char** argv) {
@@ -82,8 +69,8 @@ int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
   const uint32_t kmin = argc > 3 ? atoi(argv[3]) : 5, kspan = argc > 4 ? atoi(argv[4]) : 11;
-  const bool align16 = argc > 5 && atoi(argv[5]) != 0;
-  const bool packed_out = argc > 6 && atoi(argv[6]) != 0;
+  const uint32_t lmin = argc > 5 ? atoi(argv[5]) : 64, lspan = argc > 6 ? atoi(argv[6]) : 1287;
+  const bool packed_out = argc > 7 && atoi(argv[7]) != 0;
   uint64_t out_pos = 0;
   const uint64_t seed = 0x51554944;
   std::vector<uint32_t> ptr{0};
@@ -98,8 +85,7 @@ int main(int argc, char** argv) {
     uint32_t mx = 0;
     double s = 0, sm = 0;
     for (uint32_t i = 0; i < k; ++i) {
-      uint32_t ln = 64 + (uint32_t)(sm64(seed ^ (0x4Cull << 56) ^ (g * 256 + i)) % 1287);
-      if (align16) ln = std::min(1440u, (ln + 15u) & ~15u);  // 16-B multiples: aligned starts
+      const uint32_t ln = lmin + (uint32_t)(sm64(seed ^ (0x4Cull << 56) ^ (g * 256 + i)) % lspan);
       len.push_back((uint16_t)ln);
       off.push_back(bytes);
       bytes += ln;
@@ -144,7 +130,7 @@ int main(int argc, char** argv) {
   e.out = par;
   e.n_groups = G;
   e.err = err;
-  CK(qfec::launch_ragged(e, false, 0));  // reference parity for the recover runs
+  launch_multi<false, 2>(e, G);  // reference parity for the recover runs
   CK(hipDeviceSynchronize());
   RaggedArgs r = e;
   r.parity = par;
@@ -163,40 +149,14 @@ int main(int argc, char** argv) {
     std::function<void(const RaggedArgs&)> run;
   };
   std::vector<V> vs;
-  vs.push_back({"product encode", false, [](const RaggedArgs& a) { CK(qfec::launch_ragged(a, false, 0)); }});
-  vs.push_back({"BF U2 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 2>(a, G); }});
-  vs.push_back({"AL U2 encode", false, [=](const RaggedArgs& a) { launch_al<false, 2>(a, G); }});
-  vs.push_back({"AL U4 encode", false, [=](const RaggedArgs& a) { launch_al<false, 4>(a, G); }});
-  vs.push_back({"AL U6 encode", false, [=](const RaggedArgs& a) { launch_al<false, 6>(a, G); }});
-  vs.push_back({"AL U8 encode", false, [=](const RaggedArgs& a) { launch_al<false, 8>(a, G); }});
-  vs.push_back({"BF U3 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 3>(a, G); }});
-  vs.push_back({"BF U4 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 4>(a, G); }});
-  vs.push_back({"BF U6 encode", false, [=](const RaggedArgs& a) { launch_bf<false, 6>(a, G); }});
-  vs.push_back({"multi2 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4>(a, G); }});
-  vs.push_back({"multi2 w4 U1 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4, 1>(a, G); }});
-  vs.push_back({"multi2 w4 U3 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 4, 3>(a, G); }});
-  vs.push_back({"multi2 w2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 2>(a, G); }});
-  vs.push_back({"multi2 w8 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, 8>(a, G); }});
-  vs.push_back({"1 group/wave encode", false, [=](const RaggedArgs& a) { launch_1g<false>(a, G); }});
-  vs.push_back({"multi3 w4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, 4>(a, G); }});
-  vs.push_back({"product XCD encode", false, [=](const RaggedArgs& a) { launch_xcd<false>(a, G); }});
-  vs.push_back({"product recover", true, [](const RaggedArgs& a) { CK(qfec::launch_ragged(a, true, 0)); }});
-  vs.push_back({"BF U2 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 2>(a, G); }});
-  vs.push_back({"AL U2 recover", true, [=](const RaggedArgs& a) { launch_al<true, 2>(a, G); }});
-  vs.push_back({"AL U4 recover", true, [=](const RaggedArgs& a) { launch_al<true, 4>(a, G); }});
-  vs.push_back({"AL U6 recover", true, [=](const RaggedArgs& a) { launch_al<true, 6>(a, G); }});
-  vs.push_back({"AL U8 recover", true, [=](const RaggedArgs& a) { launch_al<true, 8>(a, G); }});
-  vs.push_back({"BF U3 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 3>(a, G); }});
-  vs.push_back({"BF U4 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 4>(a, G); }});
-  vs.push_back({"BF U6 recover", true, [=](const RaggedArgs& a) { launch_bf<true, 6>(a, G); }});
-  vs.push_back({"multi2 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4>(a, G); }});
-  vs.push_back({"multi2 w4 U1 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4, 1>(a, G); }});
-  vs.push_back({"multi2 w4 U3 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 4, 3>(a, G); }});
-  vs.push_back({"multi2 w2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 2>(a, G); }});
-  vs.push_back({"multi2 w8 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, 8>(a, G); }});
-  vs.push_back({"1 group/wave recover", true, [=](const RaggedArgs& a) { launch_1g<true>(a, G); }});
-  vs.push_back({"multi3 w4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, 4>(a, G); }});
-  vs.push_back({"product XCD recover", true, [=](const RaggedArgs& a) { launch_xcd<true>(a, G); }});
+  vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+  vs.push_back({"flat B10 g0 d8 encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 8>(a, G); }});
+  vs.push_back({"flat B10 g0 d4 encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 4>(a, G); }});
+  vs.push_back({"flat B10 g0 d0 encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 0>(a, G); }});
+  vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+  vs.push_back({"flat B10 g0 d8 recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 8>(a, G); }});
+  vs.push_back({"flat B10 g0 d4 recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 4>(a, G); }});
+  vs.push_back({"flat B10 g0 d0 recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 0>(a, G); }});
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
@@ -204,7 +164,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(want_e.data(), par, G * 1452, hipMemcpyDeviceToHost));
   CK(hipMemcpy(want_pl.data(), plen, G * 2, hipMemcpyDeviceToHost));
   CK(hipMemset(out, 0, G * 1452));
-  CK(qfec::launch_ragged(r, true, 0));
+  launch_multi<true, 2>(r, G);
   CK(hipMemcpy(want_r.data(), out, G * 1452, hipMemcpyDeviceToHost));
   {  // the product against a host XOR on a sample
     std::vector<uint8_t> h(bytes);
@@ -225,8 +185,10 @@ int main(int argc, char** argv) {
       bad += memcmp(ref, &want_e[poff[g]], mx) != 0 || want_pl[g] != mx;
       bad += memcmp(rv, &want_r[poff[g]], lm) != 0;
     }
-    std::printf("product vs host XOR: bad groups %d\n", bad);
+    std::printf("multi2 vs host XOR: bad groups %d\n", bad);
   }
+  std::vector<uint8_t> hdat(bytes);
+  CK(hipMemcpy(hdat.data(), data, bytes, hipMemcpyDeviceToHost));
   bool all_ok = true;
   for (auto& v : vs) {
     CK(hipMemset(out, 0, G * 1452));
@@ -241,7 +203,48 @@ int main(int argc, char** argv) {
     }
     uint32_t he;
     CK(hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost));
-    std::printf("%-24s == product: %s (err %u)\n", v.name.c_str(), same ? "yes" : "NO", he);
+    std::printf("%-24s == multi2: %s (err %u)\n", v.name.c_str(), same ? "yes" : "NO", he);
+    if (!same) {  // which groups, and where in them
+      const std::vector<uint8_t>& want = v.rec ? want_r : want_e;
+      uint64_t nbad = 0;
+      for (uint64_t g = 0; g < G; ++g) {
+        const uint8_t* x = &got[g * 1452];
+        const uint8_t* y = &want[g * 1452];
+        if (std::memcmp(x, y, 1452) == 0) continue;
+        if (nbad++ < 4) {
+          uint32_t j0 = 0, j1 = 0, W = 0;
+          while (x[j0] == y[j0]) ++j0;
+          j1 = 1451;
+          while (x[j1] == y[j1]) --j1;
+          for (uint32_t p = ptr[g]; p < ptr[g + 1]; ++p)
+            if (!v.rec || p - ptr[g] != miss[g]) W += (len[p] + 15) / 16;
+          std::printf("   bad g %llu k %u plen %u W %u nit %u bytes [%u, %u]\n",
+                      (unsigned long long)g, ptr[g + 1] - ptr[g], want_pl[g], W, (W + 63) / 64, j0, j1);
+          // which 16-B parity windows differ, and does the difference equal
+          // one packet's window (a lost or doubled XOR)?
+          std::printf("     windows:");
+          for (uint32_t t = 0; t < 91; ++t) {
+            if (std::memcmp(x + 16 * t, y + 16 * t, 16) == 0) continue;
+            std::printf(" %u", t);
+            // find the packet q and flat index whose window t equals the difference
+            for (uint32_t p = ptr[g], S = 0; p < ptr[g + 1]; ++p) {
+              if (v.rec && p - ptr[g] == miss[g]) continue;
+              const uint32_t n = (len[p] + 15) / 16;
+              if (t < n) {
+                uint8_t w[16] = {0};
+                for (uint32_t b = 0; b < 16 && 16 * t + b < len[p]; ++b) w[b] = hdat[off[p] + 16 * t + b];
+                bool eq = true;
+                for (uint32_t b = 0; b < 16; ++b) eq = eq && ((uint8_t)(x[16 * t + b] ^ y[16 * t + b]) == w[b]);
+                if (eq) std::printf("(=pkt%u f%u it%u)", p - ptr[g], S + t, (S + t) / 64);
+              }
+              S += n;
+            }
+          }
+          std::printf("\n");
+        }
+      }
+      std::printf("   bad groups %llu\n", (unsigned long long)nbad);
+    }
     all_ok = all_ok && same && he == 0;
   }
   hipEvent_t e0, e1;
@@ -261,8 +264,8 @@ int main(int argc, char** argv) {
       res[i].push_back((vs[i].rec ? rec_alg : enc_alg) / (ms / reps * 1e-3) / 1e9);
     }
   }
-  std::printf("k %u..%u, %llu groups, %.3f GB packets\n", kmin, kmin + kspan - 1,
-              (unsigned long long)G, bytes / 1e9);
+  std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packets\n", kmin, kmin + kspan - 1,
+              lmin, lmin + lspan - 1, (unsigned long long)G, bytes / 1e9);
   std::printf("%-24s %10s %10s %8s\n", "variant", "med GB/s", "max GB/s", "%8TB/s");
   for (size_t i = 0; i < vs.size(); ++i) {
     auto v = res[i];
