@@ -77,6 +77,16 @@ extern "C" {
                                policy instead of non-temporal (nt) loads and
                                stores — for small batches whose output is
                                consumed straight away from L2 / MALL */
+#define QFEC_PTR_MAPPED 4u  /* FEC calls (fixed, ragged, xor_into): the payload
+                               buffers (rows / bytes, parity, parity_out / out) are
+                               pinned, device-mapped host memory (qfec_host_alloc,
+                               or any hipHostMalloc'd / registered memory) that the
+                               kernels read and write IN PLACE over PCIe — no
+                               staging copy, the packets cross the link once; the
+                               index arrays (pkt_off, pkt_len, grp_ptr, parity_off,
+                               parity_len, missing_idx, out_off, parity_len_out)
+                               are ordinary host memory, staged by the call.
+                               Returns when the results are in host memory. */
 
 typedef struct qfec_ctx qfec_ctx;
 
@@ -97,6 +107,11 @@ void* qfec_own_stream(qfec_ctx* ctx);
  * device) since the previous qfec_sync, then clears it. */
 int qfec_sync(qfec_ctx* ctx);
 const char* qfec_strerror(int code);
+/* Pinned, device-mapped host memory for QFEC_PTR_MAPPED payloads (the
+ * registered receive / send buffers of a QUIC server: the GPU reads packets
+ * where the socket wrote them).  NULL on failure (qfec_last_error(NULL)). */
+void* qfec_host_alloc(size_t bytes);
+void qfec_host_free(void* p);
 const char* qfec_last_error(const qfec_ctx* ctx);
 int qfec_abi_version(void);
 

@@ -18,7 +18,12 @@
 //            through QuicFramer::ProcessRevivedPacket; the visitor reassembles
 //            the stream from received AND revived stream frames.
 // The stream must come out byte-identical with every dropped packet revived.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -124,9 +129,22 @@ class ReceiverVisitor : public QuicFramerVisitorInterface {
 
 #define SHIM_API extern "C" __attribute__((visibility("default")))
 
+namespace {
+// A crash inside the patched stack prints the native frames (addresses are
+// resolved offline with addr2line against this .so) before the default action.
+void crash_trace(int sig) {
+  void* f[64];
+  const int n = backtrace(f, 64);
+  backtrace_symbols_fd(f, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+}  // namespace
+
 SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int drop_every,
                          fec_e2e_result* r) {
   std::memset(r, 0, sizeof(*r));
+  signal(SIGSEGV, crash_trace);
   const QuicVersion v = static_cast<QuicVersion>(version);
   const QuicStreamId kStream = 5;
   // the stream: counter bytes

@@ -265,11 +265,89 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
   return collect_error(ctx, ctx->slots[0].stream);
 }
 
+// ---- QFEC_PTR_MAPPED: payloads in pinned host memory, read in place ---------
+// The kernels address the caller's pinned, device-mapped host buffers directly
+// (zero-copy over PCIe: tools/tune/tune_zero_copy.hip measures a kernel read of
+// pinned host rows at the H2D copy rate, 55-58 GB/s), so the packet bytes
+// cross the link exactly once and no host thread copies them.  Only the index
+// arrays are staged (10 B per packet + 12-23 B per group), chunked over the
+// context's slots so chunk c+1's tables are copied while chunk c runs.
+int check_mapped(qfec_ctx* ctx, const void* p, const char* what) {
+  if (!is_pinned_or_device(p))
+    return fail(ctx, QFEC_ERR_INTERNAL,
+                "QFEC_PTR_MAPPED: %s is not pinned host (qfec_host_alloc) or device memory", what);
+  return QFEC_OK;
+}
+
+int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const uint8_t* missing,
+                 uint32_t k, uint32_t L, uint64_t row_stride, uint64_t group_stride,
+                 uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
+  int rc = ensure_staging(ctx);
+  if (rc) return rc;
+  const bool recover = parity != nullptr;
+  if ((rc = check_mapped(ctx, rows, "rows")) || (rc = check_mapped(ctx, out, "out")) ||
+      (recover && (rc = check_mapped(ctx, parity, "parity"))))
+    return rc;
+  qfec::FixedArgs a{};
+  a.rows = rows;
+  a.parity = parity;
+  a.out = out;
+  a.row_stride = row_stride;
+  a.group_stride = group_stride;
+  a.parity_stride = parity_stride;
+  a.out_stride = out_stride;
+  a.k = k;
+  a.L = L;
+  a.err = ctx->d_err;
+  // the lost-slot indices are the only staged input (kStageBytes / 8 per chunk)
+  const uint64_t cg = recover ? kStageBytes / 8 : n;
+  uint64_t g0_of[kSlots] = {};
+  bool live[kSlots] = {};
+  int slot = 0;
+  for (uint64_t g0 = 0; g0 < n; g0 += cg, slot = (slot + 1) % kSlots) {
+    const uint64_t cnt = std::min(cg, n - g0);
+    Slot& s = ctx->slots[slot];
+    if (live[slot]) QFEC_HIP(ctx, hipEventSynchronize(s.done));  // h_aux free again
+    a.rows = rows + g0 * group_stride;
+    a.out = out + g0 * out_stride;
+    a.n_groups = cnt;
+    if (recover) {
+      a.parity = parity + g0 * parity_stride;
+      std::memcpy(s.h_aux, missing + g0, cnt);
+      QFEC_HIP(ctx, hipMemcpyAsync(s.d_aux, s.h_aux, cnt, hipMemcpyHostToDevice, s.stream));
+      a.missing = s.d_aux;
+    }
+    QFEC_HIP(ctx, qfec::launch_fixed(a, true, s.stream));
+    QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    g0_of[slot] = g0;
+    live[slot] = true;
+  }
+  for (int si = 0; si < kSlots; ++si)
+    if (live[si]) QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
+  (void)g0_of;
+  return collect_error(ctx, ctx->slots[0].stream);
+}
+
 }  // namespace
 
 extern "C" {
 
 int qfec_abi_version(void) { return QFEC_ABI_VERSION; }
+
+void* qfec_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  const hipError_t e =
+      hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) {
+    fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_alloc(%zu): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+void qfec_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
 
 const char* qfec_strerror(int code) {
   switch (code) {
@@ -426,6 +504,11 @@ int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, ui
     return rc;
   if (n_groups == 0) return QFEC_OK;
   if (!rows || !parity_out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if ((flags & QFEC_PTR_MAPPED) && (flags & QFEC_PTR_HOST))
+    return fail(ctx, QFEC_ERR_INTERNAL, "QFEC_PTR_MAPPED and QFEC_PTR_HOST are exclusive");
+  if (flags & QFEC_PTR_MAPPED)
+    return fixed_mapped(ctx, rows, nullptr, nullptr, k, L, row_stride, group_stride, 0, n_groups,
+                        parity_out, parity_stride);
   if (flags & QFEC_PTR_HOST)
     return fixed_host(ctx, rows, nullptr, nullptr, k, L, row_stride, group_stride, 0, n_groups,
                       parity_out, parity_stride);
@@ -460,12 +543,17 @@ int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t
     return rc;
   if (n_groups == 0) return QFEC_OK;
   if (!rows || !parity || !missing_idx || !out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
-  if (flags & QFEC_PTR_HOST) {
+  if ((flags & QFEC_PTR_MAPPED) && (flags & QFEC_PTR_HOST))
+    return fail(ctx, QFEC_ERR_INTERNAL, "QFEC_PTR_MAPPED and QFEC_PTR_HOST are exclusive");
+  if (flags & (QFEC_PTR_HOST | QFEC_PTR_MAPPED)) {
     for (uint64_t g = 0; g < n_groups; ++g)
       if (missing_idx[g] >= k)
         return fail(ctx, QFEC_ERR_INVALID_FEC_DATA,
                     "missing packet index %u >= FEC group size %u (group %llu)", missing_idx[g],
                     k, (unsigned long long)g);
+    if (flags & QFEC_PTR_MAPPED)
+      return fixed_mapped(ctx, rows, parity, missing_idx, k, L, row_stride, group_stride,
+                          parity_stride, n_groups, out, out_stride);
     return fixed_host(ctx, rows, parity, missing_idx, k, L, row_stride, group_stride,
                       parity_stride, n_groups, out, out_stride);
   }
@@ -541,15 +629,10 @@ struct RaggedLayout {  // byte offsets inside a slot's d_in / h_in (and d_out / 
   }
 };
 
-int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_t* pkt_off,
-                const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n,
-                const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
-                const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
-                uint8_t* out, const uint64_t* out_off) {
-  int rc = ensure_staging(ctx);
-  if (rc) return rc;
-  // Host-side validation of what the staging depends on (the same error
-  // words the kernel latches; the kernel re-checks everything else).
+// Host-side validation of a ragged batch whose tables are host memory (the
+// same error words the kernel latches; the kernel re-checks everything else).
+int validate_ragged(qfec_ctx* ctx, bool recover, const uint16_t* pkt_len, const uint32_t* grp_ptr,
+                    uint64_t n, const uint16_t* parity_len, const uint8_t* missing) {
   uint32_t bits = 0;
   for (uint64_t g = 0; g < n; ++g) {
     if (grp_ptr[g + 1] < grp_ptr[g] || grp_ptr[g + 1] - grp_ptr[g] > QFEC_MAX_GROUP_PACKETS ||
@@ -568,7 +651,17 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
         bits |= qfec::kErrPacketLength;
     }
   }
-  if (bits) return latch_error(ctx, bits);
+  return latch_error(ctx, bits);
+}
+
+int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_t* pkt_off,
+                const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n,
+                const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
+                const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
+                uint8_t* out, const uint64_t* out_off) {
+  int rc = ensure_staging(ctx);
+  if (rc) return rc;
+  if ((rc = validate_ragged(ctx, recover, pkt_len, grp_ptr, n, parity_len, missing))) return rc;
 
   const uint64_t in_cap = kStageBytes, out_cap = kStageBytes / 4;
   RaggedChunk chunk[kSlots];
@@ -696,6 +789,104 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
   return collect_error(ctx, ctx->slots[0].stream);
 }
 
+
+int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_t* pkt_off,
+                  const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n,
+                  const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
+                  const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
+                  uint8_t* out, const uint64_t* out_off) {
+  int rc = ensure_staging(ctx);
+  if (rc) return rc;
+  if ((rc = check_mapped(ctx, bytes, "bytes")) ||
+      (rc = check_mapped(ctx, recover ? out : parity_out, recover ? "out" : "parity_out")) ||
+      (recover && (rc = check_mapped(ctx, parity, "parity"))))
+    return rc;
+  if ((rc = validate_ragged(ctx, recover, pkt_len, grp_ptr, n, parity_len, missing))) return rc;
+  // per-chunk table layout in a slot's d_in / h_in (offsets in bytes)
+  struct Tab {
+    uint64_t off, len, ptr, poff, plen, miss, ooff, total;
+    Tab(uint64_t np, uint64_t ng, bool rec) {
+      off = 0;
+      len = off + np * 8;
+      ptr = align_up(len + np * 2, 8);
+      poff = align_up(ptr + (ng + 1) * 4, 8);
+      ooff = poff + ng * 8;
+      plen = ooff + (rec ? ng * 8 : 0);
+      miss = plen + (rec ? ng * 2 : 0);
+      total = miss + (rec ? ng : 0);
+    }
+  };
+  struct Pend {
+    uint64_t g0 = 0, cnt = 0;
+    bool live = false;
+  } pend[kSlots];
+  auto finish = [&](int si) -> int {
+    Pend& c = pend[si];
+    if (!c.live) return QFEC_OK;
+    QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
+    if (!recover)
+      std::memcpy(parity_len_out + c.g0, ctx->slots[si].h_out, c.cnt * sizeof(uint16_t));
+    c.live = false;
+    return QFEC_OK;
+  };
+  const uint64_t out_cap = (kStageBytes / 4) / sizeof(uint16_t);
+  int slot = 0;
+  uint64_t g = 0;
+  while (g < n) {
+    const uint64_t g0 = g;
+    for (; g < n; ++g) {  // whole groups while the tables fit
+      const Tab t(grp_ptr[g + 1] - grp_ptr[g0], g + 1 - g0, recover);
+      if (g > g0 && (t.total > kStageBytes || g + 1 - g0 > out_cap)) break;
+    }
+    const uint64_t cnt = g - g0, p0 = grp_ptr[g0], np = grp_ptr[g] - p0;
+    const Tab t(np, cnt, recover);
+    if ((rc = finish(slot))) return rc;
+    Slot& s = ctx->slots[slot];
+    uint8_t* h = s.h_in;
+    std::memcpy(h + t.off, pkt_off + p0, np * 8);  // payloads stay where they are
+    std::memcpy(h + t.len, pkt_len + p0, np * 2);
+    uint32_t* h_ptr = reinterpret_cast<uint32_t*>(h + t.ptr);
+    for (uint64_t i = 0; i <= cnt; ++i) h_ptr[i] = grp_ptr[g0 + i] - (uint32_t)p0;
+    std::memcpy(h + t.poff, parity_off + g0, cnt * 8);
+    if (recover) {
+      std::memcpy(h + t.ooff, out_off + g0, cnt * 8);
+      std::memcpy(h + t.plen, parity_len + g0, cnt * 2);
+      std::memcpy(h + t.miss, missing + g0, cnt);
+    }
+    QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, h, t.total, hipMemcpyHostToDevice, s.stream));
+    qfec::RaggedArgs a{};
+    a.bytes = bytes;
+    a.pkt_off = reinterpret_cast<const uint64_t*>(s.d_in + t.off);
+    a.pkt_len = reinterpret_cast<const uint16_t*>(s.d_in + t.len);
+    a.grp_ptr = reinterpret_cast<const uint32_t*>(s.d_in + t.ptr);
+    a.parity_off = reinterpret_cast<const uint64_t*>(s.d_in + t.poff);
+    a.n_groups = cnt;
+    a.err = ctx->d_err;
+    if (recover) {
+      a.parity = parity;
+      a.parity_len = reinterpret_cast<const uint16_t*>(s.d_in + t.plen);
+      a.missing = s.d_in + t.miss;
+      a.out_off = reinterpret_cast<const uint64_t*>(s.d_in + t.ooff);
+      a.out = out;
+    } else {
+      a.parity_len_out = reinterpret_cast<uint16_t*>(s.d_out);
+      a.out = parity_out;
+    }
+    QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+    if (!recover)
+      QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
+                                   hipMemcpyDeviceToHost, s.stream));
+    QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    pend[slot].g0 = g0;
+    pend[slot].cnt = cnt;
+    pend[slot].live = true;
+    slot = (slot + 1) % kSlots;
+  }
+  for (int i = 0; i < kSlots; ++i)
+    if ((rc = finish((slot + i) % kSlots))) return rc;
+  return collect_error(ctx, ctx->slots[0].stream);
+}
+
 }  // namespace
 
 int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
@@ -707,6 +898,12 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
   if (n_groups == 0) return QFEC_OK;
   if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity_out || !parity_off || !parity_len_out)
     return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if ((flags & QFEC_PTR_MAPPED) && (flags & QFEC_PTR_HOST))
+    return fail(ctx, QFEC_ERR_INTERNAL, "QFEC_PTR_MAPPED and QFEC_PTR_HOST are exclusive");
+  if (flags & QFEC_PTR_MAPPED)
+    return ragged_mapped(ctx, false, bytes, pkt_off, pkt_len, grp_ptr, n_groups, nullptr,
+                         parity_out, parity_off, nullptr, parity_len_out, nullptr, nullptr,
+                         nullptr);
   if (flags & QFEC_PTR_HOST)
     return ragged_host(ctx, false, bytes, pkt_off, pkt_len, grp_ptr, n_groups, nullptr,
                        parity_out, parity_off, nullptr, parity_len_out, nullptr, nullptr,
@@ -736,7 +933,9 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
   if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity || !parity_off || !parity_len ||
       !missing_idx || !out || !out_off)
     return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
-  if (flags & QFEC_PTR_HOST) {
+  if ((flags & QFEC_PTR_MAPPED) && (flags & QFEC_PTR_HOST))
+    return fail(ctx, QFEC_ERR_INTERNAL, "QFEC_PTR_MAPPED and QFEC_PTR_HOST are exclusive");
+  if (flags & (QFEC_PTR_HOST | QFEC_PTR_MAPPED)) {
     for (uint64_t g = 0; g < n_groups; ++g) {
       const uint32_t k = grp_ptr[g + 1] - grp_ptr[g];
       if (grp_ptr[g + 1] < grp_ptr[g] || k == 0 || k > QFEC_MAX_GROUP_PACKETS)
@@ -749,6 +948,9 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
         return fail(ctx, QFEC_ERR_INVALID_FEC_DATA, "Illegal FEC redundancy length %u",
                     parity_len[g]);
     }
+    if (flags & QFEC_PTR_MAPPED)
+      return ragged_mapped(ctx, true, bytes, pkt_off, pkt_len, grp_ptr, n_groups, parity,
+                           nullptr, parity_off, parity_len, nullptr, missing_idx, out, out_off);
     return ragged_host(ctx, true, bytes, pkt_off, pkt_len, grp_ptr, n_groups, parity, nullptr,
                        parity_off, parity_len, nullptr, missing_idx, out, out_off);
   }
@@ -774,6 +976,14 @@ int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, ui
   if (rc) return rc;
   if (n == 0) return QFEC_OK;
   if (!in || !out) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if ((flags & QFEC_PTR_MAPPED) && (flags & QFEC_PTR_HOST))
+    return fail(ctx, QFEC_ERR_INTERNAL, "QFEC_PTR_MAPPED and QFEC_PTR_HOST are exclusive");
+  if (flags & QFEC_PTR_MAPPED) {
+    if ((rc = check_mapped(ctx, in, "in")) || (rc = check_mapped(ctx, out, "out"))) return rc;
+    QFEC_HIP(ctx, qfec::launch_xor_into(in, n, out, ctx->stream));
+    QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return QFEC_OK;
+  }
   if (flags & QFEC_PTR_HOST) {
     DevBuf d_in, d_out;
     QFEC_HIP(ctx, hipMalloc(&d_in.p, n));

@@ -90,15 +90,16 @@ int QuicFecEncodeBatch::Flush(qfec_ctx* ctx) {
   for (Entry& e : entries_) groups.push_back(e.group.get());
   const int rc = QuicFecGroup::ComputeAll(ctx, groups);  // one launch
   if (rc != QFEC_OK) return rc;
-  for (Entry& e : entries_) {
-    const StringPiece red = e.group->PayloadParity();
-    e.fec_packet_body.resize(2 + red.size());
-    const size_t n = SerializeFecPacketBody(e.fec_packet_number, e.fec_group, e.entropy_flag, red,
-                                            e.fec_packet_body.data(), e.fec_packet_body.size());
-    if (n == 0) return QFEC_ERR_INVALID_FEC_DATA;
-    e.fec_packet_body.resize(n);
-  }
+  for (Entry& e : entries_) e.redundancy = e.group->PayloadParity();
   return QFEC_OK;
+}
+
+std::vector<uint8_t> QuicFecEncodeBatch::Entry::FecPacketBody() const {
+  std::vector<uint8_t> body(2 + redundancy.size());
+  const size_t n = SerializeFecPacketBody(fec_packet_number, fec_group, entropy_flag, redundancy,
+                                          body.data(), body.size());
+  body.resize(n);
+  return body;
 }
 
 // ---------------------------------------------------------------------------
@@ -195,20 +196,20 @@ void QuicFecReviveBatch::Add(void* tag, std::unique_ptr<QuicFecGroup> group) {
 }
 
 int QuicFecReviveBatch::Flush(qfec_ctx* ctx, std::vector<Revived>* revived) {
+  flushed_.clear();  // the previous Flush's payload views end here
   std::vector<QuicFecGroup*> gs;
   gs.reserve(groups_.size());
   for (auto& g : groups_) gs.push_back(g.second.get());
   const int rc = QuicFecGroup::ComputeAll(ctx, gs);  // one launch
   if (rc != QFEC_OK) return rc;
-  char buf[kMaxPacketSize];
+  if (revived) revived->reserve(revived->size() + groups_.size());
   for (auto& g : groups_) {
     Revived r;
     r.tag = g.first;
-    const size_t n = g.second->Revive(&r.header, buf, sizeof(buf));
-    if (n == 0) continue;  // cannot happen for a CanRevive() group
-    r.payload.assign(buf, n);
-    if (revived) revived->push_back(std::move(r));
+    if (g.second->ReviveInPlace(&r.header, &r.payload) == 0) continue;  // not for CanRevive() groups
+    if (revived) revived->push_back(r);
   }
+  flushed_.swap(groups_);
   groups_.clear();
   return QFEC_OK;
 }

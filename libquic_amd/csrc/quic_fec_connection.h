@@ -109,12 +109,18 @@ class QuicFecEncodeBatch {
     QuicFecGroupNumber fec_group = 0;
     bool entropy_flag = false;
     std::unique_ptr<QuicFecGroup> group;
-    std::vector<uint8_t> fec_packet_body;  // private header + redundancy (after Flush)
+    // After Flush: the FEC packet's redundancy, a view of the group's
+    // accumulator (payload arena memory the kernel wrote in place), valid
+    // while the entry lives.  QuicFramer::BuildFecPacket writes the header.
+    StringPiece redundancy;
+    // The v<=31 FEC packet body: private header + redundancy
+    // (SerializeFecPacketBody); empty before Flush.
+    std::vector<uint8_t> FecPacketBody() const;
   };
 
-  // ONE ragged encode launch for every entry (QuicFecGroup::ComputeAll), then
-  // each entry's FEC packet body (SerializeFecPacketBody).  Returns a qfec_*
-  // code; on failure no body is filled.
+  // ONE ragged encode launch for every entry (QuicFecGroup::ComputeAll); then
+  // every entry's redundancy is set.  Returns a qfec_* code; on failure no
+  // redundancy is set.
   int Flush(qfec_ctx* ctx);
   std::vector<Entry>& entries() { return entries_; }
   size_t size() const { return entries_.size(); }
@@ -172,17 +178,23 @@ class QuicFecReviveBatch {
   struct Revived {
     void* tag = nullptr;
     QuicPacketHeader header;  // packet_number of the lost packet, fec_group set
-    std::string payload;      // redundancy length, zero padded (PADDING frames)
+    // redundancy length, zero padded (PADDING frames): a view of the group's
+    // accumulator, valid until this batch's next Flush / Clear / destruction
+    StringPiece payload;
   };
 
   void Add(void* tag, std::unique_ptr<QuicFecGroup> group);
   size_t size() const { return groups_.size(); }
   // ONE ragged launch for every collected group, then each group's revived
-  // packet, in collection order.  Returns a qfec_* code.
+  // packet, in collection order.  The revived groups are kept (their
+  // accumulators back the payload views) until the next Flush or Clear.
+  // Returns a qfec_* code.
   int Flush(qfec_ctx* ctx, std::vector<Revived>* revived);
+  void Clear() { flushed_.clear(); }
 
  private:
   std::vector<std::pair<void*, std::unique_ptr<QuicFecGroup>>> groups_;
+  std::vector<std::pair<void*, std::unique_ptr<QuicFecGroup>>> flushed_;
 };
 
 }  // namespace net

@@ -7,11 +7,76 @@
 #include "quic_fec_group.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
 namespace net {
 namespace {
+
+// Per-thread bump allocator over slabs of pinned, device-mapped host memory
+// (heap slabs when no device is present).  Slabs live for the process and
+// are reused once everything allocated in them has been released.
+struct ArenaSlab {
+  uint8_t* base = nullptr;
+  size_t used = 0;
+  std::atomic<size_t> live{0};  // bytes handed out and not yet released
+  bool mapped = false;
+};
+
+class PayloadArena {
+ public:
+  static constexpr size_t kSlabBytes = 32u << 20;
+
+  static PayloadArena& ForThread() {
+    static thread_local PayloadArena a;
+    return a;
+  }
+
+  // n <= kSlabBytes; returns 16-byte aligned storage.
+  uint8_t* Alloc(size_t n, ArenaSlab** slab) {
+    n = (n + 15) & ~size_t(15);
+    if (!cur_ || cur_->used + n > kSlabBytes) cur_ = NextSlab();
+    if (!cur_) return nullptr;
+    uint8_t* p = cur_->base + cur_->used;
+    cur_->used += n;
+    cur_->live.fetch_add(n, std::memory_order_relaxed);
+    *slab = cur_;
+    return p;
+  }
+
+  static void Release(ArenaSlab* slab, size_t n) {
+    slab->live.fetch_sub((n + 15) & ~size_t(15), std::memory_order_acq_rel);
+  }
+
+ private:
+  ArenaSlab* NextSlab() {
+    for (ArenaSlab* s : slabs_) {
+      if (s != cur_ && s->live.load(std::memory_order_acquire) == 0) {
+        s->used = 0;
+        return s;
+      }
+    }
+    ArenaSlab* s = new ArenaSlab();
+    if (mapped_ok_) {
+      s->base = static_cast<uint8_t*>(qfec_host_alloc(kSlabBytes));
+      s->mapped = s->base != nullptr;
+      mapped_ok_ = s->mapped;  // no device: stop asking
+    }
+    if (!s->base) s->base = static_cast<uint8_t*>(std::malloc(kSlabBytes));
+    if (!s->base) {
+      delete s;
+      return nullptr;
+    }
+    slabs_.push_back(s);
+    return s;
+  }
+
+  std::vector<ArenaSlab*> slabs_;  // process lifetime (outstanding payloads may outlive the thread)
+  ArenaSlab* cur_ = nullptr;
+  bool mapped_ok_ = true;
+};
 
 struct ThreadCtx {
   qfec_ctx* ctx = nullptr;
@@ -31,7 +96,26 @@ qfec_ctx* thread_default_ctx() {
 QuicFecGroup::QuicFecGroup(QuicFecGroupNumber fec_group_number, qfec_ctx* ctx)
     : fec_group_number_(fec_group_number), ctx_(ctx) {}
 
-QuicFecGroup::~QuicFecGroup() = default;
+QuicFecGroup::~QuicFecGroup() {
+  for (Span& sp : payloads_) ArenaFree(&sp);
+  ArenaFree(&parity_);
+}
+
+QuicFecGroup::Span QuicFecGroup::ArenaAlloc(size_t n) {
+  Span sp;
+  ArenaSlab* slab = nullptr;
+  sp.p = PayloadArena::ForThread().Alloc(n, &slab);
+  if (sp.p) {
+    sp.slab = slab;
+    sp.n = n;
+  }
+  return sp;
+}
+
+void QuicFecGroup::ArenaFree(Span* sp) {
+  if (sp->p) PayloadArena::Release(static_cast<ArenaSlab*>(sp->slab), sp->n);
+  *sp = Span();
+}
 
 qfec_ctx* QuicFecGroup::context() const { return ctx_ ? ctx_ : thread_default_ctx(); }
 
@@ -52,15 +136,36 @@ bool QuicFecGroup::Fold(StringPiece payload, bool completes_group) {
     detailed_error_ = "FEC group holds more than 255 payloads";
     return false;
   }
-  bytes_.insert(bytes_.end(), payload.data(), payload.data() + payload.size());
+  Span sp = ArenaAlloc(payload.size());
+  if (!sp.p) {
+    detailed_error_ = "out of payload memory";
+    return false;
+  }
+  std::memcpy(sp.p, payload.data(), payload.size());
+  payloads_.push_back(sp);
   lens_.push_back(static_cast<uint16_t>(payload.size()));
   dirty_ = true;
   return true;
 }
 
+bool QuicFecGroup::HasReceived(QuicPacketNumber n) const {
+  const QuicPacketNumber d = n - fec_group_number_;
+  if (n >= fec_group_number_ && d < 256) return (recv_bits_[d >> 6] >> (d & 63)) & 1;
+  return recv_other_.count(n) != 0;
+}
+
+void QuicFecGroup::MarkReceived(QuicPacketNumber n) {
+  const QuicPacketNumber d = n - fec_group_number_;
+  if (n >= fec_group_number_ && d < 256)
+    recv_bits_[d >> 6] |= 1ull << (d & 63);
+  else
+    recv_other_.insert(n);
+  ++num_received_;
+}
+
 bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                           StringPiece decrypted_payload) {
-  if (received_packets_.count(header.packet_number) != 0) return false;
+  if (HasReceived(header.packet_number)) return false;
   if (min_protected_packet_ != kInvalidPacketNumber &&
       max_protected_packet_ != kInvalidPacketNumber &&
       (header.packet_number < min_protected_packet_ ||
@@ -70,10 +175,10 @@ bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHead
     return false;
   }
   const bool completes = min_protected_packet_ != kInvalidPacketNumber &&
-                         received_packets_.size() + 1 ==
+                         num_received_ + 1 ==
                              max_protected_packet_ - min_protected_packet_ + 1;
   if (!Fold(decrypted_payload, completes)) return false;
-  received_packets_.insert(header.packet_number);
+  MarkReceived(header.packet_number);
   if (encryption_level < effective_encryption_level_)
     effective_encryption_level_ = encryption_level;
   return true;
@@ -88,13 +193,20 @@ bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketH
     detailed_error_ = "FEC packet number outside the group's uint8 offset range";
     return false;
   }
-  for (QuicPacketNumber p : received_packets_) {
-    if (p < fec_group_number_ || p >= fec_packet_number) {
-      detailed_error_ = "FEC group does not cover received packet: " + std::to_string(p);
-      return false;
-    }
+  // every received packet must lie in [fec_group_number_, fec_packet_number)
+  QuicPacketNumber outside = kInvalidPacketNumber;
+  if (!recv_other_.empty()) outside = *recv_other_.begin();
+  const uint64_t span = fec_packet_number - fec_group_number_;  // 1..255
+  for (uint64_t w = span >> 6; w < 4 && outside == kInvalidPacketNumber; ++w) {
+    const uint64_t lo = w == (span >> 6) ? (span & 63) : 0;
+    const uint64_t bits = lo == 64 ? 0 : recv_bits_[w] & (~0ull << lo);
+    if (bits) outside = fec_group_number_ + 64 * w + __builtin_ctzll(bits);
   }
-  const bool completes = received_packets_.size() == fec_packet_number - fec_group_number_;
+  if (outside != kInvalidPacketNumber) {
+    detailed_error_ = "FEC group does not cover received packet: " + std::to_string(outside);
+    return false;
+  }
+  const bool completes = num_received_ == span;
   if (!Fold(redundancy, completes)) return false;
   min_protected_packet_ = fec_group_number_;
   max_protected_packet_ = fec_packet_number - 1;
@@ -106,7 +218,7 @@ bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketH
 QuicPacketCount QuicFecGroup::NumMissingPackets() const {
   if (min_protected_packet_ == kInvalidPacketNumber)
     return std::numeric_limits<QuicPacketCount>::max();
-  return (max_protected_packet_ - min_protected_packet_ + 1) - received_packets_.size();
+  return (max_protected_packet_ - min_protected_packet_ + 1) - num_received_;
 }
 
 bool QuicFecGroup::CanRevive() const { return NumMissingPackets() == 1; }
@@ -133,32 +245,41 @@ StringPiece QuicFecGroup::PayloadParity() const {
     return StringPiece();
   }
   if (EnsureParity() != QFEC_OK) return StringPiece();
-  return StringPiece(reinterpret_cast<const char*>(parity_.data()), payload_parity_len_);
+  return StringPiece(reinterpret_cast<const char*>(parity_.p), payload_parity_len_);
 }
 
-size_t QuicFecGroup::Revive(QuicPacketHeader* header, char* decrypted_payload, size_t len) {
+size_t QuicFecGroup::ReviveInPlace(QuicPacketHeader* header, StringPiece* payload) {
   if (!CanRevive()) return 0;
   QuicPacketNumber missing = kInvalidPacketNumber;
   for (QuicPacketNumber i = min_protected_packet_; i <= max_protected_packet_; ++i) {
-    if (received_packets_.count(i) == 0) {
+    if (!HasReceived(i)) {
       missing = i;
       break;
     }
   }
   if (missing == kInvalidPacketNumber) return 0;
   if (EnsureParity() != QFEC_OK) return 0;
-  if (payload_parity_len_ > len) {
-    detailed_error_ = "revive buffer smaller than the redundancy";
-    return 0;
-  }
-  std::memcpy(decrypted_payload, parity_.data(), payload_parity_len_);
+  *payload = StringPiece(reinterpret_cast<const char*>(parity_.p), payload_parity_len_);
   header->packet_number = missing;
   header->entropy_flag = false;  // unknown entropy
   header->fec_flag = false;
   header->is_in_fec_group = IN_FEC_GROUP;
   header->fec_group = fec_group_number_;
-  received_packets_.insert(missing);
+  MarkReceived(missing);
   return payload_parity_len_;
+}
+
+size_t QuicFecGroup::Revive(QuicPacketHeader* header, char* decrypted_payload, size_t len) {
+  if (!CanRevive()) return 0;
+  if (EnsureParity() != QFEC_OK) return 0;
+  if (payload_parity_len_ > len) {
+    detailed_error_ = "revive buffer smaller than the redundancy";
+    return 0;
+  }
+  StringPiece view;
+  const size_t n = ReviveInPlace(header, &view);
+  if (n) std::memcpy(decrypted_payload, view.data(), n);
+  return n;
 }
 
 int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups) {
@@ -173,51 +294,64 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   }
   // Ragged CSR over every folded payload of every group, addressed IN PLACE:
   // the C-ABI takes one base pointer plus 64-bit offsets, so the base is the
-  // lowest of the groups' payload buffers and each packet's offset is its
-  // distance from it (likewise for the parity accumulators).  The host path
-  // of qfec_encode_ragged gathers straight from the groups into its pinned
-  // staging — no intermediate copy here.
+  // lowest payload address and each packet's offset is its distance from it
+  // (likewise for the accumulators).  When every payload and accumulator sits
+  // in a mapped arena slab the kernel reads and writes them where they are
+  // (QFEC_PTR_MAPPED); otherwise the host path gathers them into the
+  // context's pinned staging (QFEC_PTR_HOST).
   size_t npk = 0;
   std::vector<QuicFecGroup*> launched;
   launched.reserve(work.size());
   uintptr_t in_base = UINTPTR_MAX, out_base = UINTPTR_MAX;
+  bool mapped = true;
   for (QuicFecGroup* g : work) {
     if (g->lens_.empty()) {  // only empty payloads folded: parity is empty
       g->payload_parity_len_ = 0;
-      g->parity_.clear();
       g->dirty_ = false;
       continue;
     }
-    g->parity_.resize(kMaxPacketSize);
-    in_base = std::min(in_base, reinterpret_cast<uintptr_t>(g->bytes_.data()));
-    out_base = std::min(out_base, reinterpret_cast<uintptr_t>(g->parity_.data()));
+    if (!g->parity_.p) {
+      g->parity_ = ArenaAlloc(kMaxPacketSize);
+      if (!g->parity_.p) {
+        g->detailed_error_ = "out of payload memory";
+        return QFEC_ERR_INTERNAL;
+      }
+    }
+    mapped = mapped && static_cast<ArenaSlab*>(g->parity_.slab)->mapped;
+    out_base = std::min(out_base, reinterpret_cast<uintptr_t>(g->parity_.p));
+    for (const Span& sp : g->payloads_) {
+      in_base = std::min(in_base, reinterpret_cast<uintptr_t>(sp.p));
+      mapped = mapped && static_cast<ArenaSlab*>(sp.slab)->mapped;
+    }
     npk += g->lens_.size();
     launched.push_back(g);
   }
   if (launched.empty()) return QFEC_OK;
-  std::vector<uint64_t> pkt_off;
+  // index tables: per-thread buffers that keep their capacity between flushes
+  static thread_local std::vector<uint64_t> pkt_off, parity_off;
+  static thread_local std::vector<uint16_t> pkt_len, plen;
+  static thread_local std::vector<uint32_t> grp_ptr;
+  pkt_off.clear();
   pkt_off.reserve(npk);
-  std::vector<uint16_t> pkt_len;
+  pkt_len.clear();
   pkt_len.reserve(npk);
-  std::vector<uint32_t> grp_ptr(1, 0);
+  grp_ptr.assign(1, 0);
   grp_ptr.reserve(launched.size() + 1);
-  std::vector<uint64_t> parity_off;
+  parity_off.clear();
   parity_off.reserve(launched.size());
   for (QuicFecGroup* g : launched) {
-    uint64_t o = reinterpret_cast<uintptr_t>(g->bytes_.data()) - in_base;
-    for (uint16_t l : g->lens_) {
-      pkt_off.push_back(o);
-      pkt_len.push_back(l);
-      o += l;
+    for (size_t i = 0; i < g->payloads_.size(); ++i) {
+      pkt_off.push_back(reinterpret_cast<uintptr_t>(g->payloads_[i].p) - in_base);
+      pkt_len.push_back(g->lens_[i]);
     }
     grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));
-    parity_off.push_back(reinterpret_cast<uintptr_t>(g->parity_.data()) - out_base);
+    parity_off.push_back(reinterpret_cast<uintptr_t>(g->parity_.p) - out_base);
   }
-  std::vector<uint16_t> plen(launched.size(), 0);
+  plen.assign(launched.size(), 0);
   int rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
                               pkt_len.data(), grp_ptr.data(), launched.size(),
                               reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
-                              plen.data(), QFEC_PTR_HOST);
+                              plen.data(), mapped ? QFEC_PTR_MAPPED : QFEC_PTR_HOST);
   if (rc != QFEC_OK) {
     for (QuicFecGroup* g : launched) g->detailed_error_ = qfec_last_error(ctx);
     return rc;
@@ -225,7 +359,6 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   for (size_t i = 0; i < launched.size(); ++i) {
     QuicFecGroup* g = launched[i];
     g->payload_parity_len_ = plen[i];
-    g->parity_.resize(plen[i]);
     g->dirty_ = false;
   }
   return QFEC_OK;

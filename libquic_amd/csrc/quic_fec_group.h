@@ -22,6 +22,14 @@
 // in ONE ragged kernel launch via QuicFecGroup::ComputeAll().  Results are
 // byte-identical; there is no CPU fallback — without a
 // device the group reports failure.
+//
+// Where the payloads live: a per-thread arena of pinned, device-mapped host
+// slabs (qfec_host_alloc), so ComputeAll hands the kernel the packets where
+// Update() put them (QFEC_PTR_MAPPED: read in place over PCIe, no gather, no
+// staging copy); the accumulators are written back into the same arena.  A
+// slab is reused once every payload in it has been released.  Without mapped
+// memory (no device) the arena falls back to ordinary heap slabs and
+// ComputeAll stages through the context (QFEC_PTR_HOST).
 #pragma once
 
 #include <stddef.h>
@@ -113,12 +121,16 @@ class QuicFecGroup {
   // Writes the missing packet (zero padded to the redundancy length) and
   // returns its length; 0 if it cannot be revived or `len` is too small.
   size_t Revive(QuicPacketHeader* header, char* decrypted_payload, size_t len);
+  // Revive without a copy: *payload views the group's accumulator, valid while
+  // the group lives and takes no further packets.  Same header and return
+  // value as Revive().
+  size_t ReviveInPlace(QuicPacketHeader* header, StringPiece* payload);
   // True if this group protects packets with numbers below `num`.
   bool IsWaitingForPacketBefore(QuicPacketNumber num) const;
   // XOR of every payload folded in so far (data and redundancy), zero padded;
   // on the send side this is the FEC packet's redundancy.  Computed on the GPU.
   StringPiece PayloadParity() const;
-  QuicPacketCount NumReceivedPackets() const { return received_packets_.size(); }
+  QuicPacketCount NumReceivedPackets() const { return num_received_; }
   EncryptionLevel EffectiveEncryptionLevel() const { return effective_encryption_level_; }
   QuicFecGroupNumber FecGroupNumber() const { return fec_group_number_; }
 
@@ -138,15 +150,30 @@ class QuicFecGroup {
 
   QuicFecGroupNumber fec_group_number_;
   qfec_ctx* ctx_;
-  std::set<QuicPacketNumber> received_packets_;
+  // Received packet numbers: the 256 a group can span (uint8 offset from
+  // fec_group_number_) as a bitmap; any other (only a malformed peer sends
+  // one, refused later by UpdateFec as the historical class did) in a set.
+  bool HasReceived(QuicPacketNumber n) const;
+  void MarkReceived(QuicPacketNumber n);
+  uint64_t recv_bits_[4] = {0, 0, 0, 0};
+  std::set<QuicPacketNumber> recv_other_;
+  size_t num_received_ = 0;
   QuicPacketNumber min_protected_packet_ = kInvalidPacketNumber;
   QuicPacketNumber max_protected_packet_ = kInvalidPacketNumber;
   EncryptionLevel effective_encryption_level_ = NUM_ENCRYPTION_LEVELS;
-  // Folded payloads, packed, with their lengths (data packets and redundancy).
-  std::vector<uint8_t> bytes_;
+  // Folded payloads (data packets and redundancy) in the payload arena, with
+  // their lengths; the GPU-computed accumulator (kMaxPacketSize bytes of arena,
+  // valid when !dirty_).
+  struct Span {
+    uint8_t* p = nullptr;
+    void* slab = nullptr;  // the arena slab holding p (released on destruction)
+    size_t n = 0;
+  };
+  static Span ArenaAlloc(size_t n);
+  static void ArenaFree(Span* s);
+  std::vector<Span> payloads_;
   std::vector<uint16_t> lens_;
-  // GPU-computed accumulator (valid when !dirty_).
-  mutable std::vector<uint8_t> parity_;
+  mutable Span parity_;
   mutable size_t payload_parity_len_ = 0;
   mutable bool dirty_ = false;
   bool unkept_payload_ = false;  // a 256th payload completed the group (Fold)

@@ -6,7 +6,9 @@ it never computes FEC bytes itself and has no CPU fallback: if the library or
 the GPU is missing, every call raises.
 
 Buffers may be torch tensors (device or pinned host) or numpy arrays (host);
-the caller picks ``host=True`` for host pointers (QFEC_PTR_HOST).
+the caller picks ``host=True`` for host pointers (QFEC_PTR_HOST), or
+``mapped=True`` for payloads in pinned host memory the kernels read in place
+(QFEC_PTR_MAPPED; torch ``pin_memory()`` tensors or ``HostBuffer``).
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ QFEC_ERR_INVALID_FEC_DATA = -5
 QFEC_PTR_DEVICE = 0
 QFEC_PTR_HOST = 1
 QFEC_CACHED = 2
+QFEC_PTR_MAPPED = 4
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
 MAX_GROUP_PACKETS = 255
@@ -38,6 +41,8 @@ SIGNATURES = [
     ("qfec_sync", C.c_int, [C.c_void_p]),
     ("qfec_strerror", C.c_char_p, [C.c_int]),
     ("qfec_last_error", C.c_char_p, [C.c_void_p]),
+    ("qfec_host_alloc", C.c_void_p, [C.c_size_t]),
+    ("qfec_host_free", None, [C.c_void_p]),
     ("qfec_encode_batch", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint32]),
     ("qfec_recover_batch", C.c_int,
@@ -117,6 +122,37 @@ def load(path: str = LIB_PATH):
     return _lib
 
 
+def _fl(host=False, mapped=False, cached=False):
+    return ((QFEC_PTR_HOST if host else 0) | (QFEC_PTR_MAPPED if mapped else 0)
+            | (QFEC_CACHED if cached else 0))
+
+
+class HostBuffer:
+    """n bytes of pinned, device-mapped host memory from qfec_host_alloc, as a
+    numpy uint8 view (.array); freed with close()."""
+
+    def __init__(self, n: int):
+        import numpy as np
+        self.lib = load()
+        self.ptr = self.lib.qfec_host_alloc(n)
+        if not self.ptr:
+            raise QfecError(QFEC_ERR_INTERNAL, self.lib.qfec_last_error(None).decode())
+        self.n = n
+        self.array = np.ctypeslib.as_array((C.c_uint8 * n).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self.lib.qfec_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _ptr(x):
     """Address of a torch tensor / numpy array / int / None."""
     if x is None:
@@ -182,8 +218,8 @@ class Context:
 
     # -- fixed -------------------------------------------------------------
     def encode(self, rows, k, L, n_groups, parity_out, *, row_stride=None, group_stride=None,
-               parity_stride=None, host=False, cached=False):
-        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_CACHED if cached else 0)
+               parity_stride=None, host=False, cached=False, mapped=False):
+        fl = _fl(host, mapped, cached)
         if row_stride is None and group_stride is None and parity_stride is None:
             rc = self.lib.qfec_encode_batch(self.ctx, _ptr(rows), k, L, n_groups,
                                             _ptr(parity_out), fl)
@@ -197,8 +233,8 @@ class Context:
 
     def recover(self, rows, parity, missing, k, L, n_groups, out, *, row_stride=None,
                 group_stride=None, parity_stride=None, out_stride=None, host=False,
-                cached=False):
-        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_CACHED if cached else 0)
+                cached=False, mapped=False):
+        fl = _fl(host, mapped, cached)
         if row_stride is None and group_stride is None and parity_stride is None \
                 and out_stride is None:
             rc = self.lib.qfec_recover_batch(self.ctx, _ptr(rows), _ptr(parity), _ptr(missing),
@@ -215,25 +251,24 @@ class Context:
 
     # -- ragged ------------------------------------------------------------
     def encode_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity_out, parity_off,
-                      parity_len_out, *, host=False):
+                      parity_len_out, *, host=False, mapped=False):
         rc = self.lib.qfec_encode_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                          _ptr(grp_ptr), n_groups, _ptr(parity_out),
                                          _ptr(parity_off), _ptr(parity_len_out),
-                                         QFEC_PTR_HOST if host else 0)
+                                         _fl(host, mapped))
         return self._check(rc)
 
     def recover_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity, parity_off,
-                       parity_len, missing, out, out_off, *, host=False):
+                       parity_len, missing, out, out_off, *, host=False, mapped=False):
         rc = self.lib.qfec_recover_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                           _ptr(grp_ptr), n_groups, _ptr(parity),
                                           _ptr(parity_off), _ptr(parity_len), _ptr(missing),
-                                          _ptr(out), _ptr(out_off),
-                                          QFEC_PTR_HOST if host else 0)
+                                          _ptr(out), _ptr(out_off), _fl(host, mapped))
         return self._check(rc)
 
-    def xor_into(self, src, n, dst, *, host=False):
+    def xor_into(self, src, n, dst, *, host=False, mapped=False):
         return self._check(self.lib.qfec_xor_into(self.ctx, _ptr(src), n, _ptr(dst),
-                                                  QFEC_PTR_HOST if host else 0))
+                                                  _fl(host, mapped)))
 
     # -- packet protection (ENCRYPTION_NONE) --------------------------------
     def null_encrypt(self, data, ad_off, ad_len, in_off, in_len, n, out, out_off, *, host=False):

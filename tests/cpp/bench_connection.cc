@@ -5,9 +5,11 @@
 // one FEC group of 10 data packets x 1350 B (QuicFecSender -> one shared
 // QuicFecEncodeBatch), or each have one group with exactly one lost packet and
 // the FEC packet received (QuicFecReceiver -> one shared QuicFecReviveBatch).
-// Timed: ONE Flush of the batch — CSR build, the host path's gather into
-// pinned staging, H2D, one ragged launch, D2H, scatter, FEC packet body
-// serialisation / revived packet copies — for N = 1, 64, 4096, 65536 groups.
+// Timed: ONE Flush of the batch — CSR build, index tables staged to the
+// device, one ragged launch reading the payloads in place from the groups'
+// pinned payload arena (QFEC_PTR_MAPPED) and writing the accumulators back
+// into it, the redundancy / revived-payload views — for N = 1, 64, 4096,
+// 65536 groups.
 // Beside it the CPU FEC path the reference ran on the connection thread:
 // every payload XORed into the group accumulator (the oracle's
 // qo_group_encode / qo_group_recover, word-wise XorBuffers), one core.
@@ -88,8 +90,8 @@ int main(int argc, char** argv) {
       if (r > 0) t_enc.push_back(us);
       if (r == 1) {
         for (size_t g = 0; g < N; ++g) {
-          const auto& body = batch.entries()[g].fec_packet_body;
-          ok &= body.size() == 2 + L && std::memcmp(body.data() + 2, red[g].data(), L) == 0;
+          const StringPiece rd = batch.entries()[g].redundancy;
+          ok &= rd.size() == L && std::memcmp(rd.data(), red[g].data(), L) == 0;
         }
       }
     }
@@ -130,7 +132,8 @@ int main(int argc, char** argv) {
           const size_t g = reinterpret_cast<size_t>(rv.tag);
           const int lost = static_cast<int>(g % k);
           ok &= rv.header.packet_number == static_cast<QuicPacketNumber>(1 + lost) &&
-                rv.payload == pays[g * k + lost];
+                rv.payload.size() == L &&
+                std::memcmp(rv.payload.data(), pays[g * k + lost].data(), L) == 0;
         }
       }
     }

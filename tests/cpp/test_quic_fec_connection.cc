@@ -250,10 +250,11 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
       batched_groups += enc.size();
       for (auto& e : enc.entries()) {
         const int c = static_cast<int>(reinterpret_cast<intptr_t>(e.tag));
+        const std::vector<uint8_t> body = e.FecPacketBody();
         // the body parses back: FEC | FEC_GROUP, offset to the group's first packet
         FecHeaderFields pf;
         std::string err;
-        EXPECT(ParseFecPrivateHeader(e.fec_packet_body.data(), e.fec_packet_body.size(),
+        EXPECT(ParseFecPrivateHeader(body.data(), body.size(),
                                      kQuicVersion31, e.fec_packet_number, &pf, &err) == 2);
         EXPECT(pf.fec_flag && pf.in_fec_group &&
                e.fec_packet_number - pf.fec_group_offset == e.fec_group);
@@ -267,9 +268,9 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
         }
         std::vector<uint8_t> want(kMaxPacketSize);
         const int wl = qo_group_encode(ptr.data(), len.data(), ptr.size(), want.data());
-        EXPECT(wl == static_cast<int>(e.fec_packet_body.size()) - 2);
-        EXPECT(std::memcmp(want.data(), e.fec_packet_body.data() + 2, wl) == 0);
-        wire.push_back(Wire{c, e.fec_packet_number, e.fec_packet_body});
+        EXPECT(wl == static_cast<int>(body.size()) - 2);
+        EXPECT(std::memcmp(want.data(), body.data() + 2, wl) == 0);
+        wire.push_back(Wire{c, e.fec_packet_number, body});
       }
     }
     // lossy, reordering network
@@ -331,7 +332,7 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
     const std::string& p = payloads[{c, r.header.packet_number}];
     // revived payload = original, zero padded to the redundancy length
     bool ok = r.payload.size() >= p.size() && std::memcmp(r.payload.data(), p.data(), p.size()) == 0;
-    for (size_t i = p.size(); ok && i < r.payload.size(); ++i) ok = r.payload[i] == '\0';
+    for (size_t i = p.size(); ok && i < r.payload.size(); ++i) ok = r.payload.data()[i] == '\0';
     EXPECT(ok);
     exact += ok;
   }

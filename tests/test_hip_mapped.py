@@ -1,0 +1,133 @@
+"""GPU parity tests of QFEC_PTR_MAPPED: the FEC kernels read and write payloads
+in pinned host memory in place (zero-copy over PCIe), index arrays staged by
+the call.  Bit-exact against the oracle and the golden fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle_c as OC
+from oracle import qfec_np as Q
+from libquic_amd import qfec
+
+from test_hip_ragged import sub, synth_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def pinned(a):
+    """a copy of `a` in qfec_host_alloc memory (kept alive by the returned buffer)"""
+    hb = qfec.HostBuffer(max(1, a.nbytes))
+    hb.array[:a.nbytes] = np.ascontiguousarray(a).view(np.uint8).ravel()
+    return hb
+
+
+@pytest.mark.parametrize("alloc", ["qfec_host_alloc", "torch_pin_memory"])
+def test_fixed_mapped(ctx, alloc):
+    k, L, n = 10, 1350, 9_001
+    rows = OC.synth_fixed(Q.SEED_FIXED, 0, n, k, L)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
+    _, want_p = OC.encode_fixed(rows, k, L, n)
+    if alloc == "qfec_host_alloc":
+        h_rows, h_par, h_out = pinned(rows), qfec.HostBuffer(n * L), qfec.HostBuffer(n * L)
+        r, p, o = h_rows.array, h_par.array, h_out.array
+    else:
+        r = torch.from_numpy(rows).pin_memory()
+        p = torch.zeros(n * L, dtype=torch.uint8).pin_memory()
+        o = torch.zeros(n * L, dtype=torch.uint8).pin_memory()
+    ctx.encode(r, k, L, n, p, mapped=True)
+    ctx.recover(r, p, miss, k, L, n, o, mapped=True)
+    par = p if isinstance(p, np.ndarray) else p.numpy()
+    out = o if isinstance(o, np.ndarray) else o.numpy()
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out.reshape(n, L), rows.reshape(n, k, L)[np.arange(n), miss])
+
+
+def test_fixed_mapped_strided(ctx):
+    k, L, n = 5, 1350, 3000
+    rs, ps = 1408, 1452
+    rows = OC.synth_fixed(4, 0, n, k, L, row_stride=rs, group_stride=k * rs)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
+    _, want_p = OC.encode_fixed(rows, k, L, n, rs, k * rs, ps)
+    h_rows, h_par, h_out = pinned(rows), qfec.HostBuffer(n * ps), qfec.HostBuffer(n * ps)
+    h_par.array[:] = 0
+    ctx.encode(h_rows.array, k, L, n, h_par.array, row_stride=rs, group_stride=k * rs,
+               parity_stride=ps, mapped=True)
+    assert np.array_equal(h_par.array, want_p)
+    ctx.recover(h_rows.array, h_par.array, miss, k, L, n, h_out.array, row_stride=rs,
+                group_stride=k * rs, parity_stride=ps, out_stride=ps, mapped=True)
+    o = h_out.array.reshape(n, ps)[:, :L]
+    assert np.array_equal(o, rows.reshape(n, k, rs)[np.arange(n), miss, :L])
+
+
+def run_ragged_mapped(ctx, z):
+    n = z["grp_ptr"].size - 1
+    data = pinned(z["data"])
+    par = qfec.HostBuffer(z["parity"].size)
+    par.array[:] = 0
+    plen = np.zeros(n, np.uint16)
+    ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                      z["parity_off"], plen, mapped=True)
+    out = qfec.HostBuffer(z["recovered"].size)
+    out.array[:] = 0
+    ctx.recover_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                       z["parity_off"], plen, z["missing"], out.array, z["out_off"], mapped=True)
+    return par.array.copy(), plen, out.array.copy()
+
+
+@pytest.mark.parametrize("tag", ["main", "tiny"])
+def test_golden_ragged_mapped(ctx, golden_ragged, tag):
+    z = sub(golden_ragged, tag)
+    par, plen, out = run_ragged_mapped(ctx, z)
+    assert np.array_equal(plen, z["parity_len"])
+    assert np.array_equal(par, z["parity"])
+    assert np.array_equal(out, z["recovered"])
+
+
+def test_ragged_mapped_vs_oracle(ctx):
+    n = 20_000
+    ks, ptr, ln, off = synth_batch(n, g0=5)
+    total = int(off[-1] + ln[-1])
+    data = np.random.default_rng(11).integers(0, 256, total, dtype=np.uint8)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(5, 5 + n), ks).astype(np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1452)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged_mapped(ctx, z)
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
+
+
+def test_xor_into_mapped(ctx):
+    n = 1_000_003
+    rng = np.random.default_rng(5)
+    a, b = rng.integers(0, 256, n, dtype=np.uint8), rng.integers(0, 256, n, dtype=np.uint8)
+    ha, hb = pinned(a), pinned(b)
+    ctx.xor_into(ha.array, n, hb.array, mapped=True)
+    assert np.array_equal(hb.array[:n], a ^ b)
+
+
+def test_mapped_refuses_pageable_and_bad_flags(ctx):
+    k, L, n = 3, 64, 4
+    rows = np.zeros(n * k * L, np.uint8)  # pageable numpy memory
+    par = qfec.HostBuffer(n * L)
+    with pytest.raises(qfec.QfecError, match="QFEC_PTR_MAPPED"):
+        ctx.encode(rows, k, L, n, par.array, mapped=True)
+    h_rows = pinned(rows)
+    with pytest.raises(qfec.QfecError, match="exclusive"):
+        ctx.encode(h_rows.array, k, L, n, par.array, mapped=True, host=True)
+    with pytest.raises(qfec.InvalidFecData):
+        ctx.recover(h_rows.array, par.array, np.array([0, 1, 3, 0], np.uint8), k, L, n,
+                    par.array, mapped=True)
+    # ragged: an invalid length is reported before any device work
+    ptr = np.array([0, 2], np.uint32)
+    off = np.array([0, 100], np.uint64)
+    ln = np.array([64, 1453], np.uint16)
+    plen = np.zeros(1, np.uint16)
+    with pytest.raises(qfec.InvalidFecData):
+        ctx.encode_ragged(h_rows.array, off, ln, ptr, 1, par.array,
+                          np.zeros(1, np.uint64), plen, mapped=True)
