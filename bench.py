@@ -63,6 +63,9 @@ def parse(argv=None):
                         "exercises the rank launch / shard / timing / JSON path on a CPU box")
     p.add_argument("--profile-only", action="store_true",
                    help="only the device-resident steps (for rocprofv3 runs)")
+    p.add_argument("--protect-only", action="store_true",
+                   help="only the packet-protection leg, no CPU baseline (for rocprofv3 --pmc "
+                        "instruction counts: tools/pmc_protect.sh)")
     return p.parse_args(argv)
 
 
@@ -432,6 +435,18 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
+    if args.protect_only:  # instruction-count runs of the protection kernels
+        from libquic_amd import qfec
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        ctx = qfec.Context(0)
+        stream = torch.cuda.current_stream()
+        ctx.set_stream(stream)
+        res = bench_protect(ctx, torch, dev, stream, args.groups, args.k, args.L, reps=1, cpu=False)
+        print(json.dumps({"protect": res}), flush=True)
+        ctx.close()
+        return 0
+
     cpu = args.cpu_workload
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -490,6 +505,10 @@ def main(argv=None):
                            "digests": r["digests"]} for r in per_rank]
 
     extras = rank == 0 and world == 1 and not cpu and not args.profile_only
+    if rank == 0 and world == 1 and not cpu and args.profile_only and not args.no_ragged:
+        # the ragged kernels' launches for the rocprofv3 runs (tools/pmc.sh)
+        work.release()
+        line["ragged"] = bench_ragged(work.ctx, torch, dev, work.stream, steps=3)
     if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
         if line["roofline"]:  # the encode kernel against this box's measured streaming read
@@ -538,6 +557,21 @@ def main(argv=None):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def ragged_alg_bytes(G=1 << 20):
+    """Algorithmic bytes of one encode / one recover launch
+    over bench_ragged's batch: encode reads every packet and writes
+    parity_len; recover reads the received packets and the parity and writes
+    parity_len."""
+    from libquic_amd import synth
+    ks, ptr, ln, off = synth.ragged_layout(0, G, 5, 15, 64, 1350, SEED_RAGGED)
+    plen_max = np.maximum.reduceat(ln, ptr[:-1].astype(np.int64))
+    miss = synth.drop_indices(SEED_DROP, np.arange(G, dtype=np.uint64), ks).astype(np.uint8)
+    lens_sum = float(ln.astype(np.float64).sum())
+    pl_sum = float(plen_max.astype(np.float64).sum())
+    miss_len = float(ln[ptr[:-1].astype(np.int64) + miss.astype(np.int64)].astype(np.float64).sum())
+    return lens_sum + pl_sum, (lens_sum - miss_len) + 2 * pl_sum
 
 
 def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
@@ -598,18 +632,23 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
         for q in range(int(ptr[g]), int(ptr[g + 1])):
             acc[:int(ln[q])] ^= data_h[int(off[q]):int(off[q]) + int(ln[q])]
         ok = ok and not acc.any()
-    lens_sum = float(ln.astype(np.float64).sum())
-    pl_sum = float(plen_max.astype(np.float64).sum())
-    miss_len = float(ln[ptr[:-1].astype(np.int64) + miss.astype(np.int64)].astype(np.float64).sum())
-    b_enc = lens_sum + pl_sum
-    b_rec = (lens_sum - miss_len) + 2 * pl_sum
+    b_enc, b_rec = ragged_alg_bytes(G)
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("ragged_groups") == G:
+            traffic = {kd: tj.get(f"ragged_{kd}_traffic_over_algorithmic")
+                       for kd in ("encode", "recover")}
+            traffic["source"] = "profiles/traffic_latest.json (PMC FETCH_SIZE + WRITE_SIZE)"
     return {"groups": G, "k": "5-15", "len": "64-1350", "layout": "packed CSR",
             "encode_GiBps": round(b_enc / enc / 2**30, 2),
             "recover_GiBps": round(b_rec / rec / 2**30, 2),
             "encode_frac": round(b_enc / enc / 1e9 / HBM_PEAK_GBS, 4),
             "recover_frac": round(b_rec / rec / 1e9 / HBM_PEAK_GBS, 4),
             "encode_us": round(enc * 1e6, 1), "recover_us": round(rec * 1e6, 1),
-            "verified": bool(ok)}
+            "hbm_traffic_over_algorithmic": traffic, "verified": bool(ok)}
 
 
 def _time_on(torch, stream, fn, reps):
@@ -726,11 +765,46 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
                "seal_payload_GBps": round(n * L / (ms_gs / 1e3) / 1e9, 1),
                "seal_us": round(ms_gs * 1e3, 1), "open_us": round(ms_go * 1e3, 1),
                "verified": verified_g}}
+    res["issue_bound"] = {
+        "null_encrypt": _issue_bound(lambda k: "null_encrypt" in k, n, ms_e),
+        "null_decrypt": _issue_bound(lambda k: "null_decrypt" in k, n, ms_d),
+        "chacha20poly1305_seal": _issue_bound(lambda k: "c20p1305_seal" in k, n, ms_cs),
+        "chacha20poly1305_open": _issue_bound(lambda k: "c20p1305_open" in k, n, ms_co),
+        "aes128gcm_seal": _issue_bound(lambda k: "aes128gcm_kernel" in k and ", false," in k, n,
+                                       ms_gs),
+        "aes128gcm_open": _issue_bound(lambda k: "aes128gcm_kernel" in k and ", true," in k, n,
+                                       ms_go),
+        "note": "fraction of kernel time the VALU / LDS / scalar units were busy (PMC)"}
     del cat, dout, data
     torch.cuda.empty_cache()
     if cpu:
         res["cpu_baseline"] = cpu_protect_baseline(hdr, L)
     return res
+
+
+def _issue_bound(kernel_pred, n, ms):
+    """Compute-roofline fractions of a protection kernel, from the PMC passes
+    in profiles/protect_insts_latest.json (tools/pmc_protect.sh): the
+    fraction of the kernel's time the CUs' VALU / LDS / scalar units were
+    busy (rocprofv3's VALUBusy definition) and its wave instructions per
+    packet.  A VALU-bound kernel sits near valu_busy = 1."""
+    path = os.path.join(ROOT, "profiles", "protect_insts_latest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pj = json.load(f)
+    for name, kd in pj.get("kernels", {}).items():
+        if kernel_pred(name):
+            pp = kd.get("per_packet", {})
+            r = {"kernel": name,
+                 "valu_insts_per_packet": round(pp.get("SQ_INSTS_VALU", 0.0), 1),
+                 "lds_insts_per_packet": round(pp.get("SQ_INSTS_LDS", 0.0), 1),
+                 "source": "profiles/protect_insts_latest.json"}
+            for u in ("valu", "lds", "salu"):
+                if f"{u}_busy" in kd:
+                    r[f"{u}_busy"] = round(kd[f"{u}_busy"], 4)
+            return r
+    return None
 
 
 def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
@@ -933,10 +1007,12 @@ def bench_connection(cpu=True):
     if r.returncode != 0:
         return {"error": (r.stderr or r.stdout)[-400:]}
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    res["note"] = ("one Flush = CSR build + gather into pinned staging + H2D + one ragged launch "
-                   "+ D2H + scatter + FEC body / revived copies (wall, median); cpu_1core = the "
-                   "oracle's per-group XorBuffers accumulate (the reference's connection-thread "
-                   "path), one core" + ("" if cpu else "; cpu legs requested off but always run"))
+    res["note"] = ("one Flush = CSR build + index tables staged to the device + one ragged "
+                   "launch reading the groups' payloads in place from the pinned payload arena "
+                   "(QFEC_PTR_MAPPED) + the redundancy / revived views (wall, median); "
+                   "cpu_1core = the oracle's per-group XorBuffers accumulate (the reference's "
+                   "connection-thread path), one core"
+                   + ("" if cpu else "; cpu legs requested off but always run"))
     return res
 
 
@@ -1124,10 +1200,29 @@ def bench_e2e(ctx, torch, k, L, G=1 << 18):
     t_rec = (time.perf_counter() - t0) / reps
     r3 = rows.numpy().reshape(G, k, L)
     ok = np.array_equal(out.numpy().reshape(G, L)[:4096], r3[np.arange(4096), miss[:4096]])
+    # zero-copy (QFEC_PTR_MAPPED): the kernels read the pinned rows / parity and
+    # write their outputs in host memory in place, no staging
+    par.fill_(0)
+    out.fill_(0)
+    ctx.encode(rows, k, L, G, par, mapped=True)  # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.encode(rows, k, L, G, par, mapped=True)
+    t_enc_m = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.recover(rows, par, miss, k, L, G, out, mapped=True)
+    t_rec_m = (time.perf_counter() - t0) / reps
+    ok_m = np.array_equal(out.numpy().reshape(G, L)[-4096:], r3[np.arange(G - 4096, G),
+                                                                 miss[-4096:]])
     b = G * (k * L + L)
     return {"groups": G, "encode_GiBps": round(b / t_enc / 2**30, 2),
             "recover_GiBps": round(b / t_rec / 2**30, 2),
             "pcie_bytes_encode": G * (k * L + L), "verified": bool(ok),
+            "zero_copy": {"encode_GiBps": round(b / t_enc_m / 2**30, 2),
+                          "recover_GiBps": round(b / t_rec_m / 2**30, 2), "verified": bool(ok_m),
+                          "note": "QFEC_PTR_MAPPED: kernels read/write the pinned host buffers "
+                                  "in place over PCIe"},
             "note": "algorithmic bytes / wall time, pinned host buffers, 3-slot H2D/kernel/D2H"}
 
 
