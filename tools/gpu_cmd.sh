@@ -1,3 +1,3 @@
 mkdir -p gpurun_out
-bash tools/pmc_protect.sh r2c > gpurun_out/pmc_protect_r2c.log 2>&1
+timeout -k 10 300 tools/tune/build/tune_rw 2 1 > gpurun_out/tune_rw_i.txt 2>&1
 echo rc=$?
