@@ -151,15 +151,11 @@ int main(int argc, char** argv) {
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
-  vs.push_back({"window PB4 encode", false, [=](const RaggedArgs& a) { launch_win<false, 4>(a, G); }});
-  vs.push_back({"flat B4 gated encode", false, [=](const RaggedArgs& a) { launch_flat<false, 4, true, 0, 2>(a, G); }});
   vs.push_back({"flat B10 d8 encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 8>(a, G); }});
-  vs.push_back({"flat B10 d8 1blk/CU encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 8>(a, G, 140 << 10); }});
+  vs.push_back({"flat B10 d8 det encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 24>(a, G); }});
   vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
-  vs.push_back({"window PB4 recover", true, [=](const RaggedArgs& a) { launch_win<true, 4>(a, G); }});
-  vs.push_back({"flat B4 gated recover", true, [=](const RaggedArgs& a) { launch_flat<true, 4, true, 0, 2>(a, G); }});
   vs.push_back({"flat B10 d8 recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 8>(a, G); }});
-  vs.push_back({"flat B10 d8 1blk/CU recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 8>(a, G, 140 << 10); }});
+  vs.push_back({"flat B10 d8 det recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 24>(a, G); }});
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
@@ -248,7 +244,7 @@ int main(int argc, char** argv) {
       }
       std::printf("   bad groups %llu\n", (unsigned long long)nbad);
     }
-    if (v.name.find(" d8 ") == std::string::npos || v.name.find("1blk") != std::string::npos)
+    if (v.name.find(" d8 ") == std::string::npos || v.name.find("1blk") != std::string::npos)  // NOLINT
       all_ok = all_ok && same && he == 0;
   }
   hipEvent_t e0, e1;
