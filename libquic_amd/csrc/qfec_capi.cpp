@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -272,6 +273,15 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
 // cross the link exactly once and no host thread copies them.  Only the index
 // arrays are staged (10 B per packet + 12-23 B per group), chunked over the
 // context's slots so chunk c+1's tables are copied while chunk c runs.
+// Groups per mapped-mode chunk: the staging capacity, or fewer when
+// QFEC_CHUNK_GROUPS is set (lets the tests run the multi-chunk pipeline on
+// small batches; read per call).
+uint64_t mapped_chunk_groups(uint64_t cap) {
+  const char* e = std::getenv("QFEC_CHUNK_GROUPS");
+  const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+  return v ? std::min(v, cap) : cap;
+}
+
 int check_mapped(qfec_ctx* ctx, const void* p, const char* what) {
   if (!is_pinned_or_device(p))
     return fail(ctx, QFEC_ERR_INTERNAL,
@@ -300,7 +310,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   a.L = L;
   a.err = ctx->d_err;
   // the lost-slot indices are the only staged input (kStageBytes / 8 per chunk)
-  const uint64_t cg = recover ? kStageBytes / 8 : n;
+  const uint64_t cg = mapped_chunk_groups(recover ? kStageBytes / 8 : n);
   uint64_t g0_of[kSlots] = {};
   bool live[kSlots] = {};
   int slot = 0;
@@ -829,7 +839,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     c.live = false;
     return QFEC_OK;
   };
-  const uint64_t out_cap = (kStageBytes / 4) / sizeof(uint16_t);
+  const uint64_t out_cap = mapped_chunk_groups((kStageBytes / 4) / sizeof(uint16_t));
   int slot = 0;
   uint64_t g = 0;
   while (g < n) {

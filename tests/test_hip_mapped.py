@@ -9,7 +9,7 @@ from oracle import oracle_c as OC
 from oracle import qfec_np as Q
 from libquic_amd import qfec
 
-from test_hip_ragged import sub, synth_batch
+from test_hip_ragged import run_ragged, sub, synth_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -60,18 +60,7 @@ def test_fixed_mapped_strided(ctx):
 
 
 def run_ragged_mapped(ctx, z):
-    n = z["grp_ptr"].size - 1
-    data = pinned(z["data"])
-    par = qfec.HostBuffer(z["parity"].size)
-    par.array[:] = 0
-    plen = np.zeros(n, np.uint16)
-    ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
-                      z["parity_off"], plen, mapped=True)
-    out = qfec.HostBuffer(z["recovered"].size)
-    out.array[:] = 0
-    ctx.recover_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
-                       z["parity_off"], plen, z["missing"], out.array, z["out_off"], mapped=True)
-    return par.array.copy(), plen, out.array.copy()
+    return run_ragged(ctx, z, host="mapped")
 
 
 @pytest.mark.parametrize("tag", ["main", "tiny"])
@@ -131,3 +120,36 @@ def test_mapped_refuses_pageable_and_bad_flags(ctx):
     with pytest.raises(qfec.InvalidFecData):
         ctx.encode_ragged(h_rows.array, off, ln, ptr, 1, par.array,
                           np.zeros(1, np.uint64), plen, mapped=True)
+
+
+@pytest.mark.parametrize("chunk", ["7", "1000"])
+def test_mapped_multi_chunk(ctx, chunk, monkeypatch):
+    """QFEC_CHUNK_GROUPS shrinks the mapped paths' chunks: the table staging /
+    lost-slot staging pipeline over several slots, against the oracle."""
+    monkeypatch.setenv("QFEC_CHUNK_GROUPS", chunk)
+    n = 3001
+    ks, ptr, ln, off = synth_batch(n, g0=9)
+    data = np.random.default_rng(int(chunk)).integers(0, 256, int(off[-1] + ln[-1]),
+                                                      dtype=np.uint8)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(9, 9 + n), ks).astype(np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1452)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged(ctx, z, host="mapped")
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
+    # fixed shape: the lost-slot indices staged in chunks
+    k, L, nf = 4, 200, 2003
+    rows = OC.synth_fixed(Q.SEED_FIXED, 0, nf, k, L)
+    mf = Q.drop_index(Q.SEED_DROP, np.arange(nf), k).astype(np.uint8)
+    h_rows, h_par, h_out = pinned(rows), qfec.HostBuffer(nf * L), qfec.HostBuffer(nf * L)
+    ctx.encode(h_rows.array, k, L, nf, h_par.array, mapped=True)
+    ctx.recover(h_rows.array, h_par.array, mf, k, L, nf, h_out.array, mapped=True)
+    _, want_pf = OC.encode_fixed(rows, k, L, nf)
+    assert np.array_equal(h_par.array, want_pf)
+    assert np.array_equal(h_out.array.reshape(nf, L), rows.reshape(nf, k, L)[np.arange(nf), mf])

@@ -32,8 +32,24 @@ def dview(a):
 
 
 def run_ragged(ctx, z, host=False):
+    """host: False = device pointers, True = QFEC_PTR_HOST (staged), "mapped" =
+    QFEC_PTR_MAPPED (payloads in qfec_host_alloc memory, read in place)."""
     n = z["grp_ptr"].size - 1
     psize = z["parity"].size
+    if host == "mapped":
+        data = qfec.HostBuffer(max(1, z["data"].nbytes))
+        data.array[:z["data"].nbytes] = z["data"].view(np.uint8).ravel()
+        par = qfec.HostBuffer(psize)
+        par.array[:] = 0
+        plen = np.zeros(n, np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                          z["parity_off"], plen, mapped=True)
+        out = qfec.HostBuffer(z["recovered"].size)
+        out.array[:] = 0
+        ctx.recover_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                           z["parity_off"], plen, z["missing"], out.array, z["out_off"],
+                           mapped=True)
+        return par.array.copy(), plen, out.array.copy()
     if host:
         par = np.zeros(psize, np.uint8)
         plen = np.zeros(n, np.uint16)
@@ -63,7 +79,7 @@ def sub(golden, tag):
 
 
 @pytest.mark.parametrize("tag", ["main", "tiny"])
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "mapped"])
 def test_golden_ragged(ctx, golden_ragged, tag, host):
     z = sub(golden_ragged, tag)
     par, plen, out = run_ragged(ctx, z, host=host)
@@ -136,7 +152,7 @@ def test_ragged_edges(ctx):
     assert rc == 0 and rc2 == 0
     z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
              out_off=poff, parity=want_p, recovered=want_o)
-    for host in (False, True):
+    for host in (False, True, "mapped"):
         par, plen, out = run_ragged(ctx, z, host=host)
         assert np.array_equal(plen, want_l)
         assert np.array_equal(par, want_p)
@@ -192,7 +208,7 @@ def test_cpp_quic_fec_group():
     assert " 0 failures" in r.stdout
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "mapped"])
 def test_ragged_pair_boundaries(ctx, host):
     """launch_ragged runs two consecutive groups per wave (groups 2w, 2w+1) in
     one flat window space when their received packets fit the 64-lane table,
