@@ -1016,7 +1016,7 @@ def bench_connection(cpu=True):
     return res
 
 
-def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=8192, slots=3, cpu=True):
+def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slots=3, cpu=True):
     """Host memory in, host memory out, FEC + packet protection on the device
     with ONE PCIe crossing each way:
     per chunk of cg groups, H2D of the plaintext payloads + headers, FEC encode

@@ -45,10 +45,14 @@ static T* up(const std::vector<T>& v) {
 
 using qfec::RaggedArgs;
 
-template <bool REC, int GPW, bool NT = true>
+template <bool REC, int GPW, bool NT = true, int U = 2, bool ALIGN = false>
 static void launch_multi(const RaggedArgs& a, uint64_t G) {
   const uint64_t per = (uint64_t)GPW * 4;
-  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, NT, GPW>),
+  if constexpr (ALIGN)
+    hipLaunchKernelGGL((qfec::ragged_multi_align_kernel<REC, NT, GPW, U, 4, false, true>),
+                       dim3((uint32_t)((G + per - 1) / per)), dim3(256), 0, 0, a);
+  else
+    hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, NT, GPW, U, 4, false>),
                      dim3((uint32_t)((G + per - 1) / per)), dim3(256), 0, 0, a);
 }
 
@@ -151,11 +155,15 @@ int main(int argc, char** argv) {
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
-  vs.push_back({"flat B10 d8 encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 8>(a, G); }});
-  vs.push_back({"flat B10 d8 det encode", false, [=](const RaggedArgs& a) { launch_flat<false, 10, false, 0, 24>(a, G); }});
+  vs.push_back({"multi2 align U2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 2, true>(a, G); }});
+  vs.push_back({"multi2 align U1 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 1, true>(a, G); }});
+  vs.push_back({"multi2 align U3 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 3, true>(a, G); }});
+  vs.push_back({"multi3 align U2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, true, 2, true>(a, G); }});
   vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
-  vs.push_back({"flat B10 d8 recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 8>(a, G); }});
-  vs.push_back({"flat B10 d8 det recover", true, [=](const RaggedArgs& a) { launch_flat<true, 10, false, 0, 24>(a, G); }});
+  vs.push_back({"multi2 align U2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 2, true>(a, G); }});
+  vs.push_back({"multi2 align U1 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 1, true>(a, G); }});
+  vs.push_back({"multi2 align U3 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 3, true>(a, G); }});
+  vs.push_back({"multi3 align U2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, true, 2, true>(a, G); }});
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);

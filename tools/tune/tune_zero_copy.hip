@@ -63,6 +63,31 @@ int main(int argc, char** argv) {
   std::printf("%-44s %8.3f ms %8.1f GB/s\n", "H2D memcpy (coherent pinned)", ms, gbs(nb, ms));
   ms = time_ms([&] { CK(hipMemcpyAsync(h_coh, d_rows, nb, hipMemcpyDeviceToHost, 0)); }, reps);
   std::printf("%-44s %8.3f ms %8.1f GB/s\n", "D2H memcpy (coherent pinned)", ms, gbs(nb, ms));
+  {  // both directions at once (two streams): the fused FEC + AEAD leg's budget
+    uint8_t* h2;
+    uint8_t* d2;
+    CK(hipHostMalloc(&h2, nb, hipHostMallocDefault));
+    CK(hipMalloc(&d2, nb));
+    hipStream_t s1, s2;
+    CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    auto both = [&] {
+      CK(hipMemcpyAsync(d_rows, h_coh, nb, hipMemcpyHostToDevice, s1));
+      CK(hipMemcpyAsync(h2, d2, nb, hipMemcpyDeviceToHost, s2));
+      CK(hipStreamSynchronize(s1));
+      CK(hipStreamSynchronize(s2));
+    };
+    both();
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) both();
+    const double ms2 =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
+        reps;
+    std::printf("%-44s %8.3f ms %8.1f GB/s (each way %.1f)\n", "H2D || D2H (two streams)", ms2,
+                gbs(2.0 * nb, ms2), gbs(nb, ms2));
+    CK(hipHostFree(h2));
+    CK(hipFree(d2));
+  }
   for (int nc = 0; nc < 2; ++nc) {
     uint8_t* h = nc ? h_nc : h_coh;
     const char* tag = nc ? "non-coherent" : "coherent";
