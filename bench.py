@@ -1007,9 +1007,11 @@ def bench_connection(cpu=True):
     if r.returncode != 0:
         return {"error": (r.stderr or r.stdout)[-400:]}
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    res["note"] = ("one Flush = CSR build + index tables staged to the device + one ragged "
-                   "launch reading the groups' payloads in place from the pinned payload arena "
-                   "(QFEC_PTR_MAPPED) + the redundancy / revived views (wall, median); "
+    res["note"] = ("one Flush = CSR build + one ragged launch reading the groups' payloads in "
+                   "place from the pinned payload arena (QFEC_PTR_MAPPED) + the redundancy / "
+                   "revived views (wall, median); up to 256 groups the index tables are read in "
+                   "place too and the host spins on a completion flag the kernel's last "
+                   "workgroup stores (latency path), above that they are staged to the device; "
                    "cpu_1core = the oracle's per-group XorBuffers accumulate (the reference's "
                    "connection-thread path), one core"
                    + ("" if cpu else "; cpu legs requested off but always run"))

@@ -26,6 +26,7 @@ thread_local char g_tls_error[512] = "";
 
 constexpr int kSlots = 3;                         // host path pipeline depth
 constexpr size_t kStageBytes = 64ull << 20;       // per-slot input staging
+constexpr uint64_t kDirectGroups = 256;  // mapped batches up to this size: no staging copies
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -33,9 +34,12 @@ struct Slot {
   uint8_t* d_in = nullptr;   // device input staging
   uint8_t* d_aux = nullptr;  // device parity-in / missing staging
   uint8_t* d_out = nullptr;  // device output staging
-  uint8_t* h_in = nullptr;   // pinned input bounce buffer
+  uint8_t* h_in = nullptr;   // pinned input bounce buffer (device-mapped)
   uint8_t* h_aux = nullptr;
   uint8_t* h_out = nullptr;
+  uint8_t* h_in_dev = nullptr;  // the same pinned buffers as the device addresses them
+  uint8_t* h_aux_dev = nullptr;
+  uint8_t* h_out_dev = nullptr;
   bool busy = false;
 };
 
@@ -50,6 +54,12 @@ struct qfec_ctx {
   char last_error[512] = "";
   Slot slots[kSlots];
   bool staging_ready = false;
+  // small-batch completion (launch_ragged_latency): per-slot device block
+  // counters and host-mapped flags the kernel's last workgroup stores to
+  uint32_t* d_done = nullptr;
+  uint32_t* h_flag = nullptr;
+  uint32_t* h_flag_dev = nullptr;
+  uint32_t flag_token = 0;
 };
 
 namespace {
@@ -94,12 +104,41 @@ int ensure_staging(qfec_ctx* ctx) {
     QFEC_HIP(ctx, hipMalloc(&s.d_in, kStageBytes));
     QFEC_HIP(ctx, hipMalloc(&s.d_aux, kStageBytes / 8));
     QFEC_HIP(ctx, hipMalloc(&s.d_out, kStageBytes / 4));
-    QFEC_HIP(ctx, hipHostMalloc(&s.h_in, kStageBytes, hipHostMallocDefault));
-    QFEC_HIP(ctx, hipHostMalloc(&s.h_aux, kStageBytes / 8, hipHostMallocDefault));
-    QFEC_HIP(ctx, hipHostMalloc(&s.h_out, kStageBytes / 4, hipHostMallocDefault));
+    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_in, kStageBytes, fl));
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_aux, kStageBytes / 8, fl));
+    QFEC_HIP(ctx, hipHostMalloc(&s.h_out, kStageBytes / 4, fl));
+    QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_in_dev), s.h_in, 0));
+    QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_aux_dev), s.h_aux, 0));
+    QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_out_dev), s.h_out, 0));
   }
+  QFEC_HIP(ctx, hipMalloc(&ctx->d_done, kSlots * sizeof(uint32_t)));
+  QFEC_HIP(ctx, hipMemset(ctx->d_done, 0, kSlots * sizeof(uint32_t)));
+  QFEC_HIP(ctx, hipHostMalloc(&ctx->h_flag, kSlots * sizeof(uint32_t),
+                              hipHostMallocMapped | hipHostMallocPortable));
+  std::memset(ctx->h_flag, 0, kSlots * sizeof(uint32_t));
+  QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->h_flag_dev), ctx->h_flag, 0));
   ctx->staging_ready = true;
   return QFEC_OK;
+}
+
+// Wait for a launch_ragged_latency kernel by spinning on its host-mapped
+// completion flag (a few us sooner than the event's wait path); the slot's
+// event, recorded after the launch, is polled now and then so that a flag
+// that never comes ends in an error instead of a hang.
+int wait_flag(qfec_ctx* ctx, int si, uint32_t token) {
+  const uint32_t* f = ctx->h_flag + si;
+  for (uint32_t spins = 1;; ++spins) {
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
+    if ((spins & 1023u) == 0) {
+      const hipError_t q = hipEventQuery(ctx->slots[si].done);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
+        return fail(ctx, QFEC_ERR_INTERNAL, "ragged latency kernel finished without its flag");
+      }
+      if (q != hipErrorNotReady) QFEC_HIP(ctx, q);
+    }
+  }
 }
 
 int check_fixed(qfec_ctx* ctx, uint32_t k, uint32_t L, uint64_t row_stride,
@@ -309,8 +348,13 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
-  // the lost-slot indices are the only staged input (kStageBytes / 8 per chunk)
+  // the lost-slot indices are the only staged input (kStageBytes / 8 per chunk);
+  // a small batch (one chunk of <= kDirectGroups) is latency-bound: the kernel
+  // reads them from the mapped slot buffer itself (no copy), and the error
+  // word is not fetched — the host already checked every index the kernel
+  // checks (qfec_recover_batch_strided), so the launch cannot latch one
   const uint64_t cg = mapped_chunk_groups(recover ? kStageBytes / 8 : n);
+  const bool direct = n <= std::min<uint64_t>(cg, kDirectGroups);
   uint64_t g0_of[kSlots] = {};
   bool live[kSlots] = {};
   int slot = 0;
@@ -324,8 +368,12 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
     if (recover) {
       a.parity = parity + g0 * parity_stride;
       std::memcpy(s.h_aux, missing + g0, cnt);
-      QFEC_HIP(ctx, hipMemcpyAsync(s.d_aux, s.h_aux, cnt, hipMemcpyHostToDevice, s.stream));
-      a.missing = s.d_aux;
+      if (direct) {
+        a.missing = s.h_aux_dev;
+      } else {
+        QFEC_HIP(ctx, hipMemcpyAsync(s.d_aux, s.h_aux, cnt, hipMemcpyHostToDevice, s.stream));
+        a.missing = s.d_aux;
+      }
     }
     QFEC_HIP(ctx, qfec::launch_fixed(a, true, s.stream));
     QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
@@ -335,7 +383,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   for (int si = 0; si < kSlots; ++si)
     if (live[si]) QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
   (void)g0_of;
-  return collect_error(ctx, ctx->slots[0].stream);
+  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream);
 }
 
 }  // namespace
@@ -483,6 +531,8 @@ void qfec_destroy(qfec_ctx* ctx) {
     if (s.h_aux) (void)hipHostFree(s.h_aux);
     if (s.h_out) (void)hipHostFree(s.h_out);
   }
+  if (ctx->d_done) (void)hipFree(ctx->d_done);
+  if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->h_err) (void)hipHostFree(ctx->h_err);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -828,18 +878,30 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   };
   struct Pend {
     uint64_t g0 = 0, cnt = 0;
+    uint32_t token = 0;  // direct: the completion flag's value
     bool live = false;
   } pend[kSlots];
   auto finish = [&](int si) -> int {
     Pend& c = pend[si];
     if (!c.live) return QFEC_OK;
-    QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
+    if (c.token) {
+      const int wrc = wait_flag(ctx, si, c.token);
+      if (wrc) return wrc;
+    } else {
+      QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
+    }
     if (!recover)
       std::memcpy(parity_len_out + c.g0, ctx->slots[si].h_out, c.cnt * sizeof(uint16_t));
     c.live = false;
     return QFEC_OK;
   };
   const uint64_t out_cap = mapped_chunk_groups((kStageBytes / 4) / sizeof(uint16_t));
+  // A small batch (the connection thread's flush of a few groups) is
+  // latency-bound: the kernel reads the tables from the mapped slot buffer and
+  // writes the encode lengths straight into the mapped output buffer — no
+  // copies, one launch and one synchronisation — and the error word is not
+  // fetched: validate_ragged checked every condition the kernel latches.
+  const bool direct = n <= std::min<uint64_t>(out_cap, kDirectGroups);
   int slot = 0;
   uint64_t g = 0;
   while (g < n) {
@@ -863,38 +925,52 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       std::memcpy(h + t.plen, parity_len + g0, cnt * 2);
       std::memcpy(h + t.miss, missing + g0, cnt);
     }
-    QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, h, t.total, hipMemcpyHostToDevice, s.stream));
+    uint8_t* tab = s.h_in_dev;  // direct: the device reads the tables where they are
+    if (!direct) {
+      QFEC_HIP(ctx, hipMemcpyAsync(s.d_in, h, t.total, hipMemcpyHostToDevice, s.stream));
+      tab = s.d_in;
+    }
     qfec::RaggedArgs a{};
     a.bytes = bytes;
-    a.pkt_off = reinterpret_cast<const uint64_t*>(s.d_in + t.off);
-    a.pkt_len = reinterpret_cast<const uint16_t*>(s.d_in + t.len);
-    a.grp_ptr = reinterpret_cast<const uint32_t*>(s.d_in + t.ptr);
-    a.parity_off = reinterpret_cast<const uint64_t*>(s.d_in + t.poff);
+    a.pkt_off = reinterpret_cast<const uint64_t*>(tab + t.off);
+    a.pkt_len = reinterpret_cast<const uint16_t*>(tab + t.len);
+    a.grp_ptr = reinterpret_cast<const uint32_t*>(tab + t.ptr);
+    a.parity_off = reinterpret_cast<const uint64_t*>(tab + t.poff);
     a.n_groups = cnt;
     a.err = ctx->d_err;
     if (recover) {
       a.parity = parity;
-      a.parity_len = reinterpret_cast<const uint16_t*>(s.d_in + t.plen);
-      a.missing = s.d_in + t.miss;
-      a.out_off = reinterpret_cast<const uint64_t*>(s.d_in + t.ooff);
+      a.parity_len = reinterpret_cast<const uint16_t*>(tab + t.plen);
+      a.missing = tab + t.miss;
+      a.out_off = reinterpret_cast<const uint64_t*>(tab + t.ooff);
       a.out = out;
     } else {
-      a.parity_len_out = reinterpret_cast<uint16_t*>(s.d_out);
+      a.parity_len_out = reinterpret_cast<uint16_t*>(direct ? s.h_out_dev : s.d_out);
       a.out = parity_out;
     }
-    QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
-    if (!recover)
+    uint32_t token = 0;
+    if (direct) {
+      token = ++ctx->flag_token ? ctx->flag_token : ++ctx->flag_token;  // never 0
+      a.done_count = ctx->d_done + slot;
+      a.done_flag = ctx->h_flag_dev + slot;
+      a.done_token = token;
+      QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
+    } else {
+      QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+    }
+    if (!recover && !direct)
       QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
                                    hipMemcpyDeviceToHost, s.stream));
     QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
     pend[slot].g0 = g0;
     pend[slot].cnt = cnt;
+    pend[slot].token = token;
     pend[slot].live = true;
     slot = (slot + 1) % kSlots;
   }
   for (int i = 0; i < kSlots; ++i)
     if ((rc = finish((slot + i) % kSlots))) return rc;
-  return collect_error(ctx, ctx->slots[0].stream);
+  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream);
 }
 
 }  // namespace

@@ -45,6 +45,12 @@ struct RaggedArgs {
   const uint64_t* out_off;    // recover
   uint64_t n_groups;
   uint32_t* err;
+  // launch_ragged_latency only (nullptr: none): the last workgroup to finish
+  // stores done_token into done_flag (mapped host memory, system scope) after
+  // every output is visible; done_count is a zeroed device word it resets
+  uint32_t* done_count;
+  uint32_t* done_flag;
+  uint32_t done_token;
 };
 
 // Packet protection batch (qpp_kernels.hip): packet p's associated data (the
@@ -113,6 +119,9 @@ hipError_t launch_entropy_validate(const EntropyValidateArgs& a, hipStream_t s);
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
 hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);
+// Small batches whose payloads are read over PCIe (mapped host memory): one
+// wave per group, all of a group's loads in flight at once.
+hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t s);
 hipError_t launch_stream_probe(const uint8_t* src, uint64_t n, uint8_t* dst, bool copy,
                                hipStream_t s);
 hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);

@@ -818,6 +818,157 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) 
   }
 }
 
+// Ragged CSR, parity-window form — the SMALL-BATCH (latency) kernel: the
+// mapped host path runs a batch of <= kDirectGroups groups with it
+// (qfec_capi.cpp ragged_mapped), where the payloads are read over PCIe and a
+// group's time is its count of dependent round trips, not bandwidth.  (On
+// large device-resident batches it is 0.77x ragged_multi_kernel: the
+// texture-address unit costs ~64 cycles per 64-lane load whatever its useful
+// lanes; tools/tune/tune_rw.hip)
+// One wave per group, lane l owns the parity
+// windows at bytes w0 = min(16l, plen-16) and w1 = min(16(l+64), plen-16) —
+// the fixed-shape kernel's mapping (the last window ends exactly at plen and
+// overlaps its neighbour with identical bytes), so there is no accumulator in
+// LDS, no atomics and no packet search.  The group's packet table is one
+// coalesced vector load (lane r = received packet r); packet r's offset and
+// length are then wave-uniform (v_readlane), and every lane loads the 16 bytes
+// of packet r under its window (a window crossing the packet end loads the 16
+// bytes ending at the packet end and shifts them down; a window past it loads
+// them too — the same lines as the lane that needs them — and XORs zero).
+// Load slots: window w0 of every received packet, then window w1 of the
+// packets that reach one (found by a ballot, walked with s_ff1); PB slots'
+// loads are in flight before the first XOR, independent of one another, so a
+// group costs three dependent round trips (group scalars -> packet table ->
+// all packet bytes) instead of one per 2 KiB (ragged_multi_kernel's flat
+// windows: profiles/round1/sq_stalls_fec_pq.txt, parked 68-78% of cycles).
+// Groups outside the form (more than 64 received packets, a packet < 16 B,
+// any invalid field) run the exact per-group body (ragged_group).
+template <bool RECOVER, bool NT, int PB>
+__device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
+                                             uint32_t* s_par, uint64_t* s_head, u32x4* s_meta) {
+  // trip 1: the group's scalars (s_load)
+  const uint32_t p0 = a.grp_ptr[g];
+  const uint32_t k = a.grp_ptr[g + 1] - p0;
+  uint32_t m = 0xFFFFFFFFu, plen = 0;
+  uint64_t dst_off, par_off = 0;
+  if constexpr (RECOVER) {
+    m = a.missing[g];
+    plen = a.parity_len[g];
+    dst_off = a.out_off[g];
+    par_off = a.parity_off[g];
+  } else {
+    dst_off = a.parity_off[g];
+  }
+  const uint32_t kr = RECOVER ? k - 1u : k;  // received packets
+  const bool form = k >= 1u && k <= 255u && kr <= 64u &&
+                    (!RECOVER || (m < k && plen >= 16u && plen <= kMaxPacket));
+  // trip 2: the packet table (lane r = received packet r) and, for recover,
+  // the parity windows (they need only the scalars)
+  uint32_t len = 0, offlo = 0, offhi = 0;
+  if (form && lane < kr) {
+    const uint32_t p = p0 + lane + (RECOVER && lane >= m ? 1u : 0u);
+    len = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    offlo = (uint32_t)o;
+    offhi = (uint32_t)(o >> 32);
+  }
+  u32x4 acc0 = {0u, 0u, 0u, 0u}, acc1 = {0u, 0u, 0u, 0u};
+  uint32_t w0 = 0, w1 = 0;
+  if (RECOVER && form) {
+    w0 = min(16u * lane, plen - 16u);
+    w1 = min(16u * (lane + 64u), plen - 16u);
+    const uint8_t* prow = a.parity + par_off;
+    acc0 = ld16t<NT>(prow + w0);
+    if (plen > 1024u) acc1 = ld16t<NT>(prow + w1);
+  }
+  const uint32_t lim = RECOVER ? plen : kMaxPacket;
+  if (!form || wave_any(lane < kr && (len < 16u || len > lim))) {
+    GroupPrefetch f;
+    group_scalars<RECOVER>(a, g, f);
+    group_vectors<RECOVER, NT>(a, g, lane, f);
+    ragged_group<RECOVER, NT, 2, 1>(a, g, lane, f, s_par, s_head, s_meta);
+    return;
+  }
+  if constexpr (!RECOVER) {
+    plen = wave_max11(len);
+    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
+    w0 = min(16u * lane, plen - 16u);
+    w1 = min(16u * (lane + 64u), plen - 16u);
+  }
+  // second windows: lanes' w1 >= min(1024, plen - 16), so exactly the packets
+  // longer than that reach one
+  const uint64_t longm = plen > 1024u ? __ballot(lane < kr && len > min(1024u, plen - 16u)) : 0ull;
+  const uint32_t ns = kr + (uint32_t)__popcll(longm);
+  // trip 3: every slot's bytes, PB loads in flight per lane.  Branch-free: a
+  // slot past the end loads through a descriptor of 0 bytes (the bounds check
+  // returns zeros, no memory access), so no load sits in a branch and the
+  // wait counts stay exact (branches made the compiler drain vmcnt before
+  // every load).
+  uint64_t lm = longm;
+  for (uint32_t s = 0; s < ns; s += PB) {
+    u32x4 v[PB];
+    uint32_t li[PB];
+    bool second[PB];
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const uint32_t j = s + (uint32_t)u;
+      const bool valid = j < ns;
+      second[u] = j >= kr;
+      const uint32_t r = second[u] ? (uint32_t)__builtin_ctzll(lm | (1ull << 63)) : min(j, 63u);
+      lm = valid && second[u] ? lm & (lm - 1ull) : lm;
+      li[u] = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)r);
+      const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)r) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)r);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.bytes + o), 0, valid ? 0x7FFFFFFF : 0, 0x00020000);
+      const uint32_t w = second[u] ? w1 : w0;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)min(w, li[u] - 16u), 0, NT ? 2 : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const uint32_t w = second[u] ? w1 : w0;
+      const uint32_t keep = w < li[u] ? 0xFFFFFFFFu : 0u;
+      const uint32_t sh = w + 16u > li[u] ? min(w + 16u - li[u], 15u) : 0u;
+      const u32x4 x = shr_bytes_bf(v[u], sh) & keep;
+      const u32x4 zero = {0u, 0u, 0u, 0u};
+      acc0 ^= second[u] ? zero : x;
+      acc1 ^= second[u] ? x : zero;
+    }
+  }
+  uint8_t* dst = a.out + dst_off;
+  const uint32_t nwin = (plen + 15u) >> 4;
+  if (lane < nwin) st16t<NT>(dst + w0, acc0);
+  if (lane + 64u < nwin) st16t<NT>(dst + w1, acc1);
+}
+
+template <bool RECOVER, bool NT, int PB>
+__global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[kFlatWaves][4 * kParWin];
+  __shared__ uint64_t s_head[kFlatWaves][kParWin];
+  __shared__ u32x4 s_meta[kFlatWaves][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = (uint64_t)blockIdx.x * kFlatWaves + wv;
+  if (g < a.n_groups) window_group<RECOVER, NT, PB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+  if (a.done_flag == nullptr) return;
+  // Completion signal for a host that spins on mapped memory instead of
+  // waiting on an event (~6 us less per small flush, tools/tune/tune_latency):
+  // every thread's stores (outputs in mapped host memory) are made visible
+  // system-wide, the block is counted, and the last block to finish resets
+  // the counter and stores the token into the host-mapped flag.
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.done_count, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(a.done_flag, a.done_token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // out ^= in (XorBuffers).
 // ---------------------------------------------------------------------------
@@ -1025,6 +1176,21 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t s) {
+  if (a.n_groups == 0) return hipSuccess;
+  if (a.n_groups > 0x7FFFFFFFull) return hipErrorInvalidValue;  // small batches only
+  const uint64_t blocks = (a.n_groups + kFlatWaves - 1) / kFlatWaves;
+  // all of a group's loads in flight at once: 16 load slots per lane covers
+  // up to 16 received packets (+ their second windows) in one round trip
+  if (recover)
+    hipLaunchKernelGGL((ragged_window_kernel<true, true, 16>), dim3((uint32_t)blocks),
+                       dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((ragged_window_kernel<false, true, 16>), dim3((uint32_t)blocks),
+                       dim3(kBlock), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_xor_into(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s) {

@@ -5,11 +5,12 @@
 // one FEC group of 10 data packets x 1350 B (QuicFecSender -> one shared
 // QuicFecEncodeBatch), or each have one group with exactly one lost packet and
 // the FEC packet received (QuicFecReceiver -> one shared QuicFecReviveBatch).
-// Timed: ONE Flush of the batch — CSR build, index tables staged to the
-// device, one ragged launch reading the payloads in place from the groups'
-// pinned payload arena (QFEC_PTR_MAPPED) and writing the accumulators back
-// into it, the redundancy / revived-payload views — for N = 1, 64, 4096,
-// 65536 groups.
+// Timed: ONE Flush of the batch — CSR build, one ragged launch reading the
+// payloads in place from the groups' pinned payload arena (QFEC_PTR_MAPPED)
+// and writing the accumulators back into it (up to 256 groups the index
+// tables are read in place as well and completion is a host-mapped flag;
+// above that they are staged to the device), the redundancy /
+// revived-payload views — for N = 1, 64, 4096, 65536 groups.
 // Beside it the CPU FEC path the reference ran on the connection thread:
 // every payload XORed into the group accumulator (the oracle's
 // qo_group_encode / qo_group_recover, word-wise XorBuffers), one core.

@@ -1,3 +1,3 @@
-mkdir -p gpurun_out/anom
-timeout -k 10 240 tools/debug/build/last_vgpr_ops 256 > gpurun_out/anom/last_vgpr_ops.txt 2>&1
+mkdir -p gpurun_out/lat
+timeout -k 10 120 tools/tune/build/tune_flush > gpurun_out/lat/tune_flush_pb32.txt 2>&1
 echo rc=$?
