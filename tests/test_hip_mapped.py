@@ -153,3 +153,44 @@ def test_mapped_multi_chunk(ctx, chunk, monkeypatch):
     _, want_pf = OC.encode_fixed(rows, k, L, nf)
     assert np.array_equal(h_par.array, want_pf)
     assert np.array_equal(h_out.array.reshape(nf, L), rows.reshape(nf, k, L)[np.arange(nf), mf])
+
+
+def _mapped_case(n, g0, kmin=1, kmax=80, lmin=1, lmax=1452, seed=3):
+    """a ragged batch with the latency kernel's edge shapes: k = 1, groups of more
+    than 64 received packets and packets shorter than 16 B (both run the
+    per-group fallback inside ragged_window_kernel), full-length packets."""
+    ks, ptr, ln, off = synth_batch(n, kmin=kmin, kmax=kmax, lmin=lmin, lmax=lmax, g0=g0)
+    data = np.random.default_rng(seed).integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(g0, g0 + n), ks).astype(np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1452)
+    assert rc == 0 and rc2 == 0
+    return dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+                out_off=poff, parity=want_p, recovered=want_o), want_l
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257])
+@pytest.mark.parametrize("shape", ["wide", "short", "full"])
+def test_ragged_mapped_latency_path(ctx, n, shape):
+    """<= 256 groups: tables read in place, ragged_window_kernel, completion by
+    the host-mapped flag (257: the staged path); bit-exact vs the oracle."""
+    kw = {"wide": {}, "short": dict(kmin=2, kmax=12, lmin=1, lmax=40),
+          "full": dict(kmin=10, kmax=10, lmin=1452, lmax=1452)}[shape]
+    z, want_l = _mapped_case(n, g0=1000 + n, **kw)
+    par, plen, out = run_ragged(ctx, z, host="mapped")
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, z["parity"])
+    assert np.array_equal(out, z["recovered"])
+
+
+def test_ragged_mapped_latency_repeated(ctx):
+    """many consecutive small flushes on one context (the completion token
+    advances every call; a stale flag must never release a later call)"""
+    z, want_l = _mapped_case(8, g0=77, kmin=3, kmax=12, lmin=16, lmax=1350)
+    for _ in range(200):
+        par, plen, out = run_ragged(ctx, z, host="mapped")
+        assert np.array_equal(plen, want_l)
+        assert np.array_equal(par, z["parity"])
+        assert np.array_equal(out, z["recovered"])

@@ -1,3 +1,5 @@
-mkdir -p gpurun_out/lat
-timeout -k 10 120 tools/tune/build/tune_flush > gpurun_out/lat/tune_flush_pb32.txt 2>&1
+mkdir -p gpurun_out/full
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > gpurun_out/full/tests.txt 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/full/smoke.txt 2>&1
 echo rc=$?
