@@ -51,6 +51,25 @@ def _code_object(path, tmp):
     return co
 
 
+def private_segments(path):
+    """{kernel: private (scratch) segment bytes} from a library / code object's
+    AMDHSA metadata — a product kernel that spills to scratch is a
+    performance bug (an array in bytes16_at once did: 4x slower)."""
+    with tempfile.TemporaryDirectory() as tmp:
+        co = _code_object(path, tmp)
+        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                               capture_output=True, text=True).stdout
+    out, name = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s*\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+        if m and name:
+            out[name] = int(m.group(1))
+    return out
+
+
 def kernels_co(path):
     """yield (name, vgpr_count, [instruction lines]) from a code object / library."""
     with tempfile.TemporaryDirectory() as tmp:

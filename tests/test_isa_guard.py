@@ -35,3 +35,10 @@ def test_scan_flags_the_round1_pattern(tmp_path):
         "\t.amdhsa_kernel _Zgood\n\t\t.amdhsa_next_free_vgpr 69\n\t.end_amdhsa_kernel\n")
     hits = isa_guard.scan(str(s))
     assert [h[0] for h in hits] == ["_Zbad"]
+
+
+def test_product_kernels_use_no_scratch():
+    """no kernel of libqfec.so spills to scratch (private segment 0 bytes)"""
+    segs = isa_guard.private_segments(LIB)
+    assert len(segs) == len(list(isa_guard.kernels(LIB)))
+    assert {k: v for k, v in segs.items() if v} == {}
