@@ -56,6 +56,21 @@ static void launch_multi(const RaggedArgs& a, uint64_t G) {
                      dim3((uint32_t)((G + per - 1) / per)), dim3(256), 0, 0, a);
 }
 
+// The product kernel at a given number of 4-wave blocks per CU (dynamic LDS
+// padding; 160 KiB per CU): does it run faster with more waves in flight?
+template <bool REC>
+static void launch_multi_occ(const RaggedArgs& a, uint64_t G, int blocks_per_cu) {
+  static size_t stat = 0;
+  if (!stat) {
+    hipFuncAttributes fa;
+    CK(hipFuncGetAttributes(&fa, (const void*)qfec::ragged_multi_kernel<REC, true, 2, 2, 4, false>));
+    stat = fa.sharedSizeBytes;
+  }
+  const size_t pad = (160u << 10) / blocks_per_cu - stat - 256;
+  hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, true, 2, 2, 4, false>),
+                     dim3((uint32_t)((G + 7) / 8)), dim3(256), pad, 0, a);
+}
+
 template <bool REC, int B, bool GATE, int FENCE = 0, int DBG = 0>
 static void launch_flat(const RaggedArgs& a, uint64_t G, size_t pad_lds = 0) {
   // pad_lds: extra dynamic LDS per block (140 KiB: one block = 4 waves per CU)
@@ -155,15 +170,9 @@ int main(int argc, char** argv) {
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
-  vs.push_back({"multi2 align U2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 2, true>(a, G); }});
-  vs.push_back({"multi2 align U1 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 1, true>(a, G); }});
-  vs.push_back({"multi2 align U3 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 3, true>(a, G); }});
-  vs.push_back({"multi3 align U2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 3, true, 2, true>(a, G); }});
+  vs.push_back({"window16 encode", false, [=](const RaggedArgs& a) { launch_win<false, 16>(a, G); }});
   vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
-  vs.push_back({"multi2 align U2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 2, true>(a, G); }});
-  vs.push_back({"multi2 align U1 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 1, true>(a, G); }});
-  vs.push_back({"multi2 align U3 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 3, true>(a, G); }});
-  vs.push_back({"multi3 align U2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 3, true, 2, true>(a, G); }});
+  vs.push_back({"window16 recover", true, [=](const RaggedArgs& a) { launch_win<true, 16>(a, G); }});
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
