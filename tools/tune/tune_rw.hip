@@ -170,30 +170,22 @@ int main(int argc, char** argv) {
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+  vs.push_back({"multi2 pl encode", false, [=](const RaggedArgs& a) {
+                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<false, true, 2, 2, 4, false>),
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
+                }});
+  vs.push_back({"multi2 pl U3 encode", false, [=](const RaggedArgs& a) {
+                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<false, true, 2, 3, 4, false>),
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
+                }});
   vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
-  vs.push_back({"loads-only U2 G2 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 2, 2>),
-                                     dim3((uint32_t)((G + 8 - 1) / 8)), dim3(256), 0, 0, a);
+  vs.push_back({"multi2 pl recover", true, [=](const RaggedArgs& a) {
+                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<true, true, 2, 2, 4, false>),
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
                 }});
-  vs.push_back({"loads-only U4 G2 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 4, 2>),
-                                     dim3((uint32_t)((G + 8 - 1) / 8)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"loads-only U2 G8 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 2, 8>),
-                                     dim3((uint32_t)((G + 32 - 1) / 32)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"loads-only U4 G8 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 4, 8>),
-                                     dim3((uint32_t)((G + 32 - 1) / 32)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"loads-only U2 G32 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 2, 32>),
-                                     dim3((uint32_t)((G + 128 - 1) / 128)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"loads-only U4 G32 (not exact)", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_loads_only_kernel<true, 4, 32>),
-                                     dim3((uint32_t)((G + 128 - 1) / 128)), dim3(256), 0, 0, a);
+  vs.push_back({"multi2 pl U3 recover", true, [=](const RaggedArgs& a) {
+                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<true, true, 2, 3, 4, false>),
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
                 }});
 
   // correctness: each variant's output (and parity lengths) == the product's
