@@ -1,4 +1,3 @@
-mkdir -p gpurun_out/pl
-timeout -k 10 300 tools/tune/build/tune_rw 10 5 > gpurun_out/pl/tune_rw_pl.txt 2>&1 && \
-timeout -k 10 300 tools/tune/build/tune_rw 10 5 5 11 64 400 > gpurun_out/pl/tune_rw_pl_small.txt 2>&1
+mkdir -p gpurun_out/cpol
+timeout -k 10 400 tools/tune/build/place_cpol 5 3 > gpurun_out/cpol/place_cpol.txt 2>&1
 echo rc=$?
