@@ -80,7 +80,7 @@ extern "C" {
 #define QFEC_PTR_MAPPED 4u  /* FEC calls (fixed, ragged, xor_into): the payload
                                buffers (rows / bytes, parity, parity_out / out) are
                                pinned, device-mapped host memory (qfec_host_alloc,
-                               or any hipHostMalloc'd / registered memory) that the
+                               qfec_host_register, or any hipHostMalloc'd memory) that the
                                kernels read and write IN PLACE over PCIe — no
                                staging copy, the packets cross the link once; the
                                index arrays (pkt_off, pkt_len, grp_ptr, parity_off,
@@ -112,6 +112,14 @@ const char* qfec_strerror(int code);
  * where the socket wrote them).  NULL on failure (qfec_last_error(NULL)). */
 void* qfec_host_alloc(size_t bytes);
 void qfec_host_free(void* p);
+/* Pin and device-map EXISTING host memory [p, p + bytes) for QFEC_PTR_MAPPED
+ * calls (e.g. a server's recvmmsg ring allocated by the application), the
+ * registration counterpart of qfec_host_alloc; the memory stays the caller's.
+ * The GPU addresses it at the same virtual address as the host (the mapped
+ * calls pass pointers through unchanged); a platform where that is not so is
+ * refused (QFEC_ERR_INTERNAL).  Unregister before freeing the memory. */
+int qfec_host_register(void* p, size_t bytes);
+int qfec_host_unregister(void* p);
 const char* qfec_last_error(const qfec_ctx* ctx);
 int qfec_abi_version(void);
 

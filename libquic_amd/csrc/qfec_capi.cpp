@@ -407,6 +407,31 @@ void qfec_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
+int qfec_host_register(void* p, size_t bytes) {
+  if (!p || bytes == 0) return fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_register: empty range");
+  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+  if (e != hipSuccess)
+    return fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_register(%p, %zu): %s", p, bytes,
+                hipGetErrorString(e));
+  void* dev = nullptr;
+  e = hipHostGetDevicePointer(&dev, p, 0);
+  if (e != hipSuccess || dev != p) {
+    (void)hipHostUnregister(p);
+    return fail(nullptr, QFEC_ERR_INTERNAL,
+                "qfec_host_register(%p): device address %p differs from the host address (%s); "
+                "QFEC_PTR_MAPPED needs them equal", p, dev, hipGetErrorString(e));
+  }
+  return QFEC_OK;
+}
+
+int qfec_host_unregister(void* p) {
+  const hipError_t e = hipHostUnregister(p);
+  if (e != hipSuccess)
+    return fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_unregister(%p): %s", p,
+                hipGetErrorString(e));
+  return QFEC_OK;
+}
+
 const char* qfec_strerror(int code) {
   switch (code) {
     case QFEC_OK:

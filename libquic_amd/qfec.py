@@ -43,6 +43,8 @@ SIGNATURES = [
     ("qfec_last_error", C.c_char_p, [C.c_void_p]),
     ("qfec_host_alloc", C.c_void_p, [C.c_size_t]),
     ("qfec_host_free", None, [C.c_void_p]),
+    ("qfec_host_register", C.c_int, [C.c_void_p, C.c_size_t]),
+    ("qfec_host_unregister", C.c_int, [C.c_void_p]),
     ("qfec_encode_batch", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint32]),
     ("qfec_recover_batch", C.c_int,
@@ -151,6 +153,35 @@ class HostBuffer:
             self.close()
         except Exception:
             pass
+
+
+class HostRegistration:
+    """Pins and device-maps an existing host buffer (a numpy array, a CPU torch
+    tensor or a raw address + size) for mapped=True calls; unregister() (or the
+    end of a with-block) releases it.  The buffer must outlive the
+    registration."""
+
+    def __init__(self, buf, nbytes=None):
+        self.lib = load()
+        self.ptr = _ptr(buf)
+        self.n = int(nbytes if nbytes is not None else
+                     (buf.nbytes if hasattr(buf, "nbytes") else buf.numel() * buf.element_size()))
+        rc = self.lib.qfec_host_register(self.ptr, self.n)
+        if rc != QFEC_OK:
+            raise QfecError(rc, self.lib.qfec_last_error(None).decode())
+
+    def unregister(self):
+        if self.ptr:
+            rc = self.lib.qfec_host_unregister(self.ptr)
+            self.ptr = None
+            if rc != QFEC_OK:
+                raise QfecError(rc, self.lib.qfec_last_error(None).decode())
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.unregister()
 
 
 def _ptr(x):

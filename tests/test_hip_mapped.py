@@ -194,3 +194,50 @@ def test_ragged_mapped_latency_repeated(ctx):
         assert np.array_equal(plen, want_l)
         assert np.array_equal(par, z["parity"])
         assert np.array_equal(out, z["recovered"])
+
+
+def _page_aligned(a):
+    """a copy of `a` in its own whole pages (two registrations never share a page)"""
+    a = np.ascontiguousarray(a)
+    n = max(a.nbytes, 1)
+    raw = np.zeros(n + 2 * 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    view = raw[off:off + (n + 4095) // 4096 * 4096]
+    out = view[:a.nbytes].view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out  # a view: it keeps `raw` alive
+
+
+def test_registered_host_memory(ctx):
+    """qfec_host_register: an application's own host buffers (numpy arrays here),
+    pinned and device-mapped in place, used by the mapped fixed and ragged
+    paths; bit-exact vs the oracle; unregistered afterwards."""
+    k, L, n = 10, 1350, 3001
+    rows = _page_aligned(OC.synth_fixed(Q.SEED_FIXED, 0, n, k, L))
+    par = _page_aligned(np.zeros(n * L, np.uint8))
+    out = _page_aligned(np.zeros(n * L, np.uint8))
+    miss = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
+    _, want_p = OC.encode_fixed(rows, k, L, n)
+    with qfec.HostRegistration(rows), qfec.HostRegistration(par), qfec.HostRegistration(out):
+        ctx.encode(rows, k, L, n, par, mapped=True)
+        ctx.recover(rows, par, miss, k, L, n, out, mapped=True)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out.reshape(n, L), rows.reshape(n, k, L)[np.arange(n), miss])
+    # ragged, small (latency path) and large (staged tables)
+    for m in (40, 3000):
+        z, want_l = _mapped_case(m, g0=4242 + m, kmin=2, kmax=14, lmin=1, lmax=1452)
+        data = _page_aligned(z["data"])
+        p = _page_aligned(np.zeros(z["parity"].size, np.uint8))
+        o = _page_aligned(np.zeros(z["recovered"].size, np.uint8))
+        plen = np.zeros(m, np.uint16)
+        with qfec.HostRegistration(data), qfec.HostRegistration(p), qfec.HostRegistration(o):
+            ctx.encode_ragged(data, z["pkt_off"], z["pkt_len"], z["grp_ptr"], m, p,
+                              z["parity_off"], plen, mapped=True)
+            ctx.recover_ragged(data, z["pkt_off"], z["pkt_len"], z["grp_ptr"], m, p,
+                               z["parity_off"], plen, z["missing"], o, z["out_off"], mapped=True)
+        assert np.array_equal(plen, want_l)
+        assert np.array_equal(p, z["parity"])
+        assert np.array_equal(o, z["recovered"])
+    # unregistered pageable memory is refused again
+    with pytest.raises(qfec.QfecError, match="QFEC_PTR_MAPPED"):
+        ctx.encode(rows, k, L, n, par, mapped=True)

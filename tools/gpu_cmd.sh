@@ -1,5 +1,4 @@
-mkdir -p gpurun_out/p2d
-timeout -k 10 300 tools/tune/build/place_2d 5 3 > gpurun_out/p2d/run1.txt 2>&1 && \
-timeout -k 10 300 tools/tune/build/place_2d 5 3 > gpurun_out/p2d/run2.txt 2>&1 && \
-timeout -k 10 300 tools/tune/build/place_2d 5 3 > gpurun_out/p2d/run3.txt 2>&1
+mkdir -p gpurun_out/reg
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_hip_mapped.py tests/test_abi.py > gpurun_out/reg/tests.txt 2>&1
 echo rc=$?
