@@ -614,17 +614,35 @@ __device__ __forceinline__ void poly_span_padded(Poly1305& p, const uint8_t* d, 
 
 // Keep only the `rem` bytes of the tail chunk that load_tail put at its top
 // (len >= 16) or bottom (len < 16), moved to bytes [0, rem), zero above.
+// Bytes [o, o+16) of the 32 bytes lo || hi (o in 0..15) in 32-bit lanes: two
+// 2-way dword selects and four v_alignbyte_b32 (no local byte array: indexed
+// by a runtime value, one lived in scratch memory).
+__device__ __forceinline__ u32x4 bytes16_at(u32x4 lo, u32x4 hi, uint32_t o) {
+  const bool b8 = (o & 8u) != 0u, b4 = (o & 4u) != 0u;
+  const uint32_t f0 = b8 ? lo.z : lo.x, f1 = b8 ? lo.w : lo.y, f2 = b8 ? hi.x : lo.z,
+                 f3 = b8 ? hi.y : lo.w, f4 = b8 ? hi.z : hi.x, f5 = b8 ? hi.w : hi.y;
+  const uint32_t g0 = b4 ? f1 : f0, g1 = b4 ? f2 : f1, g2 = b4 ? f3 : f2, g3 = b4 ? f4 : f3,
+                 g4 = b4 ? f5 : f4;
+  const uint32_t r = o & 3u;
+  return u32x4{__builtin_amdgcn_alignbyte(g1, g0, r), __builtin_amdgcn_alignbyte(g2, g1, r),
+               __builtin_amdgcn_alignbyte(g3, g2, r), __builtin_amdgcn_alignbyte(g4, g3, r)};
+}
+
+// The low `rem` bytes of t kept, zero above (rem in 0..16).
+__device__ __forceinline__ u32x4 keep_low_bytes(u32x4 t, uint32_t rem) {
+  const uint32_t k = rem * 8u;
+  const uint32_t m0 = k >= 32u ? ~0u : ((1u << k) - 1u);
+  const uint32_t m1 = k >= 64u ? ~0u : k <= 32u ? 0u : ((1u << (k - 32u)) - 1u);
+  const uint32_t m2 = k >= 96u ? ~0u : k <= 64u ? 0u : ((1u << (k - 64u)) - 1u);
+  const uint32_t m3 = k >= 128u ? ~0u : k <= 96u ? 0u : ((1u << (k - 96u)) - 1u);
+  return u32x4{t.x & m0, t.y & m1, t.z & m2, t.w & m3};
+}
+
 __device__ __forceinline__ u32x4 tail_bytes(u32x4 t, uint32_t len) {
   const uint32_t rem = len & 15u;
-  uint8_t b[16];
-  __builtin_memcpy(b, &t, 16);
-  const uint32_t first = len >= 16u ? 16u - rem : 0u;
-  uint8_t o[16];
-#pragma unroll
-  for (uint32_t i = 0; i < 16u; ++i) o[i] = i < rem ? b[(first + i) & 15u] : (uint8_t)0;
-  u32x4 v;
-  __builtin_memcpy(&v, o, 16);
-  return v;
+  // len >= 16: the rem bytes sit at the top (bytes 16-rem..15): shift them down
+  const u32x4 s = len >= 16u ? bytes16_at(t, u32x4{0u, 0u, 0u, 0u}, (16u - rem) & 15u) : t;
+  return keep_low_bytes(len >= 16u && rem == 0u ? u32x4{0u, 0u, 0u, 0u} : s, rem);
 }
 
 __device__ __forceinline__ u32x4 ks_chunk(const uint32_t (&ks)[16], uint32_t j) {
@@ -632,6 +650,23 @@ __device__ __forceinline__ u32x4 ks_chunk(const uint32_t (&ks)[16], uint32_t j) 
          : j == 1 ? u32x4{ks[4], ks[5], ks[6], ks[7]}
          : j == 2 ? u32x4{ks[8], ks[9], ks[10], ks[11]}
                   : u32x4{ks[12], ks[13], ks[14], ks[15]};
+}
+
+// ks_chunk for a per-lane j (the packet tails): the empty asm pins each word
+// in a VGPR, so the selects stay v_cndmask instead of being folded into one
+// load at a select-chosen address — which puts ks[] in scratch (80 B per
+// lane in the seal/open kernels before this).
+__device__ __forceinline__ u32x4 ks_chunk_lane(const uint32_t (&ks)[16], uint32_t j) {
+  uint32_t k[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    k[i] = ks[i];
+    asm volatile("" : "+v"(k[i]));
+  }
+  const bool b2 = (j & 2u) != 0u, b1 = (j & 1u) != 0u;
+  const u32x4 lo = b2 ? u32x4{k[8], k[9], k[10], k[11]} : u32x4{k[0], k[1], k[2], k[3]};
+  const u32x4 hi = b2 ? u32x4{k[12], k[13], k[14], k[15]} : u32x4{k[4], k[5], k[6], k[7]};
+  return b1 ? hi : lo;
 }
 
 // Transposed read back of the wave's LDS rows into the loading-lane layout.
@@ -754,7 +789,7 @@ __global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
     const uint32_t c = plen >> 4;
     uint32_t ks[16];
     chacha_block(key, 1u + c / 4u, ks);
-    u32x4 ct = tail ^ ks_chunk(ks, c & 3u);
+    u32x4 ct = tail ^ ks_chunk_lane(ks, c & 3u);
     uint8_t b[16];
     __builtin_memcpy(b, &ct, 16);
     for (uint32_t i = rem; i < 16u; ++i) b[i] = 0;  // zero pad for the MAC
@@ -819,7 +854,7 @@ __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
     const uint32_t c = plen >> 4;
     uint32_t ks[16];
     chacha_block(key, 1u + c / 4u, ks);
-    const u32x4 pt = tail ^ ks_chunk(ks, c & 3u);
+    const u32x4 pt = tail ^ ks_chunk_lane(ks, c & 3u);
     uint8_t b[16];
     __builtin_memcpy(b, &pt, 16);
     for (uint32_t i = 0; i < rem; ++i) o[16u * c + i] = b[i];
@@ -1027,13 +1062,20 @@ __device__ __forceinline__ Gf4 gf_mul_x(const Gf4& v) {
 // Bit-serial X * H (SP 800-38D Algorithm 1) for waves with mixed keys.
 __device__ __forceinline__ Gf4 gf_mul_bits(const Gf4& x, const Gf4& h) {
   Gf4 z{{0u, 0u, 0u, 0u}}, v = h;
-  for (int i = 0; i < 128; ++i) {
-    const uint32_t m = 0u - ((x.w[i >> 5] >> (31 - (i & 31))) & 1u);
-    z.w[0] ^= v.w[0] & m;
-    z.w[1] ^= v.w[1] & m;
-    z.w[2] ^= v.w[2] & m;
-    z.w[3] ^= v.w[3] & m;
-    v = gf_mul_x(v);
+  // word loop unrolled, bit loop not: x.w[q] is a constant index (x.w[i >> 5]
+  // in one rolled loop kept x in scratch)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t xw = x.w[q];
+#pragma unroll 1
+    for (int i = 31; i >= 0; --i) {
+      const uint32_t m = 0u - ((xw >> i) & 1u);
+      z.w[0] ^= v.w[0] & m;
+      z.w[1] ^= v.w[1] & m;
+      z.w[2] ^= v.w[2] & m;
+      z.w[3] ^= v.w[3] & m;
+      v = gf_mul_x(v);
+    }
   }
   return z;
 }

@@ -33,71 +33,90 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 SHIFT64 = re.compile(r"^\s*(v_lshlrev_b64|v_lshrrev_b64|v_ashrrev_i64)\s+(v\[\d+:\d+\]),\s*(\S+),")
 
 
-def _code_object(path, tmp):
-    """gfx950 code object of a host library (its .hip_fatbin bundle) or path itself."""
+def _code_objects(path, tmp):
+    """gfx950 code objects of a host library or executable — one per
+    translation unit: its .hip_fatbin section is a concatenation of offload
+    bundles — or [path] for a code object itself."""
     with open(path, "rb") as f:
         if f.read(4) != b"\x7fELF":
             raise ValueError(f"{path}: not ELF")
-    notes = subprocess.run([f"{LLVM}/llvm-readelf", "-h", path], capture_output=True, text=True)
-    if "AMDGPU" in notes.stdout or "EM_AMDGPU" in notes.stdout:
-        return path
+    hdr = subprocess.run([f"{LLVM}/llvm-readelf", "-h", path], capture_output=True, text=True)
+    if "AMDGPU" in hdr.stdout or "EM_AMDGPU" in hdr.stdout:
+        return [path]
     fb = os.path.join(tmp, "fb.bin")
-    co = os.path.join(tmp, "gfx950.co")
     subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fb}", path, os.path.join(tmp, "x")],
                    check=True, capture_output=True)
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"],
-                   check=True, capture_output=True)
-    return co
+    data = open(fb, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = []
+    for i, a in enumerate(starts):
+        b = starts[i + 1] if i + 1 < len(starts) else len(data)
+        part = os.path.join(tmp, f"bundle{i}.bin")
+        with open(part, "wb") as f:
+            f.write(data[a:b])
+        co = os.path.join(tmp, f"gfx950_{i}.co")
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        f"--output={co}"], check=True, capture_output=True)
+        out.append(co)
+    return out
+
+
+def _notes_and_dis(path, dis=True):
+    notes, text = [], []
+    with tempfile.TemporaryDirectory() as tmp:
+        for co in _code_objects(path, tmp):
+            notes.append(subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                                        capture_output=True, text=True).stdout)
+            if dis:
+                text.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True,
+                                           capture_output=True, text=True).stdout)
+    return notes, text
 
 
 def private_segments(path):
     """{kernel: private (scratch) segment bytes} from a library / code object's
     AMDHSA metadata — a product kernel that spills to scratch is a
     performance bug (an array in bytes16_at once did: 4x slower)."""
-    with tempfile.TemporaryDirectory() as tmp:
-        co = _code_object(path, tmp)
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
-                               capture_output=True, text=True).stdout
-    out, name = {}, None
-    for line in notes.splitlines():
-        m = re.match(r"\s*\.name:\s+(\S+)", line)
-        if m:
-            name = m.group(1)
-        m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
-        if m and name:
-            out[name] = int(m.group(1))
+    out = {}
+    for notes in _notes_and_dis(path, dis=False)[0]:
+        name = None
+        for line in notes.splitlines():
+            m = re.match(r"\s*\.name:\s+(\S+)", line)
+            if m:
+                name = m.group(1)
+            m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+            if m and name:
+                out[name] = int(m.group(1))
     return out
 
 
 def kernels_co(path):
-    """yield (name, vgpr_count, [instruction lines]) from a code object / library."""
-    with tempfile.TemporaryDirectory() as tmp:
-        co = _code_object(path, tmp)
-        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True,
-                             text=True).stdout
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
-                               capture_output=True, text=True).stdout
-    vg, name = {}, None
-    for line in notes.splitlines():
-        m = re.match(r"\s*\.name:\s+(\S+)", line)
-        if m:
-            name = m.group(1)
-        m = re.match(r"\s*\.vgpr_count:\s+(\d+)", line)
-        if m and name:
-            vg[name] = int(m.group(1))
-    cur, body = None, []
-    for line in dis.splitlines():
-        m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
-        if m:
-            if cur in vg:
-                yield cur, vg[cur], body
-            cur, body = m.group(1), []
-            continue
-        if cur:
-            body.append(line.split("//")[0].rstrip())
-    if cur in vg:
-        yield cur, vg[cur], body
+    """yield (name, vgpr_count, [instruction lines]) from every code object of
+    a library / executable / code object."""
+    notes_all, dis_all = _notes_and_dis(path)
+    for notes, dis in zip(notes_all, dis_all):
+        vg, name = {}, None
+        for line in notes.splitlines():
+            m = re.match(r"\s*\.name:\s+(\S+)", line)
+            if m:
+                name = m.group(1)
+            m = re.match(r"\s*\.vgpr_count:\s+(\d+)", line)
+            if m and name:
+                vg[name] = int(m.group(1))
+        cur, body = None, []
+        for line in dis.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
+            if m:
+                if cur in vg:
+                    yield cur, vg[cur], body
+                cur, body = m.group(1), []
+                continue
+            if cur:
+                body.append(line.split("//")[0].rstrip())
+        if cur in vg:
+            yield cur, vg[cur], body
 
 
 def kernels(path):
