@@ -46,6 +46,8 @@ def parse(argv=None):
     p.add_argument("--L", type=int, default=1350)
     p.add_argument("--cached", action="store_true",
                    help="default cache policy instead of nt loads/stores")
+    p.add_argument("--one-pass", action="store_true",
+                   help="QFEC_ONE_PASS: the one-pass fixed kernel instead of the phased one")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-ragged", action="store_true")
@@ -158,10 +160,11 @@ class HipFixedWorkload:
     encode (qfec_encode_batch) + single-loss recover (qfec_recover_batch), both
     on `stream`, bracketed by HIP events on that same stream."""
 
-    def __init__(self, torch, dev, g0, G, k, L, cached=False):
+    def __init__(self, torch, dev, g0, G, k, L, cached=False, one_pass=False):
         from libquic_amd import qfec
         self.torch, self.dev, self.g0, self.G, self.k, self.L = torch, dev, g0, G, k, L
         self.cached = cached
+        self.one_pass = one_pass
         self.ctx = qfec.Context(dev.index)
         self.stream = torch.cuda.current_stream()
         self.ctx.set_stream(self.stream)
@@ -181,10 +184,11 @@ class HipFixedWorkload:
         k, L, G = self.k, self.L, self.G
         if ev:
             ev[0].record(self.stream)
-        self.ctx.encode(self.rows, k, L, G, self.par, cached=self.cached)
+        self.ctx.encode(self.rows, k, L, G, self.par, cached=self.cached, one_pass=self.one_pass)
         if ev:
             ev[1].record(self.stream)
-        self.ctx.recover(self.rows, self.par, self.miss, k, L, G, self.out, cached=self.cached)
+        self.ctx.recover(self.rows, self.par, self.miss, k, L, G, self.out, cached=self.cached,
+                         one_pass=self.one_pass)
         if ev:
             ev[2].record(self.stream)
 
@@ -307,8 +311,28 @@ def timed_steps(work, steps, warmup, barrier, reduce_max):
     return elapsed, events
 
 
+def phased_default(G, k, L, args):
+    """Whether the library runs the phased kernel for this batch (the rule of
+    phase_plan in qfec_kernels.hip: nt, L >= 16, at least 8 phases of
+    CUs x 40 steps x floor(256 / ceil(L/16)) groups)."""
+    if args.cached or args.one_pass or args.cpu_workload or L < 16:
+        return False
+    import torch
+    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    per = ncu * 40 * (256 // ((L + 15) // 16))
+    return -(-G // per) >= 8
+
+
+def fixed_kernel_name(k, phased):
+    """The encode kernel the line's roofline is about (libquic_amd/csrc/qfec_kernels.hip)."""
+    if phased:
+        return (f"phase_xor_kernel<{k}, false> (encode, k={k}, nt; one workgroup per CU, "
+                f"reads and parity writes in separate grid-wide phases)")
+    return f"fixed_xor_kernel<{k}, false, true, false, false> (encode, k={k}, nt, one pass)"
+
+
 def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_recover,
-                enc_s=None, rec_s=None, traffic=None, verified=None):
+                enc_s=None, rec_s=None, traffic=None, verified=None, kernel=None):
     """The JSON line (rank 0).  value = algorithmic bytes of ALL ranks / max time.
     enc_s / rec_s: the slowest rank's mean encode / recover launch (seconds)."""
     total = world * steps * (bytes_encode + bytes_recover)
@@ -339,7 +363,7 @@ def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_reco
         rec_gbs = bytes_recover / rec_s / 1e9
         line["roofline"] = {
             "bound": "hbm",
-            "kernel": "fixed_xor_kernel<10, false, true, false, false> (encode, k=10, nt)",
+            "kernel": kernel or fixed_kernel_name(k, False),
             "achieved": round(enc_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -482,7 +506,8 @@ def main(argv=None):
     if cpu:
         work = CpuStandInWorkload(g0, G, k, L)
     else:
-        work = HipFixedWorkload(torch, dev, g0, G, k, L, cached=args.cached)
+        work = HipFixedWorkload(torch, dev, g0, G, k, L, cached=args.cached,
+                                one_pass=args.one_pass)
     elapsed, events = timed_steps(work, args.steps, args.warmup, barrier, reduce_max)
     enc_s, rec_s = work.kernel_seconds(events)
     verified = None if args.no_verify else work.verify()
@@ -494,7 +519,8 @@ def main(argv=None):
     if verified is not None:
         verified = all(r["verified"] for r in per_rank)
     line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
-                       work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified)
+                       work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified,
+                       kernel=fixed_kernel_name(k, phased_default(G, k, L, args)))
     if world > 1 and line["roofline"]:
         fr = [work.bytes_encode / r["enc_s"] / 1e9 / HBM_PEAK_GBS for r in per_rank]
         line["roofline"]["per_rank_frac"] = {"min": round(min(fr), 4), "max": round(max(fr), 4)}
@@ -509,6 +535,20 @@ def main(argv=None):
         # the ragged kernels' launches for the rocprofv3 runs (tools/pmc.sh)
         work.release()
         line["ragged"] = bench_ragged(work.ctx, torch, dev, work.stream, steps=3)
+    if extras and not args.one_pass and phased_default(G, k, L, args):
+        # the same steps with the one-pass kernel (QFEC_ONE_PASS), same buffers
+        work.one_pass = True
+        _, ev1 = timed_steps(work, args.steps, 1, barrier, reduce_max)
+        e1, r1 = work.kernel_seconds(ev1)
+        line["one_pass"] = {
+            "kernel": fixed_kernel_name(k, False),
+            "encode_frac": round(work.bytes_encode / e1 / 1e9 / HBM_PEAK_GBS, 4),
+            "recover_frac": round(work.bytes_recover / r1 / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_us": round(e1 * 1e6, 2), "recover_us": round(r1 * 1e6, 2),
+            "verified": None if args.no_verify else work.verify(),
+            "note": "QFEC_ONE_PASS: the one-pass fixed kernel on the same buffers, same steps "
+                    "(its rate depends on the buffers' DRAM placement, DESIGN.md §4)"}
+        work.one_pass = False
     if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
         if line["roofline"]:  # the encode kernel against this box's measured streaming read

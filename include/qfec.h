@@ -87,6 +87,13 @@ extern "C" {
                                parity_len, missing_idx, out_off, parity_len_out)
                                are ordinary host memory, staged by the call.
                                Returns when the results are in host memory. */
+#define QFEC_ONE_PASS 8u    /* fixed-shape device calls: always the one-pass
+                               kernel.  Without it a large nt batch (>= 8 phases,
+                               about 246K groups at L = 1350 on 256 CUs) runs the
+                               phased kernel: one workgroup per CU, reads and
+                               parity writes in separate grid-wide phases, which
+                               keeps its rate independent of where the buffers
+                               sit in the DRAM.  Same results either way. */
 
 typedef struct qfec_ctx qfec_ctx;
 
@@ -322,6 +329,11 @@ int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_
  * mode 1 = copy src -> dst (nt loads + nt stores).  The measured ceilings the
  * FEC kernels' rates are compared with. */
 int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* dst, int mode);
+/* Number of phased fixed-shape launches on this context that gave up their
+ * grid-wide meetings (a workgroup waited > 200 us: the GPU shared with other
+ * work, so not every workgroup was resident) and ran to the end without them
+ * — same results, one-pass-like speed.  Waits for the context's stream. */
+int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

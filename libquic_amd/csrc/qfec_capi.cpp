@@ -45,6 +45,8 @@ struct Slot {
 
 }  // namespace
 
+constexpr size_t kPhaseSyncBytes = 20 * 256;
+
 struct qfec_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -57,6 +59,9 @@ struct qfec_ctx {
   // small-batch completion (launch_ragged_latency): per-slot device block
   // counters and host-mapped flags the kernel's last workgroup stores to
   uint32_t* d_done = nullptr;
+  // sync words of the phased fixed-shape kernel (20 x 256 B; words 0-18 zero
+  // between launches, word 19 counts abandoned launches)
+  uint32_t* d_phase = nullptr;
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
   uint32_t flag_token = 0;
@@ -532,6 +537,8 @@ qfec_ctx* qfec_create(int device) {
             hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&ctx->d_err, sizeof(uint32_t)) == hipSuccess &&
             hipMemset(ctx->d_err, 0, sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc(&ctx->d_phase, kPhaseSyncBytes) == hipSuccess &&
+            hipMemset(ctx->d_phase, 0, kPhaseSyncBytes) == hipSuccess &&
             hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
   if (!ok) {
     fail(nullptr, QFEC_ERR_INTERNAL, "HIP initialisation failed on device %d", device);
@@ -557,6 +564,7 @@ void qfec_destroy(qfec_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
   }
   if (ctx->d_done) (void)hipFree(ctx->d_done);
+  if (ctx->d_phase) (void)hipFree(ctx->d_phase);
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->h_err) (void)hipHostFree(ctx->h_err);
@@ -607,6 +615,7 @@ int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, ui
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
+  a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
   QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
   return QFEC_OK;
 }
@@ -655,6 +664,7 @@ int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
+  a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
   QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
   return QFEC_OK;
 }
@@ -1338,6 +1348,15 @@ int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* ds
   if (!src || !dst) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
   if (mode != 0 && mode != 1) return fail(ctx, QFEC_ERR_INTERNAL, "probe mode %d", mode);
   QFEC_HIP(ctx, qfec::launch_stream_probe(src, n, dst, mode == 1, ctx->stream));
+  return QFEC_OK;
+}
+
+int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!count) return fail(ctx, QFEC_ERR_INTERNAL, "null count");
+  QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  QFEC_HIP(ctx, hipMemcpy(count, ctx->d_phase + 64 * 19, sizeof(uint32_t), hipMemcpyDeviceToHost));
   return QFEC_OK;
 }
 

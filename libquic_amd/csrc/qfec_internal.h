@@ -16,6 +16,10 @@ enum : uint32_t {
 };
 
 // Fixed-shape encode / recover.  parity == nullptr selects encode.
+// Most workgroups of 256 lanes per launch: an AQL dispatch packet's grid size
+// is a 32-bit count of work-items (2^32 / 256 = 2^24 workgroups).
+constexpr uint64_t kMaxBlocks256 = (1ull << 24) - 1;
+
 struct FixedArgs {
   const uint8_t* rows;
   const uint8_t* parity;   // recover only: parity rows
@@ -29,6 +33,9 @@ struct FixedArgs {
   uint32_t k;
   uint32_t L;
   uint32_t* err;
+  // large nt batches: 19 x 256 B of zeroed sync words for the phased kernel
+  // (phase_xor_kernel); nullptr: always the one-pass fixed kernel
+  uint32_t* phase_sync = nullptr;
 };
 
 struct RaggedArgs {

@@ -174,6 +174,195 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
   st16t<NT>(a.out + g * a.out_stride + off, acc);
 }
 
+// ---------------------------------------------------------------------------
+// Fixed shape, large batches: the same lanes and loads, phased.
+// ---------------------------------------------------------------------------
+// The fixed kernel above runs at 0.69-0.81 of 8 TB/s depending on where the
+// caller's rows and parity buffers sit in the DRAM relative to each other
+// (a property of the (rows, parity) PAIR — the read and write
+// streams meeting in the DRAM).  Here a persistent grid of one workgroup per
+// CU walks the batch in phases: in phase p every workgroup XORs kPhSteps x gpb
+// groups into LDS (160 KiB — the whole CU), the grid meets, every workgroup
+// stores its parity rows, the grid meets again.  The HBM then sees phases of
+// pure reads and pure writes, whatever the placement
+// (tools/tune/tune_phase.hip).
+// The meetings only shape timing: no workgroup reads what another wrote, so
+// every wait is bounded — a workgroup that waits longer than kPhTimeout
+// (e.g. the GPU shared with other work, so not all workgroups are resident)
+// raises an abandon flag and every workgroup stops waiting for the rest of the
+// launch; results are identical either way.
+constexpr int kPhSteps = 40;         // 40 x 256 lanes x 16 B = 160 KiB of LDS
+constexpr int kPhU = 2;              // steps loaded together (2k loads in flight per lane)
+constexpr uint64_t kPhTimeout = 20000;  // s_memrealtime ticks (100 MHz): 200 us
+
+// sync words, 256 B apart: [0] top, [1..16] sub-counters, [17] exits, [18] abandon,
+// [19] abandoned launches so far (never reset: qfec_phase_abandons)
+__device__ __forceinline__ uint32_t* ph_word(uint32_t* ps, uint32_t i) { return ps + 64u * i; }
+
+__device__ __forceinline__ uint32_t ph_load(uint32_t* w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Meeting number `epoch` (1, 2, ...).  A workgroup adds to one of 16
+// sub-counters (one counter for every workgroup cost ~60 us per meeting at
+// 1,024 adders); the last adder of a sub-counter in this epoch, told by the
+// value its add returned, adds to the top counter, which the waiters poll.
+__device__ __forceinline__ void phase_meet(uint32_t* ps, uint32_t epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0 && ph_load(ph_word(ps, 18)) == 0u) {
+    const uint32_t B = gridDim.x, sub = blockIdx.x & 15u, nsub = (B - sub + 15u) / 16u;
+    const uint32_t old =
+        __hip_atomic_fetch_add(ph_word(ps, 1u + sub), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == epoch * nsub)
+      __hip_atomic_fetch_add(ph_word(ps, 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = epoch * min(B, 16u);
+    const uint64_t t0 = wall_clock64();
+    while (ph_load(ph_word(ps, 0)) < target) {
+      if (wall_clock64() - t0 > kPhTimeout) {
+        if (__hip_atomic_fetch_or(ph_word(ps, 18), 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == 0u)  // count abandoned launches
+          __hip_atomic_fetch_add(ph_word(ps, 19), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (ph_load(ph_word(ps, 18)) != 0u) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// The last workgroup out zeroes the sync words for the next launch on the
+// stream (vector atomics; the launch boundary orders them before it).
+__device__ __forceinline__ void phase_exit(uint32_t* ps) {
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(ph_word(ps, 17), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          gridDim.x - 1u) {
+    for (uint32_t i = 0; i < 19u; ++i)
+      __hip_atomic_store(ph_word(ps, i), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int KC, bool RECOVER>
+__global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
+                                                           uint32_t nphase) {
+  __shared__ u32x4 s_par[kPhSteps][kBlock];  // lane tid's parity of each step
+  const uint32_t tid = threadIdx.x, gl = tid / C, t = tid - gl * C;
+  const bool lane_on = gl < gpb;
+  const uint32_t off = min(t * 16u, a.L - 16u);
+  const uint32_t k = KC > 0 ? (uint32_t)KC : a.k;
+  const uint64_t B = gridDim.x;
+  for (uint32_t p = 0; p < nphase; ++p) {
+    // steps i, i+1 of phase p cover one contiguous window of B x 2 gpb groups
+    // (the fixed kernel's sliding window); workgroup b owns 2 gpb of them
+    const uint64_t base = ((uint64_t)p * (kPhSteps / kPhU) * B + blockIdx.x) * (gpb * kPhU) + gl;
+    // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
+    // 32-bit shifts only, kPhSteps <= 64)
+    uint32_t bad_lo = 0, bad_hi = 0;
+    auto gidx = [&](int i) {
+      return base + (uint64_t)(i / kPhU) * B * gpb * kPhU + (uint64_t)(i % kPhU) * gpb;
+    };
+    // recover: the lost-slot indices of the next steps are loaded one
+    // iteration ahead (every row address depends on them)
+    uint32_t m_next[kPhU];
+    if constexpr (RECOVER) {
+#pragma unroll
+      for (int u = 0; u < kPhU; ++u) {
+        const uint64_t g = gidx(u);
+        m_next[u] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
+      }
+    }
+#pragma unroll 1
+    for (int i = 0; i < kPhSteps; i += kPhU) {
+      u32x4 acc[kPhU];
+      uint32_t m[kPhU];
+      const uint8_t* src[kPhU];
+#pragma unroll
+      for (int u = 0; u < kPhU; ++u) {
+        const uint64_t g = gidx(i + u);
+        const bool on = lane_on && g < a.n_groups;
+        src[u] = a.rows + (on ? g : 0) * a.group_stride + off;
+        acc[u] = u32x4{0u, 0u, 0u, 0u};
+        m[u] = k;  // encode: no slot replaced
+        if constexpr (RECOVER) {
+          m[u] = m_next[u];
+          if (m[u] >= k) {
+            if (on) {
+              if (i + u < 32) bad_lo |= 1u << (i + u);
+              else bad_hi |= 1u << (i + u - 32);
+            }
+            m[u] = 0u;  // read something valid; the group is not stored
+          }
+        }
+      }
+      if constexpr (KC > 0) {
+        u32x4 v[kPhU][KC];
+#pragma unroll
+        for (int u = 0; u < kPhU; ++u) {
+          const uint64_t g = gidx(i + u);
+          const uint8_t* par = RECOVER ? a.parity + (lane_on && g < a.n_groups ? g : 0) * a.parity_stride + off
+                                       : nullptr;
+#pragma unroll
+          for (int r = 0; r < KC; ++r) {
+            const uint8_t* q = (RECOVER && (uint32_t)r == m[u]) ? par : src[u] + r * a.row_stride;
+            v[u][r] = ld16t<true>(q);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPhU; ++u)
+#pragma unroll
+          for (int r = 0; r < KC; ++r) acc[u] ^= v[u][r];
+      } else {
+#pragma unroll
+        for (int u = 0; u < kPhU; ++u) {
+          const uint64_t g = gidx(i + u);
+          const uint8_t* par = RECOVER ? a.parity + (lane_on && g < a.n_groups ? g : 0) * a.parity_stride + off
+                                       : nullptr;
+          uint32_t r = 0;
+          for (; r + 8 <= k; r += 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (uint32_t w = 0; w < 8; ++w) {
+              const uint8_t* q = (RECOVER && r + w == m[u]) ? par : src[u] + (r + w) * a.row_stride;
+              v[w] = ld16t<true>(q);
+            }
+#pragma unroll
+            for (uint32_t w = 0; w < 8; ++w) acc[u] ^= v[w];
+          }
+          for (; r < k; ++r) {
+            const uint8_t* q = (RECOVER && r == m[u]) ? par : src[u] + r * a.row_stride;
+            acc[u] ^= ld16t<true>(q);
+          }
+        }
+      }
+      if constexpr (RECOVER) {
+        if (i + kPhU < kPhSteps) {
+#pragma unroll
+          for (int u = 0; u < kPhU; ++u) {
+            const uint64_t g = gidx(i + kPhU + u);
+            m_next[u] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPhU; ++u) s_par[i + u][tid] = acc[u];
+    }
+    if constexpr (RECOVER) {
+      if ((bad_lo | bad_hi) != 0u && t == 0u) atomicOr(a.err, kErrMissingIndex);
+    }
+    phase_meet(a.phase_sync, 2u * p + 1u);
+#pragma unroll 4
+    for (int i = 0; i < kPhSteps; ++i) {
+      const uint64_t g = gidx(i);
+      const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
+      if (lane_on && g < a.n_groups && !skip)
+        st16t<true>(a.out + g * a.out_stride + off, s_par[i][tid]);
+    }
+    phase_meet(a.phase_sync, 2u * p + 2u);
+  }
+  phase_exit(a.phase_sync);
+}
+
 // Fixed shape, L < 16 (degenerate tiny packets): one lane per output byte.
 template <bool RECOVER>
 __global__ __launch_bounds__(kBlock) void fixed_small_kernel(FixedArgs a) {
@@ -1078,13 +1267,56 @@ hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t
   return hipGetLastError();
 }
 
+template <bool RECOVER>
+hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t grid,
+                          uint32_t nphase, hipStream_t s) {
+  switch (a.k) {
+#define QFEC_K_CASE(KV)                                                                     \
+  case KV:                                                                                   \
+    hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C, \
+                       gpb, nphase);                                                         \
+    break;
+    QFEC_K_CASE(2)
+    QFEC_K_CASE(4)
+    QFEC_K_CASE(5)
+    QFEC_K_CASE(8)
+    QFEC_K_CASE(10)
+    QFEC_K_CASE(16)
+#undef QFEC_K_CASE
+    default:
+      hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C,
+                         gpb, nphase);
+  }
+  return hipGetLastError();
+}
+
+// The phased kernel for a batch of at least kPhMinPhases phases (about 246K
+// groups at L = 1350 on 256 CUs): the two meetings per phase cost ~2-3 us
+// each, and below that the one-pass kernel's placement luck matters less
+// than they do.  Returns false when it does not apply.
+constexpr uint32_t kPhMinPhases = 8;
+
+bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    return false;
+  const uint64_t per = (uint64_t)ncu * kPhSteps * gpb;
+  const uint64_t np = (a.n_groups + per - 1) / per;
+  if (np < kPhMinPhases || np > 0xFFFFFFFFull) return false;
+  *grid = (uint32_t)ncu;
+  *nphase = (uint32_t)np;
+  return true;
+}
+
 }  // namespace
 
 hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   const bool recover = a0.parity != nullptr;
   if (a0.n_groups == 0) return hipSuccess;
   if (a0.L < 16u) {
-    const uint64_t maxg = ((uint64_t)1 << 31) * kBlock / a0.L / 2;
+    const uint64_t maxg = kMaxBlocks256 * kBlock / a0.L;  // one lane per output byte
     for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
       FixedArgs a = a0;
       a.n_groups = std::min<uint64_t>(maxg, a0.n_groups - g);
@@ -1106,8 +1338,11 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   }
   const uint32_t C = (a0.L + 15u) / 16u;  // <= 91 for L <= 1452
   const uint32_t gpb = kBlock / C;         // whole groups per workgroup (>= 2)
-  const uint64_t max_blocks = 0x7FFFFFFFull;
-  const uint64_t maxg = max_blocks * gpb;
+  uint32_t grid = 0, nphase = 0;
+  if (a0.phase_sync && nontemporal && phase_plan(a0, gpb, &grid, &nphase))
+    return recover ? launch_phase_k<true>(a0, C, gpb, grid, nphase, s)
+                   : launch_phase_k<false>(a0, C, gpb, grid, nphase, s);
+  const uint64_t maxg = kMaxBlocks256 * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     FixedArgs a = a0;
     a.n_groups = std::min<uint64_t>(maxg, a0.n_groups - g);
@@ -1136,7 +1371,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
 hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
   if (a0.n_groups == 0) return hipSuccess;
   const uint64_t gpb = (kBlock / 64) * kRaggedGPW;  // kRaggedGPW groups per wave
-  const uint64_t maxg = 0x7FFFFFFFull * gpb;
+  const uint64_t maxg = kMaxBlocks256 * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     RaggedArgs a = a0;
     a.n_groups = std::min<uint64_t>(maxg, a0.n_groups - g);
@@ -1165,7 +1400,7 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
 
 hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t s) {
   if (a.n_groups == 0) return hipSuccess;
-  if (a.n_groups > 0x7FFFFFFFull) return hipErrorInvalidValue;  // small batches only
+  if (a.n_groups > kMaxBlocks256) return hipErrorInvalidValue;  // small batches only
   const uint64_t blocks = (a.n_groups + kFlatWaves - 1) / kFlatWaves;
   // all of a group's loads in flight at once: 16 load slots per lane covers
   // up to 16 received packets (+ their second windows) in one round trip
@@ -1202,7 +1437,7 @@ hipError_t launch_synth_fixed(uint8_t* rows, uint32_t k, uint32_t L, uint64_t ro
                               uint64_t group_stride, uint64_t g0, uint64_t n, uint64_t seed,
                               hipStream_t s) {
   const uint64_t total_rows = n * k;
-  const uint64_t chunk = 0x40000000ull;  // rows per launch
+  const uint64_t chunk = kMaxBlocks256;  // rows per launch (one workgroup each)
   for (uint64_t r = 0; r < total_rows; r += chunk) {
     const uint64_t cnt = std::min<uint64_t>(chunk, total_rows - r);
     hipLaunchKernelGGL(synth_fixed_kernel, dim3((uint32_t)cnt), dim3(kBlock), 0, s, rows, k, L,
@@ -1216,7 +1451,7 @@ hipError_t launch_synth_fixed(uint8_t* rows, uint32_t k, uint32_t L, uint64_t ro
 hipError_t launch_synth_ragged(uint8_t* bytes, const uint64_t* pkt_off, const uint16_t* pkt_len,
                                const uint32_t* grp_ptr, uint64_t g0, uint64_t n, uint64_t seed,
                                hipStream_t s) {
-  const uint64_t chunk = 0x40000000ull;
+  const uint64_t chunk = kMaxBlocks256;  // groups per launch (one workgroup each)
   for (uint64_t g = 0; g < n; g += chunk) {
     const uint64_t cnt = std::min<uint64_t>(chunk, n - g);
     hipLaunchKernelGGL(synth_ragged_kernel, dim3((uint32_t)cnt), dim3(kBlock), 0, s, bytes,

@@ -1417,7 +1417,7 @@ aes128gcm_kernel(AeadArgs a) {
 }  // namespace
 
 hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t s) {
-  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
+  const uint64_t chunk = kMaxBlocks256 * kBlock;
   for (uint64_t p = 0; p < a0.n; p += chunk) {
     ProtectArgs a = a0;
     a.n = a0.n - p < chunk ? a0.n - p : chunk;
@@ -1447,7 +1447,7 @@ namespace qfec {
 // (profiles/round1/tune_protect_a4.txt).
 hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t s) {
   constexpr uint32_t SC = 16;
-  const uint64_t chunk = (uint64_t)0x7FFFFFFF * kBlock;
+  const uint64_t chunk = kMaxBlocks256 * kBlock;
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;
     a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;
@@ -1490,7 +1490,7 @@ template <bool OPEN, int BLOCK>
 hipError_t launch_gcm_shape(const AeadArgs& a0, hipStream_t s) {
   constexpr uint32_t SC = BLOCK == 768 ? 4u : 8u;
   constexpr int WPE = BLOCK == 768 ? 3 : 2;
-  const uint64_t chunk = (uint64_t)0x7FFFFFFF * BLOCK;
+  const uint64_t chunk = kMaxBlocks256 * 256u / BLOCK * BLOCK;  // < 2^32 work-items
   for (uint64_t p = 0; p < a0.io.n; p += chunk) {
     AeadArgs a = a0;
     a.io.n = a0.io.n - p < chunk ? a0.io.n - p : chunk;

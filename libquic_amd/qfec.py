@@ -25,6 +25,7 @@ QFEC_PTR_DEVICE = 0
 QFEC_PTR_HOST = 1
 QFEC_CACHED = 2
 QFEC_PTR_MAPPED = 4
+QFEC_ONE_PASS = 8
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
 MAX_GROUP_PACKETS = 255
@@ -87,6 +88,7 @@ SIGNATURES = [
      [_vp, _u8p, _vp, _vp, _u8p, C.c_uint64, _vp, _vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p,
       C.c_uint32]),
     ("qfec_stream_probe", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_int]),
+    ("qfec_phase_abandons", C.c_int, [_vp, _vp]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -124,9 +126,9 @@ def load(path: str = LIB_PATH):
     return _lib
 
 
-def _fl(host=False, mapped=False, cached=False):
+def _fl(host=False, mapped=False, cached=False, one_pass=False):
     return ((QFEC_PTR_HOST if host else 0) | (QFEC_PTR_MAPPED if mapped else 0)
-            | (QFEC_CACHED if cached else 0))
+            | (QFEC_CACHED if cached else 0) | (QFEC_ONE_PASS if one_pass else 0))
 
 
 class HostBuffer:
@@ -249,8 +251,8 @@ class Context:
 
     # -- fixed -------------------------------------------------------------
     def encode(self, rows, k, L, n_groups, parity_out, *, row_stride=None, group_stride=None,
-               parity_stride=None, host=False, cached=False, mapped=False):
-        fl = _fl(host, mapped, cached)
+               parity_stride=None, host=False, cached=False, mapped=False, one_pass=False):
+        fl = _fl(host, mapped, cached, one_pass)
         if row_stride is None and group_stride is None and parity_stride is None:
             rc = self.lib.qfec_encode_batch(self.ctx, _ptr(rows), k, L, n_groups,
                                             _ptr(parity_out), fl)
@@ -264,8 +266,8 @@ class Context:
 
     def recover(self, rows, parity, missing, k, L, n_groups, out, *, row_stride=None,
                 group_stride=None, parity_stride=None, out_stride=None, host=False,
-                cached=False, mapped=False):
-        fl = _fl(host, mapped, cached)
+                cached=False, mapped=False, one_pass=False):
+        fl = _fl(host, mapped, cached, one_pass)
         if row_stride is None and group_stride is None and parity_stride is None \
                 and out_stride is None:
             rc = self.lib.qfec_recover_batch(self.ctx, _ptr(rows), _ptr(parity), _ptr(missing),
@@ -360,6 +362,12 @@ class Context:
                                                       1 if copy else 0))
 
     # -- synthetic inputs ----------------------------------------------------
+    def phase_abandons(self):
+        """Phased fixed-shape launches that gave up their grid-wide meetings."""
+        n = C.c_uint32(0)
+        self._check(self.lib.qfec_phase_abandons(self.ctx, C.byref(n)))
+        return n.value
+
     def synth_fixed(self, rows, k, L, g0, n_groups, seed, *, row_stride=None, group_stride=None):
         rs = L if row_stride is None else row_stride
         gs = k * rs if group_stride is None else group_stride

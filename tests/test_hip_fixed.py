@@ -132,6 +132,19 @@ def test_device_synth_matches_oracle(ctx):
         assert np.array_equal(host(t), OC.synth_fixed(Q.SEED_FIXED, g0, n, k, L))
 
 
+def test_device_synth_many_rows(ctx):
+    """More than 2^24 rows: several synth launches (a dispatch's grid is at most
+    2^32 work-items); sampled groups, the first and the last, vs the oracle."""
+    k, L, n = 5, 17, 4_000_000
+    t = torch.zeros(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(t, k, L, 0, n, Q.SEED_FIXED)
+    h = host(t)
+    for g in [0, 3_355_443, 3_355_444, n - 1] + list(np.random.default_rng(3).choice(n, 16)):
+        g = int(g)
+        assert np.array_equal(h[g * k * L:(g + 1) * k * L],
+                              OC.synth_fixed(Q.SEED_FIXED, g, 1, k, L)), g
+
+
 def test_errors(ctx):
     t = torch.zeros(4096, dtype=torch.uint8, device=DEV)
     with pytest.raises(qfec.InvalidFecData):
