@@ -65,10 +65,16 @@ __device__ __forceinline__ void phase_wait(uint32_t* ctr, uint32_t epoch, uint32
 // A phase is S = R + M steps of 3 groups per block: the first R steps keep
 // their parity in registers (static indices: fully unrolled), the other M in
 // LDS (M <= 40: 160 KiB).  Bigger phases, fewer waits.
-template <int M, int U, int SYNC, int PART = 0, int BS = 256, int R = 0>
+// FLAT: the row pointer passes through an empty asm (generic pointer: flat
+// loads with immediate row offsets); RT: the row stride is a runtime value
+// (kRtStride, as in the product) instead of the constant 1350.
+__device__ uint32_t kRtStride = kL;
+template <int M, int U, int SYNC, int PART = 0, int BS = 256, int R = 0, bool FLAT = true,
+          bool RT = false>
 __global__ __launch_bounds__(BS) void phase_kernel(const uint8_t* rows, uint8_t* out, uint64_t n,
                                                     uint32_t nphase, uint32_t* ctr,
                                                     uint32_t* timeouts) {
+  const uint32_t rstride = RT ? kRtStride : kL;
   constexpr uint32_t kGpb = BS / kC;  // groups per step: 3 (256 lanes), 6, 12 (1,024)
   constexpr int S = R + M;
   static_assert(R % U == 0 && M % U == 0, "steps in units of U");
@@ -89,11 +95,11 @@ __global__ __launch_bounds__(BS) void phase_kernel(const uint8_t* rows, uint8_t*
       for (int u = 0; u < U; ++u) {
         const uint64_t g = base + (uint64_t)(i / U) * B * kGpb * U + (uint64_t)u * kGpb;
         const bool on = lane_on && g < n;
-        const uint8_t* src = rows + (on ? g : 0) * (kK * kL) + off;
-        asm volatile("" : "+v"(src) : : "memory");  // no hoisting across steps
+        const uint8_t* src = rows + (on ? g : 0) * (kK * rstride) + off;
+        if constexpr (FLAT) asm volatile("" : "+v"(src) : : "memory");  // no hoisting across steps
 #pragma unroll
         for (uint32_t r = 0; r < kK; ++r)
-          v[u][r] = PART == 2 ? u32x4{(uint32_t)g, 0u, 0u, 0u} : qfec::ld16t<true>(src + r * kL);
+          v[u][r] = PART == 2 ? u32x4{(uint32_t)g, 0u, 0u, 0u} : qfec::ld16t<true>(src + r * rstride);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -129,6 +135,59 @@ __global__ __launch_bounds__(BS) void phase_kernel(const uint8_t* rows, uint8_t*
     for (int i = R; i < S; ++i) {
       const uint64_t g = gidx(i);
       if (PART != 1 && lane_on && g < n) qfec::st16t<true>(out + g * kL + off, s_acc[i - R][tid]);
+    }
+    if constexpr (SYNC == 2) phase_wait(ctr, 2u * p + 2u, timeouts);
+  }
+}
+
+// Software-pipelined read phase: the next U steps' loads are issued before
+// the current U steps are XORed and stored to LDS, so a wave never drains its
+// loads between steps.
+template <int M, int U, int SYNC, int PART = 0>
+__global__ __launch_bounds__(256) void pipe_kernel(const uint8_t* rows, uint8_t* out, uint64_t n,
+                                                   uint32_t nphase, uint32_t* ctr,
+                                                   uint32_t* timeouts) {
+  constexpr uint32_t kGpb = 3;
+  static_assert(M % U == 0, "steps in units of U");
+  const uint32_t tid = threadIdx.x, gl = tid / kC, t = tid - gl * kC;
+  const bool lane_on = gl < kGpb;
+  const uint32_t off = min(t * 16u, kL - 16u);
+  const uint32_t B = gridDim.x;
+  __shared__ u32x4 s_acc[M][256];
+  for (uint32_t p = 0; p < nphase; ++p) {
+    const uint64_t base = ((uint64_t)p * (M / U) * B + blockIdx.x) * (kGpb * U) + gl;
+    auto issue = [&](int i, u32x4 (&v)[U][kK]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t g = base + (uint64_t)(i / U) * B * kGpb * U + (uint64_t)u * kGpb;
+        const bool on = lane_on && g < n;
+        const uint8_t* src = rows + (on ? g : 0) * (kK * kL) + off;
+#pragma unroll
+        for (uint32_t r = 0; r < kK; ++r) v[u][r] = qfec::ld16t<true>(src + r * kL);
+      }
+    };
+    u32x4 cur[U][kK], nxt[U][kK];
+    issue(0, cur);
+#pragma unroll 1
+    for (int i = 0; i < M; i += U) {
+      if (i + U < M) issue(i + U, nxt);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u32x4 a = cur[u][0];
+#pragma unroll
+        for (uint32_t r = 1; r < kK; ++r) a ^= cur[u][r];
+        s_acc[i + u][tid] = a;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (uint32_t r = 0; r < kK; ++r) cur[u][r] = nxt[u][r];
+    }
+    if constexpr (SYNC >= 1) phase_wait(ctr, SYNC == 2 ? 2u * p + 1u : p + 1u, timeouts);
+#pragma unroll 4
+    for (int i = 0; i < M; ++i) {
+      const uint64_t g = base + (uint64_t)(i / U) * B * kGpb * U + (uint64_t)(i % U) * kGpb;
+      if (PART != 1 && lane_on && g < n) qfec::st16t<true>(out + g * kL + off, s_acc[i][tid]);
     }
     if constexpr (SYNC == 2) phase_wait(ctr, 2u * p + 2u, timeouts);
   }
@@ -181,14 +240,15 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Var> vs = {
-      {"M40 U2 sync2", phase_kernel<40, 2, 2>, 40, 2},
-      {"M40 U2 sync1", phase_kernel<40, 2, 1>, 40, 1},
-      {"M40+R16 U2 sync2", phase_kernel<40, 2, 2, 0, 256, 16>, 56, 2},
-      {"M40+R32 U2 sync2", phase_kernel<40, 2, 2, 0, 256, 32>, 72, 2},
-      {"M40+R32 U2 sync1", phase_kernel<40, 2, 1, 0, 256, 32>, 72, 1},
-      {"M40+R32 U2 nosync ld-only", phase_kernel<40, 2, 0, 1, 256, 32>, 72, 0, 1},
-      {"M40+R32 U2 sync2 ld-only", phase_kernel<40, 2, 2, 1, 256, 32>, 72, 2, 1},
-      {"M40+R32 U2 sync2 st-only", phase_kernel<40, 2, 2, 2, 256, 32>, 72, 2, 2},
+      {"flat const sync2", phase_kernel<40, 2, 2>, 40, 2},
+      {"global const sync2", phase_kernel<40, 2, 2, 0, 256, 0, false, false>, 40, 2},
+      {"flat rt sync2", phase_kernel<40, 2, 2, 0, 256, 0, true, true>, 40, 2},
+      {"global rt sync2", phase_kernel<40, 2, 2, 0, 256, 0, false, true>, 40, 2},
+      {"flat const sync1", phase_kernel<40, 2, 1>, 40, 1},
+      {"flat rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, true, true>, 40, 1},
+      {"global rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, false, true>, 40, 1},
+      {"flat const nosync ld-only", phase_kernel<40, 2, 0, 1>, 40, 0, 1},
+      {"global rt nosync ld-only", phase_kernel<40, 2, 0, 1, 256, 0, false, true>, 40, 0, 1},
   };
   for (auto& v : vs) {
     int bpc = 0;
@@ -211,6 +271,24 @@ int main(int argc, char** argv) {
     a.k = kK;
     a.L = kL;
     a.err = d_err;
+    CK(qfec::launch_fixed(a, true, 0));
+  };
+  uint32_t* psync;
+  CK(hipMalloc(&psync, 20 * 256));
+  CK(hipMemset(psync, 0, 20 * 256));
+  auto product_phased = [&](int i, int j) {
+    qfec::FixedArgs a{};
+    a.rows = rows[i];
+    a.out = par[j];
+    a.row_stride = kL;
+    a.group_stride = kK * kL;
+    a.parity_stride = kL;
+    a.out_stride = kL;
+    a.n_groups = G;
+    a.k = kK;
+    a.L = kL;
+    a.err = d_err;
+    a.phase_sync = psync;
     CK(qfec::launch_fixed(a, true, 0));
   };
   auto launch = [&](const Var& v, int i, int j) {
@@ -236,7 +314,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int NV = (int)vs.size() + 1;
+  const int NV = (int)vs.size() + 2;
   std::vector<std::vector<double>> res(NV * NR * NP);
   for (int r = 0; r < rounds; ++r)
     for (int i = 0; i < NR; ++i)
@@ -249,8 +327,10 @@ int main(int argc, char** argv) {
             if (v < (int)vs.size())
               hipLaunchKernelGGL(vs[v].k, dim3(vs[v].grid), dim3(vs[v].bs), 0, 0, rows[i], par[j], G,
                                  vs[v].nphase, ctr, tmo);
-            else
+            else if (v == (int)vs.size())
               product(i, j);
+            else
+              product_phased(i, j);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -266,7 +346,9 @@ int main(int argc, char** argv) {
     for (int j = 0; j < NP; ++j) std::printf("  r%d/p%d", i, j);
   std::printf("\n");
   for (int v = 0; v < NV; ++v) {
-    std::printf("%-24s", v < (int)vs.size() ? vs[v].name.c_str() : "product fixed_xor_kernel");
+    std::printf("%-24s", v < (int)vs.size()    ? vs[v].name.c_str()
+                         : v == (int)vs.size() ? "product one-pass"
+                                               : "product phased");
     for (int i = 0; i < NR; ++i)
       for (int j = 0; j < NP; ++j) {
         auto x = res[(v * NR + i) * NP + j];
