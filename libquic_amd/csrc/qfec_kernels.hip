@@ -183,8 +183,8 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
 // streams meeting in the DRAM).  Here a persistent grid of one workgroup per
 // CU walks the batch in phases: in phase p every workgroup XORs kPhSteps x gpb
 // groups into LDS (160 KiB — the whole CU), the grid meets, every workgroup
-// stores its parity rows, the grid meets again.  The HBM then sees phases of
-// pure reads and pure writes, whatever the placement
+// stores its parity rows and goes on to the next phase.  The HBM then sees
+// (mostly) separate phases of reads and writes, whatever the placement
 // (tools/tune/tune_phase.hip).
 // The meetings only shape timing: no workgroup reads what another wrote, so
 // every wait is bounded — a workgroup that waits longer than kPhTimeout
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
 // raises an abandon flag and every workgroup stops waiting for the rest of the
 // launch; results are identical either way.
 constexpr int kPhSteps = 40;         // 40 x 256 lanes x 16 B = 160 KiB of LDS
-constexpr int kPhU = 2;              // steps loaded together (2k loads in flight per lane)
+constexpr int kPhUDefault = 1;       // steps loaded together (k loads in flight per lane)
 constexpr uint64_t kPhTimeout = 20000;  // s_memrealtime ticks (100 MHz): 200 us
 
 // sync words, 256 B apart: [0] top, [1..16] sub-counters, [17] exits, [18] abandon,
@@ -243,7 +243,11 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
   }
 }
 
-template <int KC, bool RECOVER>
+// Defaults = the product (tools/tune/tune_phase.hip, profiles/round2/phase/
+// tune_phase8.txt): one meeting per phase, before the stores (MEET2 adds one
+// after them: -3%), one step's k loads in flight per lane (kPhU = 2: -4%);
+// FLAT (row pointers as generic pointers: flat loads) changes nothing.
+template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault>
 __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   __shared__ u32x4 s_par[kPhSteps][kBlock];  // lane tid's parity of each step
@@ -253,8 +257,9 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
   const uint32_t k = KC > 0 ? (uint32_t)KC : a.k;
   const uint64_t B = gridDim.x;
   for (uint32_t p = 0; p < nphase; ++p) {
-    // steps i, i+1 of phase p cover one contiguous window of B x 2 gpb groups
-    // (the fixed kernel's sliding window); workgroup b owns 2 gpb of them
+    // the kPhU steps from i of phase p cover one contiguous window of
+    // B x kPhU gpb groups (the fixed kernel's sliding window); workgroup b
+    // owns kPhU gpb of them
     const uint64_t base = ((uint64_t)p * (kPhSteps / kPhU) * B + blockIdx.x) * (gpb * kPhU) + gl;
     // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
     // 32-bit shifts only, kPhSteps <= 64)
@@ -282,6 +287,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
         const uint64_t g = gidx(i + u);
         const bool on = lane_on && g < a.n_groups;
         src[u] = a.rows + (on ? g : 0) * a.group_stride + off;
+        if constexpr (FLAT) asm volatile("" : "+v"(src[u]));
         acc[u] = u32x4{0u, 0u, 0u, 0u};
         m[u] = k;  // encode: no slot replaced
         if constexpr (RECOVER) {
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
     if constexpr (RECOVER) {
       if ((bad_lo | bad_hi) != 0u && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
-    phase_meet(a.phase_sync, 2u * p + 1u);
+    phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
 #pragma unroll 4
     for (int i = 0; i < kPhSteps; ++i) {
       const uint64_t g = gidx(i);
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
       if (lane_on && g < a.n_groups && !skip)
         st16t<true>(a.out + g * a.out_stride + off, s_par[i][tid]);
     }
-    phase_meet(a.phase_sync, 2u * p + 2u);
+    if constexpr (MEET2) phase_meet(a.phase_sync, 2u * p + 2u);
   }
   phase_exit(a.phase_sync);
 }

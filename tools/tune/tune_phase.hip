@@ -240,15 +240,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Var> vs = {
-      {"flat const sync2", phase_kernel<40, 2, 2>, 40, 2},
-      {"global const sync2", phase_kernel<40, 2, 2, 0, 256, 0, false, false>, 40, 2},
       {"flat rt sync2", phase_kernel<40, 2, 2, 0, 256, 0, true, true>, 40, 2},
-      {"global rt sync2", phase_kernel<40, 2, 2, 0, 256, 0, false, true>, 40, 2},
-      {"flat const sync1", phase_kernel<40, 2, 1>, 40, 1},
       {"flat rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, true, true>, 40, 1},
       {"global rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, false, true>, 40, 1},
-      {"flat const nosync ld-only", phase_kernel<40, 2, 0, 1>, 40, 0, 1},
-      {"global rt nosync ld-only", phase_kernel<40, 2, 0, 1, 256, 0, false, true>, 40, 0, 1},
+      {"global rt sync1 U1", phase_kernel<40, 1, 1, 0, 256, 0, false, true>, 40, 1},
   };
   for (auto& v : vs) {
     int bpc = 0;
@@ -291,6 +286,48 @@ int main(int argc, char** argv) {
     a.phase_sync = psync;
     CK(qfec::launch_fixed(a, true, 0));
   };
+  // the product's phase_xor_kernel instantiated directly: MEET2 x FLAT
+  using PK = void (*)(qfec::FixedArgs, uint32_t, uint32_t, uint32_t);
+  std::vector<std::pair<std::string, PK>> pks = {
+      {"prod meet2 global", qfec::phase_xor_kernel<10, false, true, false>},
+      {"prod meet1 global", qfec::phase_xor_kernel<10, false, false, false>},
+      {"prod meet2 U1", qfec::phase_xor_kernel<10, false, true, false, 1>},
+      {"prod meet1 U1", qfec::phase_xor_kernel<10, false, false, false, 1>},
+      {"prod recover meet2 U2", qfec::phase_xor_kernel<10, true, true, false, 2>},
+      {"prod recover meet1 U1", qfec::phase_xor_kernel<10, true, false, false, 1>},
+  };
+  pks.push_back({"prod recover one-pass", nullptr});
+  uint8_t* d_miss;
+  CK(hipMalloc(&d_miss, G));
+  {
+    std::vector<uint8_t> hm(G);
+    for (uint64_t g = 0; g < G; ++g) hm[g] = (uint8_t)((g * 2654435761u >> 7) % kK);
+    CK(hipMemcpy(d_miss, hm.data(), G, hipMemcpyHostToDevice));
+  }
+  const uint32_t pnph = (uint32_t)((G + (uint64_t)ncu * 40 * 3 - 1) / ((uint64_t)ncu * 40 * 3));
+  auto prod_variant = [&](int w, int i, int j) {
+    qfec::FixedArgs a{};
+    a.rows = rows[i];
+    a.out = par[j];
+    a.row_stride = kL;
+    a.group_stride = kK * kL;
+    a.parity_stride = kL;
+    a.out_stride = kL;
+    a.n_groups = G;
+    a.k = kK;
+    a.L = kL;
+    a.err = d_err;
+    a.phase_sync = psync;
+    if (pks[w].first.find("recover") != std::string::npos) {
+      a.parity = par[(j + 1) % NP];
+      a.missing = d_miss;
+    }
+    if (!pks[w].second) a.phase_sync = nullptr;
+    if (pks[w].second)
+      hipLaunchKernelGGL(pks[w].second, dim3(ncu), dim3(256), 0, 0, a, 85u, 3u, pnph);
+    else
+      CK(qfec::launch_fixed(a, true, 0));  // one-pass (no phase_sync)
+  };
   auto launch = [&](const Var& v, int i, int j) {
     CK(hipMemsetAsync(ctr, 0, 17 * 256, 0));
     hipLaunchKernelGGL(v.k, dim3(v.grid), dim3(v.bs), 0, 0, rows[i], par[j], G, v.nphase, ctr, tmo);
@@ -310,11 +347,25 @@ int main(int argc, char** argv) {
       if (h) std::printf("%s rows%d: %u differing words\n", v.name.c_str(), i, h);
     }
   }
+  for (int i = 0; i < NR; ++i) {
+    product(i, 0);
+    CK(hipMemcpy(want, par[0], par_b, hipMemcpyDeviceToDevice));
+    for (int w = 0; w < (int)pks.size(); ++w) {
+      if (pks[w].first.find("recover") != std::string::npos) continue;  // tests/test_hip_phase.py
+      CK(hipMemset(par[1], 0, par_b));
+      prod_variant(w, i, 1);
+      CK(hipMemset(bad, 0, 4));
+      hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, par[1], want, par_b, bad);
+      uint32_t h = 0;
+      CK(hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost));
+      if (h) std::printf("%s rows%d: %u differing words\n", pks[w].first.c_str(), i, h);
+    }
+  }
   std::printf("exactness checked (silence = every variant equals the product)\n");
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int NV = (int)vs.size() + 2;
+  const int NV = (int)vs.size() + 2 + (int)pks.size();
   std::vector<std::vector<double>> res(NV * NR * NP);
   for (int r = 0; r < rounds; ++r)
     for (int i = 0; i < NR; ++i)
@@ -329,8 +380,10 @@ int main(int argc, char** argv) {
                                  vs[v].nphase, ctr, tmo);
             else if (v == (int)vs.size())
               product(i, j);
-            else
+            else if (v == (int)vs.size() + 1)
               product_phased(i, j);
+            else
+              prod_variant(v - (int)vs.size() - 2, i, j);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -346,9 +399,10 @@ int main(int argc, char** argv) {
     for (int j = 0; j < NP; ++j) std::printf("  r%d/p%d", i, j);
   std::printf("\n");
   for (int v = 0; v < NV; ++v) {
-    std::printf("%-24s", v < (int)vs.size()    ? vs[v].name.c_str()
-                         : v == (int)vs.size() ? "product one-pass"
-                                               : "product phased");
+    std::printf("%-24s", v < (int)vs.size()        ? vs[v].name.c_str()
+                         : v == (int)vs.size()     ? "product one-pass"
+                         : v == (int)vs.size() + 1 ? "product phased"
+                                                   : pks[v - vs.size() - 2].first.c_str());
     for (int i = 0; i < NR; ++i)
       for (int j = 0; j < NP; ++j) {
         auto x = res[(v * NR + i) * NP + j];
