@@ -247,10 +247,12 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // tune_phase8.txt): one meeting per phase, before the stores (MEET2 adds one
 // after them: -3%), one step's k loads in flight per lane (kPhU = 2: -4%);
 // FLAT (row pointers as generic pointers: flat loads) changes nothing.
-template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault>
-__global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
+template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
+          int STEPS = kPhSteps, int NTHR = kBlock>
+__global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
-  __shared__ u32x4 s_par[kPhSteps][kBlock];  // lane tid's parity of each step
+  static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
+  __shared__ u32x4 s_par[STEPS][NTHR];  // lane tid's parity of each step
   const uint32_t tid = threadIdx.x, gl = tid / C, t = tid - gl * C;
   const bool lane_on = gl < gpb;
   const uint32_t off = min(t * 16u, a.L - 16u);
@@ -260,9 +262,9 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
     // the kPhU steps from i of phase p cover one contiguous window of
     // B x kPhU gpb groups (the fixed kernel's sliding window); workgroup b
     // owns kPhU gpb of them
-    const uint64_t base = ((uint64_t)p * (kPhSteps / kPhU) * B + blockIdx.x) * (gpb * kPhU) + gl;
+    const uint64_t base = ((uint64_t)p * (STEPS / kPhU) * B + blockIdx.x) * (gpb * kPhU) + gl;
     // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
-    // 32-bit shifts only, kPhSteps <= 64)
+    // 32-bit shifts only, STEPS <= 64)
     uint32_t bad_lo = 0, bad_hi = 0;
     auto gidx = [&](int i) {
       return base + (uint64_t)(i / kPhU) * B * gpb * kPhU + (uint64_t)(i % kPhU) * gpb;
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
       }
     }
 #pragma unroll 1
-    for (int i = 0; i < kPhSteps; i += kPhU) {
+    for (int i = 0; i < STEPS; i += kPhU) {
       u32x4 acc[kPhU];
       uint32_t m[kPhU];
       const uint8_t* src[kPhU];
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
         }
       }
       if constexpr (RECOVER) {
-        if (i + kPhU < kPhSteps) {
+        if (i + kPhU < STEPS) {
 #pragma unroll
           for (int u = 0; u < kPhU; ++u) {
             const uint64_t g = gidx(i + kPhU + u);
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void phase_xor_kernel(FixedArgs a, uint32_t
     }
     phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
 #pragma unroll 4
-    for (int i = 0; i < kPhSteps; ++i) {
+    for (int i = 0; i < STEPS; ++i) {
       const uint64_t g = gidx(i);
       const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
       if (lane_on && g < a.n_groups && !skip)

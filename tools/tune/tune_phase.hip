@@ -240,9 +240,6 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Var> vs = {
-      {"flat rt sync2", phase_kernel<40, 2, 2, 0, 256, 0, true, true>, 40, 2},
-      {"flat rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, true, true>, 40, 1},
-      {"global rt sync1", phase_kernel<40, 2, 1, 0, 256, 0, false, true>, 40, 1},
       {"global rt sync1 U1", phase_kernel<40, 1, 1, 0, 256, 0, false, true>, 40, 1},
   };
   for (auto& v : vs) {
@@ -289,12 +286,12 @@ int main(int argc, char** argv) {
   // the product's phase_xor_kernel instantiated directly: MEET2 x FLAT
   using PK = void (*)(qfec::FixedArgs, uint32_t, uint32_t, uint32_t);
   std::vector<std::pair<std::string, PK>> pks = {
-      {"prod meet2 global", qfec::phase_xor_kernel<10, false, true, false>},
-      {"prod meet1 global", qfec::phase_xor_kernel<10, false, false, false>},
-      {"prod meet2 U1", qfec::phase_xor_kernel<10, false, true, false, 1>},
-      {"prod meet1 U1", qfec::phase_xor_kernel<10, false, false, false, 1>},
-      {"prod recover meet2 U2", qfec::phase_xor_kernel<10, true, true, false, 2>},
-      {"prod recover meet1 U1", qfec::phase_xor_kernel<10, true, false, false, 1>},
+      {"prod (256 x 40)", qfec::phase_xor_kernel<10, false>},
+      {"prod 128 x 80", qfec::phase_xor_kernel<10, false, false, false, 1, 80, 128>},
+      {"prod 192 x 53", qfec::phase_xor_kernel<10, false, false, false, 1, 53, 192>},
+      {"prod 256 x 32", qfec::phase_xor_kernel<10, false, false, false, 1, 32, 256>},
+      {"prod recover (256 x 40)", qfec::phase_xor_kernel<10, true>},
+      {"prod recover 192 x 53", qfec::phase_xor_kernel<10, true, false, false, 1, 53, 192>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
@@ -323,8 +320,20 @@ int main(int argc, char** argv) {
       a.missing = d_miss;
     }
     if (!pks[w].second) a.phase_sync = nullptr;
+    // geometry from the name: threads x steps, blocks per CU
+    uint32_t nt = 256, st = 40, bpc = 1;
+    if (pks[w].first.find("512 x 20") != std::string::npos) nt = 512, st = 20;
+    if (pks[w].first.find("1024 x 10") != std::string::npos) nt = 1024, st = 10;
+    if (pks[w].first.find("256 x 20") != std::string::npos) st = 20, bpc = 2;
+    if (pks[w].first.find("256 x 32") != std::string::npos) st = 32;
+    if (pks[w].first.find("128 x 80") != std::string::npos) nt = 128, st = 80;
+    if (pks[w].first.find("192 x 53") != std::string::npos) nt = 192, st = 53;
+    const uint32_t gpb = nt / 85u, grid = ncu * bpc;
+    const uint64_t per = (uint64_t)grid * st * gpb;
+    const uint32_t nph = (uint32_t)((G + per - 1) / per);
+    (void)pnph;
     if (pks[w].second)
-      hipLaunchKernelGGL(pks[w].second, dim3(ncu), dim3(256), 0, 0, a, 85u, 3u, pnph);
+      hipLaunchKernelGGL(pks[w].second, dim3(grid), dim3(nt), 0, 0, a, 85u, gpb, nph);
     else
       CK(qfec::launch_fixed(a, true, 0));  // one-pass (no phase_sync)
   };
