@@ -378,12 +378,16 @@ def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_reco
     return line
 
 
-def measured_traffic(G, k, L):
+def measured_traffic(G, k, L, phased=False):
+    """PMC bytes per encode launch (tools/pmc.sh -> profiles/traffic_latest.json),
+    when that run measured this shape with the same kernel (phased or one-pass)."""
     tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("groups") == G and tj.get("k") == k and tj.get("L") == L:
+        names = " ".join(tj.get("kernels", {}).get("encode", []))
+        same_kernel = ("phase_xor_kernel" in names) == phased if names else not phased
+        if tj.get("groups") == G and tj.get("k") == k and tj.get("L") == L and same_kernel:
             return tj.get("encode_hbm_bytes_per_launch")
     return None
 
@@ -519,7 +523,8 @@ def main(argv=None):
     if verified is not None:
         verified = all(r["verified"] for r in per_rank)
     line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
-                       work.bytes_recover, enc_s, rec_s, measured_traffic(G, k, L), verified,
+                       work.bytes_recover, enc_s, rec_s,
+                       measured_traffic(G, k, L, phased_default(G, k, L, args)), verified,
                        kernel=fixed_kernel_name(k, phased_default(G, k, L, args)))
     if world > 1 and line["roofline"]:
         fr = [work.bytes_encode / r["enc_s"] / 1e9 / HBM_PEAK_GBS for r in per_rank]

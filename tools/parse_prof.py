@@ -20,14 +20,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kind(name):
-    """fixed_xor_kernel<K, RECOVER, NT, SM> / ragged_multi_kernel<RECOVER, NT, ...>."""
-    m = re.search(r"fixed_xor_kernel<(-?\d+), (true|false)", name)
+    """fixed_xor_kernel<K, RECOVER, NT, SM> / phase_xor_kernel<K, RECOVER, ...> (the
+    product's fixed-shape kernels: one-pass and phased) / ragged_multi_kernel<RECOVER, NT, ...>."""
+    m = re.search(r"(?:fixed|phase)_xor_kernel<(-?\d+), (true|false)", name)
     if m:
         return "recover" if m.group(2) == "true" else "encode"
     m = re.search(r"ragged_(?:multi|xor)_kernel<(true|false)", name)
     if m:
         return "ragged_recover" if m.group(1) == "true" else "ragged_encode"
     return None
+
+
+KERNELS = {}
 
 
 def pmc(run_dir, counter):
@@ -42,6 +46,8 @@ def pmc(run_dir, counter):
                 k = kind(row.get("Kernel_Name", ""))
                 if k:
                     vals.setdefault(k, []).append(float(row["Counter_Value"]))
+                    kn = re.search(r"(\w+_kernel<[^()]*>)", row.get("Kernel_Name", ""))
+                    KERNELS.setdefault(k, set()).add(kn.group(1) if kn else row.get("Kernel_Name", ""))
     return vals
 
 
@@ -78,6 +84,7 @@ def main(run_dir, groups=1 << 20, k=10, L=1350):
                 out[f"ragged_{kd}_write_bytes"] = w
                 out[f"ragged_{kd}_algorithmic_bytes"] = alg
                 out[f"ragged_{kd}_traffic_over_algorithmic"] = (f + w) / alg
+    out["kernels"] = {k: sorted(v) for k, v in KERNELS.items()}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w") as fh:
         json.dump(out, fh, indent=1)
