@@ -821,25 +821,21 @@ __device__ __forceinline__ T sel_n(const T (&v)[N], uint32_t j) {
   return r;
 }
 
-template <bool RECOVER, bool NT, int GPW, int U = 2, int WAVES = kFlatWaves, bool BF = false>
-__global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) {
-  constexpr int ACC = 1;
-  constexpr uint32_t kAccWords = 4 * kParWin;
-  __shared__ uint32_t s_par[WAVES][GPW * kAccWords];
-  __shared__ uint64_t s_head[WAVES][kParWin];
-  __shared__ u32x4 s_meta[WAVES][64];
-  const uint32_t lane = lane_id();
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g0 = ((uint64_t)blockIdx.x * WAVES + wv) * GPW;
-  if (g0 >= a.n_groups) return;
-  const uint32_t ng = (uint32_t)min<uint64_t>((uint64_t)GPW, a.n_groups - g0);
-  uint32_t* par = s_par[wv];
-  uint64_t* head = s_head[wv];
-  u32x4* meta = s_meta[wv];
+// GPW groups g0 .. g0+ng-1 of one wave, up to their XOR into the LDS
+// accumulators `par` (GPW x kAccWords).  Returns false when the groups took
+// the per-group body (odd packets, invalid fields, > 64 received packets):
+// then their outputs are already stored; true: ragged_pair_store writes them
+// from `par` with lengths pl[] at offsets doff[].
+constexpr uint32_t kAccWords = 4 * kParWin;
 
+template <bool RECOVER, bool NT, int GPW, int U, bool BF>
+__device__ __forceinline__ bool ragged_pair_xor(const RaggedArgs& a, uint64_t g0, uint32_t ng,
+                                                uint32_t lane, uint32_t* par, uint64_t* head,
+                                                u32x4* meta, uint32_t (&pl)[GPW],
+                                                uint64_t (&doff)[GPW]) {
+  constexpr int ACC = 1;
   // wave-uniform group scalars
-  uint32_t kb[GPW + 1], rb[GPW + 1], mm[GPW], pl[GPW];
-  uint64_t doff[GPW];
+  uint32_t kb[GPW + 1], rb[GPW + 1], mm[GPW];
   const uint32_t P0 = a.grp_ptr[g0];
   bool ok = true;
   kb[0] = rb[0] = 0;
@@ -919,7 +915,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) 
       ragged_group<RECOVER, NT, U, ACC, BF>(a, g0 + j, lane, f, par, head, meta);
       wave_lds_order();
     }
-    return;
+    return false;
   }
   const uint32_t n = (len + 15u) >> 4;
   const uint32_t incl = wave_incl_scan(n, lane);
@@ -971,6 +967,14 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) 
       if (lane == 0 && (uint32_t)j < ng) a.parity_len_out[g0 + j] = (uint16_t)pl[j];
     }
   }
+  return true;
+}
+
+template <bool NT, int GPW>
+__device__ __forceinline__ void ragged_pair_store(const RaggedArgs& a, uint32_t ng, uint32_t lane,
+                                                  const uint32_t* par, const uint32_t (&pl)[GPW],
+                                                  const uint64_t (&doff)[GPW]) {
+  constexpr int ACC = 1;
   wave_lds_order();  // every lane's XORs done
   // write-out, flattened over the groups' output windows
   uint32_t ob[GPW + 1];
@@ -998,6 +1002,23 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) 
       st16t<NT>(dst + plen - 16u, bytes16_at(lo, hi, o));
     }
   }
+}
+
+template <bool RECOVER, bool NT, int GPW, int U = 2, int WAVES = kFlatWaves, bool BF = false>
+__global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[WAVES][GPW * kAccWords];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * WAVES + wv) * GPW;
+  if (g0 >= a.n_groups) return;
+  const uint32_t ng = (uint32_t)min<uint64_t>((uint64_t)GPW, a.n_groups - g0);
+  uint32_t pl[GPW];
+  uint64_t doff[GPW];
+  if (ragged_pair_xor<RECOVER, NT, GPW, U, BF>(a, g0, ng, lane, s_par[wv], s_head[wv], s_meta[wv],
+                                                pl, doff))
+    ragged_pair_store<NT, GPW>(a, ng, lane, s_par[wv], pl, doff);
 }
 
 // Ragged CSR, parity-window form — the SMALL-BATCH (latency) kernel: the

@@ -296,7 +296,8 @@ class Context:
         rc = self.lib.qfec_recover_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                           _ptr(grp_ptr), n_groups, _ptr(parity),
                                           _ptr(parity_off), _ptr(parity_len), _ptr(missing),
-                                          _ptr(out), _ptr(out_off), _fl(host, mapped))
+                                          _ptr(out), _ptr(out_off),
+                                          _fl(host, mapped))
         return self._check(rc)
 
     def xor_into(self, src, n, dst, *, host=False, mapped=False):

@@ -250,3 +250,64 @@ def test_ragged_pair_boundaries(ctx, host):
     assert np.array_equal(plen, want_l)
     assert np.array_equal(par, want_p)
     assert np.array_equal(out, want_o)
+
+
+def test_ragged_large_batch_odd_groups(ctx):
+    """A large device batch (~213K groups) with odd groups mixed in (> 64
+    received packets and packets < 16 B take the per-group body of
+    ragged_multi_kernel): parity, lengths and revived packets against the
+    oracle on sampled groups, the odd ones among them."""
+    n = 212_992 + 333
+    gs = np.arange(n, dtype=np.uint64)
+    ks = Q.ragged_k(Q.SEED_RAGGED, gs, 5, 15)
+    rng = np.random.default_rng(11)
+    big = rng.choice(n, 40, replace=False)
+    ks[big] = rng.integers(65, 200, big.size)  # > 64 received packets
+    ptr = np.zeros(n + 1, np.uint32)
+    ptr[1:] = np.cumsum(ks)
+    gidx = np.repeat(gs, ks)
+    iidx = np.arange(ptr[-1]) - np.repeat(ptr[:-1].astype(np.int64), ks)
+    ln = Q.ragged_len(Q.SEED_RAGGED, gidx, iidx, 64, 1350).astype(np.uint16)
+    short = rng.choice(ln.size, 300, replace=False)
+    ln[short] = rng.integers(1, 16, short.size)  # packets below 16 B
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    total = int(off[-1] + ln[-1])
+    data = torch.empty(total, dtype=torch.uint8, device=DEV)
+    d_off, d_ln, d_ptr = dview(off), dview(ln), dview(ptr)
+    ctx.synth_ragged(data, d_off, d_ln, d_ptr, 0, n, Q.SEED_RAGGED)
+    miss = Q.drop_index(Q.SEED_DROP, gs, ks).astype(np.uint8)
+    poff = gs * np.uint64(1460) + np.uint64(5)
+    d_poff, d_miss = dview(poff), dview(miss)
+    size = n * 1460 + 5
+    pp = torch.full((size,), 0xA5, dtype=torch.uint8, device=DEV)
+    pl = torch.zeros(n, dtype=torch.int16, device=DEV)
+    ctx.encode_ragged(data, d_off, d_ln, d_ptr, n, pp, d_poff, pl)
+    po = torch.full((size,), 0x5A, dtype=torch.uint8, device=DEV)
+    ctx.recover_ragged(data, d_off, d_ln, d_ptr, n, pp, d_poff, pl, d_miss, po, d_poff)
+    ctx.sync()
+    torch.cuda.synchronize()
+    # oracle on sampled groups (the big and short ones among them)
+    data_h = data.cpu().numpy()
+    par_h, plen_h, out_h = pp.cpu().numpy(), pl.cpu().numpy().view(np.uint16), po.cpu().numpy()
+    pg = np.searchsorted(ptr, short, side="right") - 1
+    sample = np.unique(np.concatenate([big[:10], pg[:20], rng.choice(n, 40, replace=False),
+                                       [0, n - 1]]))
+    for g in sample:
+        g = int(g)
+        a, b = int(ptr[g]), int(ptr[g + 1])
+        sub_ln = ln[a:b].copy()
+        sub_data = np.concatenate([data_h[int(off[q]):int(off[q]) + int(ln[q])] for q in range(a, b)])
+        sub_off = np.zeros(b - a, np.uint64)
+        sub_off[1:] = np.cumsum(sub_ln[:-1].astype(np.uint64))
+        sub_ptr = np.array([0, b - a], np.uint32)
+        zp = np.zeros(1, np.uint64)
+        rc, wp, wl = OC.encode_ragged(sub_data, sub_off, sub_ln, sub_ptr, zp, 1460)
+        rc2, wo = OC.recover_ragged(sub_data, sub_off, sub_ln, sub_ptr, wp, zp, wl,
+                                    miss[g:g + 1], zp, 1460)
+        assert rc == 0 and rc2 == 0
+        L = int(wl[0])
+        assert int(plen_h[g]) == L, g
+        o = int(poff[g])
+        assert np.array_equal(par_h[o:o + L], wp[:L]), g
+        assert np.array_equal(out_h[o:o + L], wo[:L]), g

@@ -170,23 +170,30 @@ int main(int argc, char** argv) {
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
-  vs.push_back({"multi2 pl encode", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<false, true, 2, 2, 4, false>),
-                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"multi2 pl U3 encode", false, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<false, true, 2, 3, 4, false>),
-                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
-                }});
+  // phased (ragged_phase_kernel): waves per CU x slots per wave
+  uint32_t* psync;
+  CK(hipMalloc(&psync, 20 * 256));
+  CK(hipMemset(psync, 0, 20 * 256));
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+#define RG_PHASE(REC, W, S, BPC)                                                                \
+  vs.push_back({std::string("phase W" #W " S" #S " x" #BPC " ") + (REC ? "recover" : "encode"), \
+                REC, [=](const RaggedArgs& a0) {                                                \
+                  const uint64_t per = (uint64_t)ncu * BPC * W * S * 2;                         \
+                  hipLaunchKernelGGL((qfec::ragged_phase_kernel<REC, S, W>), dim3(ncu * BPC),   \
+                                     dim3(64 * W), 0, 0, a0, (uint32_t)((G + per - 1) / per),  \
+                                     psync);                                                    \
+                }})
+  RG_PHASE(false, 4, 13, 1);
+  RG_PHASE(false, 8, 6, 1);
+  RG_PHASE(false, 12, 3, 1);
+  RG_PHASE(false, 16, 2, 1);
+  RG_PHASE(false, 16, 1, 2);
+  RG_PHASE(false, 8, 2, 3);
   vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
-  vs.push_back({"multi2 pl recover", true, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<true, true, 2, 2, 4, false>),
-                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
-                }});
-  vs.push_back({"multi2 pl U3 recover", true, [=](const RaggedArgs& a) {
-                  hipLaunchKernelGGL((qfec::ragged_multi_pl_kernel<true, true, 2, 3, 4, false>),
-                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a);
-                }});
+  RG_PHASE(true, 16, 2, 1);
+  RG_PHASE(true, 16, 1, 2);
+#undef RG_PHASE
 
   // correctness: each variant's output (and parity lengths) == the product's
   std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
