@@ -30,6 +30,7 @@
 #include "qfec_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace qfec {
 namespace {
@@ -248,7 +249,7 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // after them: -3%), one step's k loads in flight per lane (kPhU = 2: -4%);
 // FLAT (row pointers as generic pointers: flat loads) changes nothing.
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
-          int STEPS = kPhSteps, int NTHR = kBlock>
+          int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
@@ -262,7 +263,10 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     // the kPhU steps from i of phase p cover one contiguous window of
     // B x kPhU gpb groups (the fixed kernel's sliding window); workgroup b
     // owns kPhU gpb of them
-    const uint64_t base = ((uint64_t)p * (STEPS / kPhU) * B + blockIdx.x) * (gpb * kPhU) + gl;
+    // XCDW: the workgroups of one XCD (b, b+8, ...) take one contiguous share
+    // of the window, so the lines two neighbouring groups share stay in one L2
+    const uint64_t wb = XCDW ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t base = ((uint64_t)p * (STEPS / kPhU) * B + wb) * (gpb * kPhU) + gl;
     // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
     // 32-bit shifts only, STEPS <= 64)
     uint32_t bad_lo = 0, bad_hi = 0;
@@ -1331,10 +1335,14 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     return false;
-  const uint64_t per = (uint64_t)ncu * kPhSteps * gpb;
+  // test hook (tests/test_hip_phase.py): extra workgroups beyond one per CU
+  // cannot all be resident, so the first meeting times out — the abandon path
+  const char* extra = std::getenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS");
+  const int ex = extra ? std::max(0, std::min(64, std::atoi(extra))) : 0;
+  const uint64_t per = (uint64_t)(ncu + ex) * kPhSteps * gpb;
   const uint64_t np = (a.n_groups + per - 1) / per;
   if (np < kPhMinPhases || np > 0xFFFFFFFFull) return false;
-  *grid = (uint32_t)ncu;
+  *grid = (uint32_t)(ncu + ex);
   *nphase = (uint32_t)np;
   return true;
 }

@@ -158,3 +158,70 @@ def test_phased_repeated_and_rate(ctx):
         assert torch.equal(pars[0], pars[1]) and torch.equal(pars[1], pars[2])
     assert ctx.phase_abandons() == before
     assert times[False] < 1.2 * times[True], times
+
+
+def test_phased_concurrent_launches(ctx):
+    """Two phased launches on two streams of two contexts (each wants every
+    CU's whole LDS, so they cannot both be resident) produce the one-pass
+    kernel's bytes; a later launch on the same context meets normally."""
+    k, L, n = 10, 1350, 1 << 19
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    want = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    ctx.encode(rows, k, L, n, want, one_pass=True)
+    ctx.sync()
+    torch.cuda.synchronize()
+    ctx2 = qfec.Context(0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros(n * L, dtype=torch.uint8, device=DEV) for _ in range(4)]
+    try:
+        ctx.set_stream(s1)
+        ctx2.set_stream(s2)
+        a0, b0 = ctx.phase_abandons(), ctx2.phase_abandons()
+        for r in range(2):
+            ctx.encode(rows, k, L, n, outs[2 * r])
+            ctx2.encode(rows, k, L, n, outs[2 * r + 1])
+        ctx.sync()
+        ctx2.sync()
+        torch.cuda.synchronize()
+        for o in outs:
+            assert torch.equal(o, want)
+        print(f"abandoned launches: {ctx.phase_abandons() - a0} + {ctx2.phase_abandons() - b0}")
+        # alone again: meets normally
+        a1 = ctx.phase_abandons()
+        ctx.encode(rows, k, L, n, outs[0])
+        ctx.sync()
+        torch.cuda.synchronize()
+        assert ctx.phase_abandons() == a1
+        assert torch.equal(outs[0], want)
+    finally:
+        ctx.set_stream(torch.cuda.current_stream())
+        ctx2.close()
+
+
+def test_phased_abandon_path(ctx, monkeypatch):
+    """More workgroups than CUs (test hook): the extra one is not resident
+    until another exits, so the first meeting times out, the launch raises its
+    abandon flag and runs to the end without meetings — same bytes as the
+    one-pass kernel, counted once by qfec_phase_abandons; the next launch
+    (sync words reset by the last workgroup out) meets normally."""
+    k, L, n = 10, 1350, 1 << 19
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    want = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    ctx.encode(rows, k, L, n, want, one_pass=True)
+    out = torch.zeros(n * L, dtype=torch.uint8, device=DEV)
+    a0 = ctx.phase_abandons()
+    monkeypatch.setenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS", "1")
+    ctx.encode(rows, k, L, n, out)
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert ctx.phase_abandons() == a0 + 1
+    assert torch.equal(out, want)
+    monkeypatch.delenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS")
+    out.zero_()
+    ctx.encode(rows, k, L, n, out)
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert ctx.phase_abandons() == a0 + 1
+    assert torch.equal(out, want)

@@ -287,11 +287,9 @@ int main(int argc, char** argv) {
   using PK = void (*)(qfec::FixedArgs, uint32_t, uint32_t, uint32_t);
   std::vector<std::pair<std::string, PK>> pks = {
       {"prod (256 x 40)", qfec::phase_xor_kernel<10, false>},
-      {"prod 128 x 80", qfec::phase_xor_kernel<10, false, false, false, 1, 80, 128>},
-      {"prod 192 x 53", qfec::phase_xor_kernel<10, false, false, false, 1, 53, 192>},
-      {"prod 256 x 32", qfec::phase_xor_kernel<10, false, false, false, 1, 32, 256>},
+      {"prod xcd-window", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, true>},
       {"prod recover (256 x 40)", qfec::phase_xor_kernel<10, true>},
-      {"prod recover 192 x 53", qfec::phase_xor_kernel<10, true, false, false, 1, 53, 192>},
+      {"prod recover xcd-window", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, true>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
