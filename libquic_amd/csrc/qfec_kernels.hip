@@ -247,11 +247,15 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // Defaults = the product (tools/tune/tune_phase.hip, profiles/round2/phase/
 // tune_phase8.txt): one meeting per phase, before the stores (MEET2 adds one
 // after them: -3%), one step's k loads in flight per lane (kPhU = 2: -4%);
-// FLAT (row pointers as generic pointers: flat loads) changes nothing.
+// FLAT (row pointers as generic pointers: flat loads) changes nothing; XCDW
+// (XCD-aware order in the window) +0.5% encode / -3% recover; PARFIRST
+// (recover, templated k: the phase's parity rows first, then only the
+// received rows) +2.7% recover (tune_phase12.txt).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
-          int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false>
+          int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
+  constexpr bool PF = RECOVER && PARFIRST && KC > 0;
   static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
   __shared__ u32x4 s_par[STEPS][NTHR];  // lane tid's parity of each step
   const uint32_t tid = threadIdx.x, gl = tid / C, t = tid - gl * C;
@@ -283,6 +287,23 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         m_next[u] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
       }
     }
+    if constexpr (PF) {
+      // PARFIRST: the phase's parity rows first, into the accumulators (one
+      // stream over the parity buffer), then the received rows only
+#pragma unroll 1
+      for (int i = 0; i < STEPS; i += 8) {
+        u32x4 w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint64_t g = gidx(i + j < STEPS ? i + j : 0);
+          const bool on = i + j < STEPS && lane_on && g < a.n_groups;
+          w[j] = ld16t<true>(a.parity + (on ? g : 0) * a.parity_stride + off);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (i + j < STEPS) s_par[i + j][tid] = w[j];
+      }
+    }
 #pragma unroll 1
     for (int i = 0; i < STEPS; i += kPhU) {
       u32x4 acc[kPhU];
@@ -307,7 +328,20 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
           }
         }
       }
-      if constexpr (KC > 0) {
+      if constexpr (PF) {
+#pragma unroll
+        for (int u = 0; u < kPhU; ++u) {
+          u32x4 v[KC];
+#pragma unroll
+          for (int r = 0; r < KC; ++r) {
+            v[r] = u32x4{0u, 0u, 0u, 0u};
+            if ((uint32_t)r != m[u]) v[r] = ld16t<true>(src[u] + r * a.row_stride);
+          }
+          acc[u] = s_par[i + u][tid];
+#pragma unroll
+          for (int r = 0; r < KC; ++r) acc[u] ^= v[r];
+        }
+      } else if constexpr (KC > 0) {
         u32x4 v[kPhU][KC];
 #pragma unroll
         for (int u = 0; u < kPhU; ++u) {

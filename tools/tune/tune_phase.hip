@@ -287,9 +287,8 @@ int main(int argc, char** argv) {
   using PK = void (*)(qfec::FixedArgs, uint32_t, uint32_t, uint32_t);
   std::vector<std::pair<std::string, PK>> pks = {
       {"prod (256 x 40)", qfec::phase_xor_kernel<10, false>},
-      {"prod xcd-window", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, true>},
       {"prod recover (256 x 40)", qfec::phase_xor_kernel<10, true>},
-      {"prod recover xcd-window", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, true>},
+      {"prod recover parity-first", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
