@@ -215,7 +215,7 @@ struct Var {
 };
 
 int main(int argc, char** argv) {
-  const uint64_t G = 1 << 20;
+  const uint64_t G = argc > 3 ? strtoull(argv[3], nullptr, 10) : (1 << 20);
   const uint64_t rows_b = G * kK * kL, par_b = G * kL;
   const int reps = argc > 1 ? atoi(argv[1]) : 5, rounds = argc > 2 ? atoi(argv[2]) : 3;
   const int NR = 2, NP = 3;
@@ -240,7 +240,6 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Var> vs = {
-      {"global rt sync1 U1", phase_kernel<40, 1, 1, 0, 256, 0, false, true>, 40, 1},
   };
   for (auto& v : vs) {
     int bpc = 0;
