@@ -28,13 +28,15 @@ def phase_groups(L):
     return ncu * STEPS * (256 // ((L + 15) // 16))
 
 
-def sample_vs_oracle(rows_seed, par_h, out_h, miss_np, k, L, n, ps=None, os_=None, count=48):
+def sample_vs_oracle(rows3, par_h, out_h, miss_np, k, L, n, ps=None, os_=None, count=48):
+    """rows3: the device rows as [n][k][>= L]; sampled groups' rows go through
+    the oracle's encode, the revived row must equal the lost row."""
     ps = ps or L
     os_ = os_ or L
     rng = np.random.default_rng(n + k + L)
     for g in list(rng.choice(n, count, replace=False)) + [0, n - 1]:
         g = int(g)
-        rr = OC.synth_fixed(rows_seed, g, 1, k, L)
+        rr = np.ascontiguousarray(rows3[g, :, :L].cpu().numpy()).ravel()
         _, pp = OC.encode_fixed(rr, k, L, 1)
         assert np.array_equal(par_h[g * ps:g * ps + L], pp), g
         m = int(miss_np[g])
@@ -61,11 +63,16 @@ def run_both(ctx, rows, miss, k, L, n, ps=None, os_=None, **strides):
     return res
 
 
-@pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (16, 1452), (2, 100), (5, 17)])
+@pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
+                                 (5, 17), (2, 16)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
-    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    if n <= 1 << 24:
+        ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    else:  # beyond the synthetic generator's group index range
+        rows.copy_(torch.randint(0, 256, (n * k * L,), dtype=torch.uint8, device=DEV,
+                                 generator=torch.Generator(device=DEV).manual_seed(k * L)))
     miss_np = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
     miss = torch.from_numpy(miss_np).to(DEV)
     before = ctx.phase_abandons()
@@ -80,7 +87,7 @@ def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     for i in range(k):
         acc ^= r3[:, i]
     assert not bool(acc.any())
-    sample_vs_oracle(Q.SEED_FIXED, pp.cpu().numpy(), po.cpu().numpy(), miss_np, k, L, n)
+    sample_vs_oracle(r3, pp.cpu().numpy(), po.cpu().numpy(), miss_np, k, L, n)
 
 
 def test_phased_strided(ctx):
@@ -101,7 +108,7 @@ def test_phased_strided(ctx):
     # the padding between rows is never written
     assert bool((pp.view(n, ps)[:, L:] == 0xA5).all())
     assert bool((po.view(n, os_)[:, L:] == 0x5A).all())
-    sample_vs_oracle(Q.SEED_FIXED, pp.cpu().numpy(), po.cpu().numpy(), miss_np, k, L, n,
+    sample_vs_oracle(rows, pp.cpu().numpy(), po.cpu().numpy(), miss_np, k, L, n,
                      ps=ps, os_=os_)
 
 
