@@ -65,6 +65,10 @@ struct qfec_ctx {
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
   uint32_t flag_token = 0;
+  // device scratch of the host-pointer xor / protection / entropy calls:
+  // grow-only buffers kept for the context's life (no allocation per call)
+  std::vector<void*> scratch_p;
+  std::vector<size_t> scratch_n;
 };
 
 namespace {
@@ -565,6 +569,8 @@ void qfec_destroy(qfec_ctx* ctx) {
   }
   if (ctx->d_done) (void)hipFree(ctx->d_done);
   if (ctx->d_phase) (void)hipFree(ctx->d_phase);
+  for (void* q : ctx->scratch_p)
+    if (q) (void)hipFree(q);
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->h_err) (void)hipHostFree(ctx->h_err);
@@ -690,12 +696,33 @@ namespace {
 // call: the slots' device and pinned buffers (ensure_staging) are reused.
 // Only exactly what the device path writes is written: parity_len[g] bytes
 // per group (+ parity_len_out on encode).
-struct DevBuf {  // scoped device allocation (the protection / entropy host paths)
+struct DevBuf {  // a device buffer of a host-pointer call (from the context's scratch)
   void* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
 };
+
+// The i-th scratch buffer of a host-pointer call, at least `bytes` long.
+// Host-pointer calls are synchronous and a context is used by one thread, so
+// the next call may reuse every buffer; a buffer only grows (x2).
+hipError_t scratch(qfec_ctx* ctx, size_t i, size_t bytes, void** out) {
+  if (ctx->scratch_p.size() <= i) {
+    ctx->scratch_p.resize(i + 1, nullptr);
+    ctx->scratch_n.resize(i + 1, 0);
+  }
+  if (ctx->scratch_n[i] < bytes) {
+    if (ctx->scratch_p[i]) {
+      hipError_t e = hipFree(ctx->scratch_p[i]);
+      ctx->scratch_p[i] = nullptr;
+      ctx->scratch_n[i] = 0;
+      if (e != hipSuccess) return e;
+    }
+    const size_t want = std::max<size_t>({bytes, 2 * ctx->scratch_n[i], 4096});
+    hipError_t e = hipMalloc(&ctx->scratch_p[i], want);
+    if (e != hipSuccess) return e;
+    ctx->scratch_n[i] = want;
+  }
+  *out = ctx->scratch_p[i];
+  return hipSuccess;
+}
 
 struct RaggedChunk {
   uint64_t g0 = 0, n = 0;
@@ -1107,8 +1134,9 @@ int qfec_xor_into(qfec_ctx* ctx, const uint8_t* in, uint64_t n, uint8_t* out, ui
   }
   if (flags & QFEC_PTR_HOST) {
     DevBuf d_in, d_out;
-    QFEC_HIP(ctx, hipMalloc(&d_in.p, n));
-    QFEC_HIP(ctx, hipMalloc(&d_out.p, n));
+    size_t si = 0;
+    QFEC_HIP(ctx, scratch(ctx, si++, n, &d_in.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, n, &d_out.p));
     QFEC_HIP(ctx, hipMemcpyAsync(d_in.p, in, n, hipMemcpyHostToDevice, ctx->stream));
     QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, out, n, hipMemcpyHostToDevice, ctx->stream));
     QFEC_HIP(ctx, qfec::launch_xor_into(static_cast<const uint8_t*>(d_in.p), n,
@@ -1157,13 +1185,14 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
   }
   hipStream_t st = ctx->stream;
   DevBuf d_bytes, d_aoff, d_alen, d_ioff, d_ilen, d_out, d_ooff, d_ok;
-  QFEC_HIP(ctx, hipMalloc(&d_bytes.p, std::max<uint64_t>(hi - lo, 1)));
-  QFEC_HIP(ctx, hipMalloc(&d_aoff.p, n * 8));
-  QFEC_HIP(ctx, hipMalloc(&d_alen.p, n * 2));
-  QFEC_HIP(ctx, hipMalloc(&d_ioff.p, n * 8));
-  QFEC_HIP(ctx, hipMalloc(&d_ilen.p, n * 2));
-  QFEC_HIP(ctx, hipMalloc(&d_out.p, std::max<uint64_t>(ohi - olo, 1)));
-  QFEC_HIP(ctx, hipMalloc(&d_ooff.p, n * 8));
+  size_t si = 0;
+  QFEC_HIP(ctx, scratch(ctx, si++, std::max<uint64_t>(hi - lo, 1), &d_bytes.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, n * 8, &d_aoff.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, n * 2, &d_alen.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, n * 8, &d_ioff.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, n * 2, &d_ilen.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, std::max<uint64_t>(ohi - olo, 1), &d_out.p));
+  QFEC_HIP(ctx, scratch(ctx, si++, n * 8, &d_ooff.p));
   QFEC_HIP(ctx, hipMemcpyAsync(d_bytes.p, bytes + lo, hi - lo, hipMemcpyHostToDevice, st));
   QFEC_HIP(ctx, hipMemcpyAsync(d_aoff.p, aoff.data(), n * 8, hipMemcpyHostToDevice, st));
   QFEC_HIP(ctx, hipMemcpyAsync(d_alen.p, ad_len, n * 2, hipMemcpyHostToDevice, st));
@@ -1172,7 +1201,7 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
   QFEC_HIP(ctx, hipMemcpyAsync(d_ooff.p, ooff.data(), n * 8, hipMemcpyHostToDevice, st));
   // seed the output span with the caller's bytes (gaps and failed packets stay)
   QFEC_HIP(ctx, hipMemcpyAsync(d_out.p, out + olo, ohi - olo, hipMemcpyHostToDevice, st));
-  if (decrypt) QFEC_HIP(ctx, hipMalloc(&d_ok.p, n));
+  if (decrypt) QFEC_HIP(ctx, scratch(ctx, si++, n, &d_ok.p));
   qfec::ProtectArgs a{};
   a.bytes = static_cast<const uint8_t*>(d_bytes.p);
   a.ad_off = static_cast<const uint64_t*>(d_aoff.p);
@@ -1188,16 +1217,16 @@ int protect_host(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
     for (uint64_t p = 0; p < n; ++p) nkeys = std::max(nkeys, aead->key_idx[p] + 1u);
     DevBuf d_keys, d_pre, d_kidx, d_pn, d_path;
     const uint64_t ksz = aead->aes ? 16ull : 32ull;
-    QFEC_HIP(ctx, hipMalloc(&d_keys.p, ksz * nkeys));
-    QFEC_HIP(ctx, hipMalloc(&d_pre.p, 4ull * nkeys));
-    QFEC_HIP(ctx, hipMalloc(&d_kidx.p, n * 4));
-    QFEC_HIP(ctx, hipMalloc(&d_pn.p, n * 8));
+    QFEC_HIP(ctx, scratch(ctx, si++, ksz * nkeys, &d_keys.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, 4ull * nkeys, &d_pre.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, n * 4, &d_kidx.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, n * 8, &d_pn.p));
     QFEC_HIP(ctx, hipMemcpyAsync(d_keys.p, aead->keys, ksz * nkeys, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_pre.p, aead->prefixes, 4ull * nkeys, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_kidx.p, aead->key_idx, n * 4, hipMemcpyHostToDevice, st));
     QFEC_HIP(ctx, hipMemcpyAsync(d_pn.p, aead->packet_number, n * 8, hipMemcpyHostToDevice, st));
     if (aead->path_id) {
-      QFEC_HIP(ctx, hipMalloc(&d_path.p, n));
+      QFEC_HIP(ctx, scratch(ctx, si++, n, &d_path.p));
       QFEC_HIP(ctx, hipMemcpyAsync(d_path.p, aead->path_id, n, hipMemcpyHostToDevice, st));
     }
     qfec::AeadArgs aa{};
@@ -1395,14 +1424,15 @@ int qfec_entropy_cumulative_batch(qfec_ctx* ctx, const uint8_t* entropy, const u
   if (flags & QFEC_PTR_HOST) {
     const uint64_t n = conn_ptr[n_conns];
     DevBuf d_e, d_ptr, d_base, d_cum;
-    QFEC_HIP(ctx, hipMalloc(&d_e.p, n + 1));
-    QFEC_HIP(ctx, hipMalloc(&d_ptr.p, 8 * (n_conns + 1)));
-    QFEC_HIP(ctx, hipMalloc(&d_cum.p, n + 1));
+    size_t si = 0;
+    QFEC_HIP(ctx, scratch(ctx, si++, n + 1, &d_e.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, 8 * (n_conns + 1), &d_ptr.p));
+    QFEC_HIP(ctx, scratch(ctx, si++, n + 1, &d_cum.p));
     QFEC_HIP(ctx, hipMemcpyAsync(d_e.p, entropy, n, hipMemcpyHostToDevice, ctx->stream));
     QFEC_HIP(ctx, hipMemcpyAsync(d_ptr.p, conn_ptr, 8 * (n_conns + 1), hipMemcpyHostToDevice,
                                  ctx->stream));
     if (cum_base) {
-      QFEC_HIP(ctx, hipMalloc(&d_base.p, n_conns));
+      QFEC_HIP(ctx, scratch(ctx, si++, n_conns, &d_base.p));
       QFEC_HIP(ctx, hipMemcpyAsync(d_base.p, cum_base, n_conns, hipMemcpyHostToDevice,
                                    ctx->stream));
     }
@@ -1439,6 +1469,7 @@ int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_
   if (flags & QFEC_PTR_HOST) {
     const uint64_t n = n_conns ? conn_ptr[n_conns] : 0, nr = range_ptr[n_acks];
     DevBuf d_cum, d_ptr, d_first, d_base, d_conn, d_larg, d_claim, d_rptr, d_lo, d_hi, d_ok;
+    size_t si = 0;
     struct In {
       DevBuf* d;
       const void* h;
@@ -1450,11 +1481,11 @@ int qfec_entropy_validate_batch(qfec_ctx* ctx, const uint8_t* cum, const uint64_
                {&d_lo, range_lo, 8 * nr},      {&d_hi, range_hi, 8 * nr}};
     for (auto& i : ins) {
       if (!i.h) continue;
-      QFEC_HIP(ctx, hipMalloc(&i.d->p, i.bytes + 8));
+      QFEC_HIP(ctx, scratch(ctx, si++, i.bytes + 8, &i.d->p));
       if (i.bytes)
         QFEC_HIP(ctx, hipMemcpyAsync(i.d->p, i.h, i.bytes, hipMemcpyHostToDevice, ctx->stream));
     }
-    QFEC_HIP(ctx, hipMalloc(&d_ok.p, n_acks));
+    QFEC_HIP(ctx, scratch(ctx, si++, n_acks, &d_ok.p));
     a.cum = static_cast<const uint8_t*>(d_cum.p);
     a.conn_ptr = static_cast<const uint64_t*>(d_ptr.p);
     a.first_pn = static_cast<const uint64_t*>(d_first.p);

@@ -289,3 +289,15 @@ def test_xor_into(ctx):
             hb = b.copy()
             ctx.xor_into(a, n, hb, host=True)
             assert np.array_equal(hb, a ^ b)
+
+
+def test_xor_into_host_scratch_reuse(ctx):
+    """Host-pointer calls run on the context's grow-only device scratch:
+    growing, shrinking and growing again sizes keep every result exact."""
+    rng = np.random.default_rng(6)
+    for n in [10, 3_000_001, 50, 17, 5_000_000, 1, 3_000_001]:
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        hb = b.copy()
+        ctx.xor_into(a, n, hb, host=True)
+        assert np.array_equal(hb, a ^ b), n
