@@ -526,6 +526,9 @@ def main(argv=None):
                        work.bytes_recover, enc_s, rec_s,
                        measured_traffic(G, k, L, phased_default(G, k, L, args)), verified,
                        kernel=fixed_kernel_name(k, phased_default(G, k, L, args)))
+    if line["roofline"] and not cpu and phased_default(G, k, L, args):
+        # phased launches that gave up their meetings (should be 0 on an idle GPU)
+        line["roofline"]["phase_abandons"] = work.ctx.phase_abandons()
     if world > 1 and line["roofline"]:
         fr = [work.bytes_encode / r["enc_s"] / 1e9 / HBM_PEAK_GBS for r in per_rank]
         line["roofline"]["per_rank_frac"] = {"min": round(min(fr), 4), "max": round(max(fr), 4)}
