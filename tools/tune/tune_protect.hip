@@ -53,6 +53,92 @@ __global__ void fnv_valu_chunk_kernel(uint32_t bytes, uint32_t* sink) {
   if ((h.x0 ^ h.x1 ^ h.x2 ^ h.x3) == 0x12345678u) sink[0] = h.x0;
 }
 
+// the same with two independent packets per lane (ILP 2): does a lane's
+// serial FNV chain leave the VALU idle at the 2 waves/SIMD the staged kernels run at?
+__global__ void fnv_valu_chunk2_kernel(uint32_t bytes, uint32_t* sink) {
+  qfec::Fnv128 h = qfec::fnv_init(), g = qfec::fnv_init();
+  uint32_t w = threadIdx.x * 0x9E3779B9u, x = w ^ 0x1234567u;
+  for (uint32_t i = 0; i < bytes; i += 32) {
+    const qfec::u32x4 v = {w, w ^ 0x5bd1e995u, w * 3u + 1u, w + 0x27d4eb2du};
+    const qfec::u32x4 u = {x, x ^ 0x5bd1e995u, x * 3u + 1u, x + 0x27d4eb2du};
+    qfec::fnv_chunk<true>(h, v);
+    qfec::fnv_chunk<true>(g, u);
+    w = w * 1664525u + 1013904223u;
+    x = x * 1664525u + 1013904223u;
+  }
+  if ((h.x0 ^ h.x1 ^ h.x2 ^ h.x3 ^ g.x0 ^ g.x3) == 0x12345678u) sink[0] = h.x0;
+}
+
+// null_encrypt_staged_kernel<16> with a per-wave timeline (s_memrealtime,
+// 10 ns ticks): where does a wave's life go?
+namespace qfec {
+namespace {
+__global__ __launch_bounds__(kBlock) void null_enc_timed(ProtectArgs a, uint64_t* tl) {
+  constexpr uint32_t SC = 16;
+  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
+  __shared__ StageMeta s_meta[kWaves][64];
+  const uint64_t t0 = wall_clock64();
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = p < a.n;
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = nullptr;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  if (valid) {
+    ad = a.bytes + a.ad_off[p];
+    pt = a.bytes + a.in_off[p];
+    alen = a.ad_len[p];
+    plen = a.in_len[p];
+    o = a.out + a.out_off[p];
+  }
+  s_meta[wv][lane] = StageMeta{pt, o + kTag, plen >> 4};
+  const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  Fnv128 h = fnv_init();
+  if (valid) fnv_span<true>(h, ad, alen);
+  const uint64_t t1 = wall_clock64();
+  uint64_t th = 0, tw = 0, tx = 0;
+  {
+    const StageMeta* meta = s_meta[wv];
+    u32x4* rows = s_rows[wv];
+    const uint32_t my_nfull = plen >> 4;
+    const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
+    u32x4 cur[SC], nxt[SC];
+    if (nslab) stage_load<SC>(meta, lane, 0, cur);
+    for (uint32_t sl = 0; sl < nslab; ++sl) {
+      const uint64_t a0 = wall_clock64();
+      stage_to_lds<SC>(rows, lane, cur);
+      if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, nxt);
+      const uint64_t a1 = wall_clock64();
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j)
+        if (sl * SC + j < my_nfull) fnv_chunk<true>(h, rows[lane * (SC + 1u) + j]);
+      const uint64_t a2 = wall_clock64();
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      stage_store<SC>(meta, lane, sl, cur);
+      const uint64_t a3 = wall_clock64();
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
+      tx += a1 - a0;
+      th += a2 - a1;
+      tw += a3 - a2;
+    }
+  }
+  if (valid) {
+    fnv_tail(h, tail, plen);
+    store_tail(o + kTag, tail, plen);
+    const uint32_t tag[3] = {h.x0, h.x1, h.x2};
+    __builtin_memcpy(o, tag, kTag);
+  }
+  const uint64_t t2 = wall_clock64();
+  if (lane == 0) {
+    uint64_t* r = tl + 8ull * (blockIdx.x * kWaves + wv);
+    r[0] = t0; r[1] = t1; r[2] = t2; r[3] = th; r[4] = tw; r[5] = tx;
+  }
+}
+}  // namespace
+}  // namespace qfec
+
 int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 21);
   const uint32_t L = 1350, H = 22;
@@ -180,6 +266,17 @@ int main(int argc, char** argv) {
        [&] { hipLaunchKernelGGL(fnv_valu_kernel, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
       {"FNV chunk VALU-only R3", 0.0, (double)vgrid * 256 * vb,
        [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<true>, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
+      // occupancy forced by dynamic LDS: 128 KiB -> 1 wave/SIMD, 64 KiB -> 2, 40 KiB -> 4
+      {"FNV chunk VALU-only R3 @1 wave/SIMD", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<true>, dim3(vgrid), dim3(256), 128 << 10, 0, vb, sink); }},
+      {"FNV chunk VALU-only R3 @2 waves/SIMD", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<true>, dim3(vgrid), dim3(256), 64 << 10, 0, vb, sink); }},
+      {"FNV chunk VALU-only R3 @4 waves/SIMD", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<true>, dim3(vgrid), dim3(256), 40 << 10, 0, vb, sink); }},
+      {"FNV 2-chain VALU-only @2 waves/SIMD", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk2_kernel, dim3(vgrid), dim3(256), 64 << 10, 0, vb, sink); }},
+      {"FNV 2-chain VALU-only @8 waves/SIMD", 0.0, (double)vgrid * 256 * vb,
+       [&] { hipLaunchKernelGGL(fnv_valu_chunk2_kernel, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
       {"FNV chunk VALU-only serial", 0.0, (double)vgrid * 256 * vb,
        [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<false>, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
       {"null encrypt staged serial FNV", enc_b, hashed, [&] {
@@ -187,6 +284,41 @@ int main(int argc, char** argv) {
       {"null decrypt staged serial FNV", dec_b, hashed, [&] {
          hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
   };
+  {  // per-wave timeline of the encrypt kernel
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    uint64_t* d_tl;
+    CK(hipMalloc(&d_tl, 8ull * 8 * blocks * 4));
+    hipLaunchKernelGGL(qfec::null_enc_timed, dim3(blocks), dim3(256), 0, 0, e, d_tl);
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(qfec::null_enc_timed, dim3(blocks), dim3(256), 0, 0, e, d_tl);
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> tl(8ull * blocks * 4);
+    CK(hipMemcpy(tl.data(), d_tl, tl.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t mn = UINT64_MAX, mx = 0;
+    double pro = 0, life = 0, hs = 0, ws = 0, xs = 0, epi = 0;
+    const uint64_t W = (uint64_t)blocks * 4;
+    for (uint64_t w = 0; w < W; ++w) {
+      const uint64_t* r = &tl[8 * w];
+      mn = std::min(mn, r[0]);
+      mx = std::max(mx, r[2]);
+      pro += r[1] - r[0];
+      life += r[2] - r[0];
+      hs += r[3];
+      ws += r[4];
+      xs += r[5];
+      epi += (r[2] - r[1]) - (r[3] + r[4] + r[5]);
+    }
+    std::printf("timeline (us, mean per wave; 1 tick = 10 ns): life %.2f = prologue %.2f + "
+                "lds/issue %.2f + hash %.2f + wait/store %.2f + rest %.2f; kernel span %.1f us, "
+                "waves %llu\n",
+                life / W / 100, pro / W / 100, xs / W / 100, hs / W / 100, ws / W / 100,
+                epi / W / 100, (mx - mn) / 100.0, (unsigned long long)W);
+    CK(hipFree(d_tl));
+  }
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fnv_valu_chunk_kernel<true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fnv_valu_chunk2_kernel),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
