@@ -274,6 +274,8 @@ __device__ __forceinline__ void stage_to_lds(u32x4* rows, uint32_t lane, const u
   wave_lds_order();  // then the lanes read their own rows
 }
 
+__device__ __forceinline__ bool wave_any_qpp(bool p) { return __ballot(p) != 0ull; }
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -284,7 +286,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // payloads.  In-place safe for dst == src + 12: slab s is stored only after
 // slab s+1 has been loaded AND the loads have completed (waitcnt), so no store
 // overtakes a load of the 12 bytes it overwrites.
-template <bool COPY, uint32_t SC, bool R3 = true>
+template <bool COPY, uint32_t SC, bool R3 = true, bool INPLACE = true>
 __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32x4* rows,
                                            uint32_t lane, uint32_t my_nfull) {
   const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
@@ -297,7 +299,9 @@ __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32
     for (uint32_t j = 0; j < SC; ++j)
       if (sl * SC + j < my_nfull) fnv_chunk<R3>(h, rows[lane * (SC + 1u) + j]);
     if constexpr (COPY) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next slab's loads are done
+      // in place: vmcnt(0), the next slab's loads are done before this slab's
+      // stores overwrite them; out of place the stores go out at once
+      if constexpr (INPLACE) __builtin_amdgcn_s_waitcnt(0x0F70);
       stage_store<SC>(meta, lane, sl, cur);
     }
 #pragma unroll
@@ -328,7 +332,12 @@ __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs
   const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
   Fnv128 h = fnv_init();
   if (valid) fnv_span<R3>(h, ad, alen);
-  stage_hash<true, SC, R3>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+  // does any packet of the wave write over its own payload (EncryptInPlace)?
+  const bool overlap = valid && o + kTag < pt + plen && pt < o + kTag + plen;
+  if (wave_any_qpp(overlap))
+    stage_hash<true, SC, R3, true>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+  else
+    stage_hash<true, SC, R3, false>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
   if (!valid) return;
   fnv_tail(h, tail, plen);
   store_tail(o + kTag, tail, plen);
