@@ -22,6 +22,10 @@
 //    L2/TA handle the line crossing.
 //  * Recover reads the parity row *in place of* the lost row: k loads per lane,
 //    every one unconditional — the lost slot is never read and no lane idles.
+//  * Batches of >= 8 phases (about 246K groups at L = 1350) run
+//    phase_xor_kernel instead: the same lanes and loads in a persistent
+//    one-workgroup-per-CU grid that separates the row reads and the parity
+//    writes into grid-wide phases (0.80 of 8 TB/s on any buffer placement).
 //  * Ragged CSR batches: two groups per wave (ragged_multi_kernel; the
 //    one-group body below is its exact fallback), lanes own 16-byte windows of the
 //    parity; a packet shorter than the window is loaded as the 16 bytes that
