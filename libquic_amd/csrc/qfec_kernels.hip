@@ -256,7 +256,8 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // (recover, templated k: the phase's parity rows first, then only the
 // received rows) +2.7% recover (tune_phase12.txt).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
-          int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true>
+          int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
+          bool NTLD = true>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         for (int j = 0; j < 8; ++j) {
           const uint64_t g = gidx(i + j < STEPS ? i + j : 0);
           const bool on = i + j < STEPS && lane_on && g < a.n_groups;
-          w[j] = ld16t<true>(a.parity + (on ? g : 0) * a.parity_stride + off);
+          w[j] = ld16t<NTLD>(a.parity + (on ? g : 0) * a.parity_stride + off);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
           for (int r = 0; r < KC; ++r) {
             v[r] = u32x4{0u, 0u, 0u, 0u};
-            if ((uint32_t)r != m[u]) v[r] = ld16t<true>(src[u] + r * a.row_stride);
+            if ((uint32_t)r != m[u]) v[r] = ld16t<NTLD>(src[u] + r * a.row_stride);
           }
           acc[u] = s_par[i + u][tid];
 #pragma unroll
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
           for (int r = 0; r < KC; ++r) {
             const uint8_t* q = (RECOVER && (uint32_t)r == m[u]) ? par : src[u] + r * a.row_stride;
-            v[u][r] = ld16t<true>(q);
+            v[u][r] = ld16t<NTLD>(q);
           }
         }
 #pragma unroll
@@ -374,14 +375,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
             for (uint32_t w = 0; w < 8; ++w) {
               const uint8_t* q = (RECOVER && r + w == m[u]) ? par : src[u] + (r + w) * a.row_stride;
-              v[w] = ld16t<true>(q);
+              v[w] = ld16t<NTLD>(q);
             }
 #pragma unroll
             for (uint32_t w = 0; w < 8; ++w) acc[u] ^= v[w];
           }
           for (; r < k; ++r) {
             const uint8_t* q = (RECOVER && r == m[u]) ? par : src[u] + r * a.row_stride;
-            acc[u] ^= ld16t<true>(q);
+            acc[u] ^= ld16t<NTLD>(q);
           }
         }
       }

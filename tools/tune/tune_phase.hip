@@ -288,6 +288,8 @@ int main(int argc, char** argv) {
       {"prod (256 x 40)", qfec::phase_xor_kernel<10, false>},
       {"prod recover (256 x 40)", qfec::phase_xor_kernel<10, true>},
       {"prod recover parity-first", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true>},
+      {"prod dflt-load", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, false>},
+      {"prod recover dflt-load", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, false>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
