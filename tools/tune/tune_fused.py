@@ -1,35 +1,24 @@
-"""Chunk size / slot count sweep of bench.py's fused FEC + AES-128-GCM-12
-host-memory leg (bench_fused), against the measured bidirectional PCIe copy
-rate (tools/tune/tune_zero_copy.hip: 97 GB/s total, 48.6 GB/s each way).
-Usage: python tools/tune/tune_fused.py"""
-import json
+"""Chunking of the fused FEC + AES-128-GCM-12 host-memory leg (bench.bench_fused):
+chunk size x slots, payload GiB/s over wall time (pinned host buffers).
+python tools/tune/tune_fused.py > gpurun_out/tune_fused.txt"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, ROOT)
-
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 from libquic_amd import qfec  # noqa: E402
 
-
-def main():
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
-    ctx = qfec.Context(0)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream)
-    for cg, slots in ((8192, 3), (4096, 3), (4096, 4), (8192, 4), (16384, 3), (2048, 6),
-                      (4096, 6)):
-        r = bench.bench_fused(ctx, torch, dev, stream, 10, 1350, cg=cg, slots=slots, cpu=False)
-        moved = r["pcie_h2d_bytes"] + r["pcie_d2h_bytes"]
-        print(json.dumps({"chunk_groups": cg, "slots": slots, "payload_GiBps": r["payload_GiBps"],
-                          "wall_ms": r["wall_ms"], "link_GBps": round(moved / r["wall_ms"] / 1e6, 1),
-                          "verified": r["verified"]}), flush=True)
-    ctx.close()
-
-
-if __name__ == "__main__":
-    main()
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+ctx = qfec.Context(0)
+stream = torch.cuda.current_stream()
+ctx.set_stream(stream)
+for cg, slots in [(4096, 3), (4096, 4), (8192, 3), (8192, 4), (2048, 4), (2048, 6), (16384, 3)]:
+    r = bench.bench_fused(ctx, torch, dev, stream, 10, 1350, cg=cg, slots=slots, cpu=False)
+    print(f"cg {cg:6d} slots {slots}: staged {r['payload_GiBps']:6.2f} GiB/s "
+          f"({r['wall_ms']:.1f} ms, ok {r['verified']}), direct_out "
+          f"{r['direct_out']['payload_GiBps']:6.2f} GiB/s (ok {r['direct_out']['verified']})",
+          flush=True)
+ctx.close()
