@@ -1137,26 +1137,31 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
         FEC plaintext == XOR of the group's rows"""
         ok = True
         vs = S[0]
+        torch.cuda.synchronize()
         for c in (0, nchunk - 1):
-            ob = npk * (L + 12)
-            ct = host_out[c * ob:(c + 1) * ob].to(dev)
-            vb = vs["buf"]
-            vb[rows_b + par_b:].copy_(host_hdr[c * hdr_b:(c + 1) * hdr_b])
-            cat = torch.empty(hdr_b + ob, dtype=torch.uint8, device=dev)
-            cat[:hdr_b] = vb[rows_b + par_b:]
-            cat[hdr_b:] = ct
-            pt = torch.empty(npk * L, dtype=torch.uint8, device=dev)
-            okv = torch.zeros(npk, dtype=torch.uint8, device=dev)
-            vs["ctx"].aes128gcm_open(key, pre, kidx, pn[c], None, cat, q * hdr, ad_len,
-                                     hdr_b + q * (L + 12), (in_len + 12).to(torch.int16), npk, pt,
-                                     q * L, okv)
-            vs["ctx"].sync()
-            rows_c = host_rows[c * rows_b:(c + 1) * rows_b].to(dev)
-            par_c = rows_c.view(cg, k, L)[:, 0].clone()
-            for i in range(1, k):
-                par_c ^= rows_c.view(cg, k, L)[:, i]
-            ok = ok and bool(okv.all()) and torch.equal(pt[:rows_b], rows_c) and \
-                torch.equal(pt[rows_b:], par_c.reshape(-1))
+            # torch's copies and the context's launches on the SAME stream (the
+            # open kernel must not read `cat` before the copies have filled it)
+            with torch.cuda.stream(vs["stream"]):
+                ob = npk * (L + 12)
+                ct = host_out[c * ob:(c + 1) * ob].to(dev)
+                vb = vs["buf"]
+                vb[rows_b + par_b:].copy_(host_hdr[c * hdr_b:(c + 1) * hdr_b])
+                cat = torch.empty(hdr_b + ob, dtype=torch.uint8, device=dev)
+                cat[:hdr_b] = vb[rows_b + par_b:]
+                cat[hdr_b:] = ct
+                pt = torch.empty(npk * L, dtype=torch.uint8, device=dev)
+                okv = torch.zeros(npk, dtype=torch.uint8, device=dev)
+                vs["ctx"].aes128gcm_open(key, pre, kidx, pn[c], None, cat, q * hdr, ad_len,
+                                         hdr_b + q * (L + 12), (in_len + 12).to(torch.int16), npk, pt,
+                                         q * L, okv)
+                vs["ctx"].sync()
+                rows_c = host_rows[c * rows_b:(c + 1) * rows_b].to(dev)
+                par_c = rows_c.view(cg, k, L)[:, 0].clone()
+                for i in range(1, k):
+                    par_c ^= rows_c.view(cg, k, L)[:, i]
+                ok = ok and bool(okv.all()) and torch.equal(pt[:rows_b], rows_c) and \
+                    torch.equal(pt[rows_b:], par_c.reshape(-1))
+        torch.cuda.synchronize()
         return ok
 
     def timed(direct_out):

@@ -181,6 +181,7 @@ def test_phased_concurrent_launches(ctx):
     ctx2 = qfec.Context(0)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     outs = [torch.zeros(n * L, dtype=torch.uint8, device=DEV) for _ in range(4)]
+    torch.cuda.synchronize()  # the fills (current stream) before launches on s1 / s2
     try:
         ctx.set_stream(s1)
         ctx2.set_stream(s2)
