@@ -257,7 +257,7 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // received rows) +2.7% recover (tune_phase12.txt).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
-          bool NTLD = true>
+          bool NTLD = true, bool EDGE = false>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
@@ -356,7 +356,17 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
           for (int r = 0; r < KC; ++r) {
             const uint8_t* q = (RECOVER && (uint32_t)r == m[u]) ? par : src[u] + r * a.row_stride;
-            v[u][r] = ld16t<NTLD>(q);
+            if constexpr (EDGE) {
+              // EDGE: windows in the first / last 128-B line of a row (lines
+              // the neighbouring row shares) by default-policy loads, so the
+              // second row's load finds the line in L2; nt loads elsewhere
+              const uint32_t aw = (uint32_t)(uintptr_t)q;
+              const uint32_t rs = (uint32_t)(uintptr_t)(src[u] - off + r * a.row_stride);
+              const bool edge = (aw >> 7) == (rs >> 7) || ((aw + 15u) >> 7) == ((rs + a.L - 1u) >> 7);
+              v[u][r] = edge ? ld16t<false>(q) : ld16t<true>(q);
+            } else {
+              v[u][r] = ld16t<NTLD>(q);
+            }
           }
         }
 #pragma unroll

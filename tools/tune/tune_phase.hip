@@ -290,6 +290,7 @@ int main(int argc, char** argv) {
       {"prod recover parity-first", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true>},
       {"prod dflt-load", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, false>},
       {"prod recover dflt-load", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, false>},
+      {"prod edge-dflt", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, true>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
