@@ -85,6 +85,7 @@ static void launch_win(const RaggedArgs& a, uint64_t G) {
 }
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);  // progress lines reach the log as they happen
   const uint64_t G = 1 << 20;
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
@@ -183,10 +184,16 @@ int main(int argc, char** argv) {
     RG_DIAG(false, 0, "diag0 product");
     RG_DIAG(false, 1, "diag1 nostore (not exact)");
     RG_DIAG(false, 2, "diag2 L2 store (not exact)");
+    RG_DIAG(false, 3, "diag3 wb stores");
+    RG_DIAG(false, 4, "diag4 xcd order");
+    RG_DIAG(false, 5, "diag5 xcd+wb");
     vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
     RG_DIAG(true, 0, "diag0 product");
     RG_DIAG(true, 1, "diag1 nostore (not exact)");
     RG_DIAG(true, 2, "diag2 L2 store (not exact)");
+    RG_DIAG(true, 3, "diag3 wb stores");
+    RG_DIAG(true, 4, "diag4 xcd order");
+    RG_DIAG(true, 5, "diag5 xcd+wb");
   }
 #undef RG_DIAG
   const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr;
@@ -204,7 +211,26 @@ int main(int argc, char** argv) {
                                      dim3(64 * W), 0, 0, a0, (uint32_t)((G + per - 1) / per),  \
                                      psync);                                                    \
                 }})
-  if (!diag_only) {
+#define RG_PHASE2(REC, W, NP, DYN, U)                                                          \
+  vs.push_back({std::string("phase2 W" #W " NP" #NP " U" #U " ") + (REC ? "recover" : "encode"),  \
+                REC, [=](const RaggedArgs& a0) {                                               \
+                  const uint64_t per = (uint64_t)ncu * NP * 2;                                 \
+                  hipLaunchKernelGGL((qfec::ragged_phase2_kernel<REC, W, NP, DYN, U>), dim3(ncu), \
+                                     dim3(64 * W), 0, 0, a0, (uint32_t)((G + per - 1) / per), \
+                                     psync);                                                   \
+                }})
+  if (getenv("TUNE_RW_PHASE2")) {
+    RG_PHASE2(false, 16, 40, true, 2);
+    RG_PHASE2(false, 16, 40, true, 4);
+    RG_PHASE2(false, 16, 40, true, 6);
+    RG_PHASE2(false, 16, 40, true, 8);
+    RG_PHASE2(false, 12, 42, true, 4);
+    vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_PHASE2(true, 16, 40, true, 4);
+    RG_PHASE2(true, 16, 40, true, 8);
+  }
+#undef RG_PHASE2
+  if (!diag_only && !getenv("TUNE_RW_PHASE2")) {
     RG_PHASE(false, 4, 13, 1);
     RG_PHASE(false, 8, 6, 1);
     RG_PHASE(false, 12, 3, 1);
@@ -252,6 +278,7 @@ int main(int argc, char** argv) {
   for (auto& v : vs) {
     CK(hipMemset(out, 0, G * 1452));
     CK(hipMemset(plen2, 0, G * 2));
+    std::printf("check %s ...\n", v.name.c_str());
     v.run(v.rec ? r : e2);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(got.data(), out, G * 1452, hipMemcpyDeviceToHost));
