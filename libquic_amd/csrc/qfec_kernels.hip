@@ -254,10 +254,14 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps) {
 // FLAT (row pointers as generic pointers: flat loads) changes nothing; XCDW
 // (XCD-aware order in the window) +0.5% encode / -3% recover; PARFIRST
 // (recover, templated k: the phase's parity rows first, then only the
-// received rows) +2.7% recover (tune_phase12.txt).
+// received rows) +2.7% recover (tune_phase12.txt); COMPACT (with PARFIRST: the
+// k-1 received rows loaded in order, r + (r >= m), so no load instruction runs
+// with the lost row's lanes masked off: 17 loads and 22 exec branches per step
+// instead of 18 and 32) +2.5% recover, 0.780 vs 0.761 on six buffer pairs
+// (profiles/round2/phase/tune_phase_compact.txt).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
-          bool NTLD = true, bool EDGE = false>
+          bool NTLD = true, bool EDGE = false, bool COMPACT = true>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
@@ -337,10 +341,19 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
         for (int u = 0; u < kPhU; ++u) {
           u32x4 v[KC];
+          if constexpr (COMPACT) {
+            // the k-1 received rows in order, every lane on every load (no
+            // instruction with the lost row's lanes masked off)
 #pragma unroll
-          for (int r = 0; r < KC; ++r) {
-            v[r] = u32x4{0u, 0u, 0u, 0u};
-            if ((uint32_t)r != m[u]) v[r] = ld16t<NTLD>(src[u] + r * a.row_stride);
+            for (int r = 0; r + 1 < KC; ++r)
+              v[r] = ld16t<NTLD>(src[u] + ((uint32_t)r + ((uint32_t)r >= m[u] ? 1u : 0u)) * a.row_stride);
+            v[KC - 1] = u32x4{0u, 0u, 0u, 0u};
+          } else {
+#pragma unroll
+            for (int r = 0; r < KC; ++r) {
+              v[r] = u32x4{0u, 0u, 0u, 0u};
+              if ((uint32_t)r != m[u]) v[r] = ld16t<NTLD>(src[u] + r * a.row_stride);
+            }
           }
           acc[u] = s_par[i + u][tid];
 #pragma unroll

@@ -291,6 +291,8 @@ int main(int argc, char** argv) {
       {"prod dflt-load", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, false>},
       {"prod recover dflt-load", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, false>},
       {"prod edge-dflt", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, true>},
+      {"prod recover compact", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true>},
+      {"prod recover masked", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, false>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
@@ -367,6 +369,26 @@ int main(int argc, char** argv) {
       uint32_t h = 0;
       CK(hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost));
       if (h) std::printf("%s rows%d: %u differing words\n", pks[w].first.c_str(), i, h);
+    }
+  }
+  {  // recover variants against the product's recover on the same buffers
+    int w0 = -1;
+    for (int w = 0; w < (int)pks.size(); ++w)
+      if (pks[w].first == "prod recover (256 x 40)") w0 = w;
+    for (int i = 0; i < NR; ++i) {
+      CK(hipMemset(par[1], 0, par_b));
+      prod_variant(w0, i, 1);
+      CK(hipMemcpy(want, par[1], par_b, hipMemcpyDeviceToDevice));
+      for (int w = 0; w < (int)pks.size(); ++w) {
+        if (w == w0 || pks[w].first.find("recover") == std::string::npos || !pks[w].second) continue;
+        CK(hipMemset(par[1], 0, par_b));
+        prod_variant(w, i, 1);
+        CK(hipMemset(bad, 0, 4));
+        hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, par[1], want, par_b, bad);
+        uint32_t h = 0;
+        CK(hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost));
+        if (h) std::printf("%s rows%d: %u differing words\n", pks[w].first.c_str(), i, h);
+      }
     }
   }
   std::printf("exactness checked (silence = every variant equals the product)\n");
