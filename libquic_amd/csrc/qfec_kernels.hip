@@ -618,6 +618,23 @@ __device__ __forceinline__ u32x4 packet_window(const uint8_t* row, uint32_t len,
   return window16_small(row, len, 0u);  // t == 0 (rare: packets below 16 B)
 }
 
+// Window t of a zero-padded row of len >= 16 bytes without a branch: a window
+// at or past len loads the row's last 16 bytes and returns zero.
+template <bool NT>
+__device__ __forceinline__ u32x4 parity_window_bf(const uint8_t* row, uint32_t len, uint32_t t) {
+  const uint32_t win = 16u * t;
+  const bool in = win < len;
+  const bool full = win + 16u <= len;
+  const uint32_t at = in && full ? win : len - 16u;
+  u32x4 v = shr_bytes_bf(ld16t<NT>(row + at), in && !full ? win + 16u - len : 0u);
+  const uint32_t keep = in ? 0xFFFFFFFFu : 0u;
+  v.x &= keep;
+  v.y &= keep;
+  v.z &= keep;
+  v.w &= keep;
+  return v;
+}
+
 // Per-group inputs a wave can fetch one group ahead: the group scalars and,
 // for the first 64 received packets, lane r's packet length / offset (and for
 // recover the parity row's two windows per lane).
@@ -894,7 +911,7 @@ __device__ __forceinline__ T sel_n(const T (&v)[N], uint32_t j) {
 // from `par` with lengths pl[] at offsets doff[].
 constexpr uint32_t kAccWords = 4 * kParWin;
 
-template <bool RECOVER, bool NT, int GPW, int U, bool BF>
+template <bool RECOVER, bool NT, int GPW, int U, bool BF, bool PBF = true>
 __device__ __forceinline__ bool ragged_pair_xor(const RaggedArgs& a, uint64_t g0, uint32_t ng,
                                                 uint32_t lane, uint32_t* par, uint64_t* head,
                                                 u32x4* meta, uint32_t (&pl)[GPW],
@@ -958,10 +975,19 @@ __device__ __forceinline__ bool ragged_pair_xor(const RaggedArgs& a, uint64_t g0
       if constexpr (RECOVER) {
         const uint8_t* prow = a.parity + ((uint32_t)j < ng ? a.parity_off[g0 + j] : 0ull);
         const uint32_t plj = (uint32_t)j < ng ? pl[j] : 0u;
+        // branch-free parity windows: every lane loads a window inside the
+        // row (lanes past plj re-read its last 16 bytes and keep zero), so
+        // neither load runs with lanes masked off.  plj >= 16 whenever the
+        // pair takes this path (ok); the branch is wave-uniform.
         const u32x4 zero = {0u, 0u, 0u, 0u};
         u32x4 w0 = zero, w1 = zero;
-        if (16u * lane < plj) w0 = packet_window<NT>(prow, plj, lane);
-        if (16u * (lane + 64u) < plj) w1 = packet_window<NT>(prow, plj, lane + 64u);
+        if (!PBF) {  // the round-2 form (A/B reference, tools/tune/ragged_exp.inc)
+          if (16u * lane < plj) w0 = packet_window<NT>(prow, plj, lane);
+          if (16u * (lane + 64u) < plj) w1 = packet_window<NT>(prow, plj, lane + 64u);
+        } else if (plj >= 16u) {
+          w0 = parity_window_bf<NT>(prow, plj, lane);
+          w1 = parity_window_bf<NT>(prow, plj, lane + 64u);
+        }
         lds_put16<ACC>(acc, lane, w0);
         if (lane + 64u < kParWin) lds_put16<ACC>(acc, lane + 64u, w1);
       } else {
