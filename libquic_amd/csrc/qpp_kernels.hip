@@ -146,6 +146,16 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
 }
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 
+// Global-address-space forms for pointers the compiler cannot prove global
+// (StageMeta entries read back from LDS): a generic pointer becomes a FLAT
+// access, and FLAT loads count against lgkmcnt as well as vmcnt, so every LDS
+// wait of a slab's hashing would also wait for the next slab's loads.
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef const __attribute__((address_space(1))) u32x4_a1* gld_ptr;
+typedef __attribute__((address_space(1))) u32x4_a1* gst_ptr;
+__device__ __forceinline__ u32x4 ld16g(const uint8_t* p) { return *(gld_ptr)p; }
+__device__ __forceinline__ void st16g(uint8_t* p, u32x4 v) { *(gst_ptr)p = v; }
+
 // The last len % 16 bytes of a span as the upper bytes of one 16-byte chunk
 // (len >= 16: the 16 bytes ending at the span end) or, for len < 16, the
 // whole span byte by byte into bytes [0, len).
@@ -235,7 +245,7 @@ __device__ __forceinline__ void wave_lds_order() {
 // Cooperative load of slab `sl` (SC chunks per packet) for the wave's 64
 // packets: lane (SC*i + m) of instruction I takes chunk m of packet
 // (64/SC)*I + i; SC instructions cover the 64 packets.
-template <uint32_t SC>
+template <uint32_t SC, bool G = true>
 __device__ __forceinline__ void stage_load(const StageMeta* meta, uint32_t lane, uint32_t sl,
                                            u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
@@ -244,12 +254,12 @@ __device__ __forceinline__ void stage_load(const StageMeta* meta, uint32_t lane,
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
-    if (c < q.nfull) v[I] = ld16(q.src + 16u * c);
+    if (c < q.nfull) v[I] = G ? ld16g(q.src + 16u * c) : ld16(q.src + 16u * c);
   }
   wave_lds_order();
 }
 
-template <uint32_t SC>
+template <uint32_t SC, bool G = true>
 __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane, uint32_t sl,
                                             const u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
@@ -258,7 +268,10 @@ __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
-    if (c < q.nfull && q.dst) st16(q.dst + 16u * c, v[I]);
+    if (c < q.nfull && q.dst) {
+      if (G) st16g(q.dst + 16u * c, v[I]);
+      else st16(q.dst + 16u * c, v[I]);
+    }
   }
   wave_lds_order();  // before a lane rewrites its meta entry
 }
