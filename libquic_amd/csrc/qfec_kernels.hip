@@ -1049,8 +1049,18 @@ __device__ __forceinline__ bool ragged_pair_xor(const RaggedArgs& a, uint64_t g0
       tt[u] = fl < W ? (md[u].z >> 16) * kAccWords + (fl - md[u].w) : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (tt[u] != 0xFFFFFFFFu) lds_xor16<ACC>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+    for (int u = 0; u < U; ++u) {
+      if constexpr (BF) {
+        // branch-free: a lane past W XORs ZERO into window `lane` of the first
+        // accumulator (a no-op, conflict-free), so no load or LDS atomic sits
+        // in an exec-masked block
+        uint32_t keep = tt[u] != 0xFFFFFFFFu ? 0xFFFFFFFFu : 0u;
+        __asm__ volatile("" : "+v"(keep));
+        lds_xor16<ACC>(par, tt[u] != 0xFFFFFFFFu ? tt[u] : lane, shr_bytes_bf(v[u], sh[u]) & keep);
+      } else if (tt[u] != 0xFFFFFFFFu) {
+        lds_xor16<ACC>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+      }
+    }
   }
   if constexpr (!RECOVER) {
 #pragma unroll

@@ -184,6 +184,7 @@ int main(int argc, char** argv) {
     RG_DIAG(false, 0, "diag0 product");
     RG_DIAG(false, 1, "diag1 nostore (not exact)");
     RG_DIAG(false, 2, "diag2 L2 store (not exact)");
+    RG_DIAG(false, 9, "diag9 bf xor loop");
     RG_DIAG(false, 7, "diag7 bf tail st");
     RG_DIAG(false, 6, "diag6 aligned st");
     RG_DIAG(false, 3, "diag3 wb stores");
@@ -193,6 +194,7 @@ int main(int argc, char** argv) {
     RG_DIAG(true, 0, "diag0 product");
     RG_DIAG(true, 1, "diag1 nostore (not exact)");
     RG_DIAG(true, 2, "diag2 L2 store (not exact)");
+    RG_DIAG(true, 9, "diag9 bf xor loop");
     RG_DIAG(true, 8, "diag8 masked parity");
     RG_DIAG(true, 7, "diag7 bf tail st");
     RG_DIAG(true, 6, "diag6 aligned st");
