@@ -184,6 +184,9 @@ int main(int argc, char** argv) {
     RG_DIAG(false, 0, "diag0 product");
     RG_DIAG(false, 1, "diag1 nostore (not exact)");
     RG_DIAG(false, 2, "diag2 L2 store (not exact)");
+    vs.push_back({"multi2 U1 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 1>(a, G); }});
+    vs.push_back({"multi2 U3 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 3>(a, G); }});
+    vs.push_back({"multi2 U4 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2, true, 4>(a, G); }});
     RG_DIAG(false, 9, "diag9 bf xor loop");
     RG_DIAG(false, 7, "diag7 bf tail st");
     RG_DIAG(false, 6, "diag6 aligned st");
@@ -194,6 +197,9 @@ int main(int argc, char** argv) {
     RG_DIAG(true, 0, "diag0 product");
     RG_DIAG(true, 1, "diag1 nostore (not exact)");
     RG_DIAG(true, 2, "diag2 L2 store (not exact)");
+    vs.push_back({"multi2 U1 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 1>(a, G); }});
+    vs.push_back({"multi2 U3 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 3>(a, G); }});
+    vs.push_back({"multi2 U4 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2, true, 4>(a, G); }});
     RG_DIAG(true, 9, "diag9 bf xor loop");
     RG_DIAG(true, 8, "diag8 masked parity");
     RG_DIAG(true, 7, "diag7 bf tail st");
