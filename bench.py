@@ -63,6 +63,8 @@ def parse(argv=None):
     p.add_argument("--cpu-workload", action="store_true",
                    help="test switch: numpy stand-in for the GPU step over gloo (no GPU); "
                         "exercises the rank launch / shard / timing / JSON path on a CPU box")
+    p.add_argument("--digests", action="store_true",
+                   help="test switch: every rank's parity / revived digests on the line (shards)")
     p.add_argument("--profile-only", action="store_true",
                    help="only the device-resident steps (for rocprofv3 runs)")
     p.add_argument("--protect-only", action="store_true",
@@ -143,7 +145,10 @@ def cpu_baseline(rows, G, k, L, seconds, threads=0):
     # configs[0]: 1 group of 10 x 1350 B, encode + recover 1 drop, ns/group (1 core)
     ns_group = lib.qo_time_single_group_ns(k, L, 200000)
     return {
-        "value": round(mt, 3), "unit": "GiB/s", "cores": best, "kind": "port",
+        # cores = what the threads ran on (the box's CPU share caps it); the
+        # thread count is reported separately
+        "value": round(mt, 3), "unit": "GiB/s", "cores": min(best, share), "threads": best,
+        "kind": "port",
         "sample": f"oracle encode+recover of the bench workload itself ({G} groups x {k} x {L} B,"
                   f" {bytes_per_pass / 1e9:.1f} GB per pass): best of a thread sweep "
                   f"{sweep} (GiB/s by threads; box CPU share {share} of nproc "
@@ -476,15 +481,18 @@ def main(argv=None):
         return 0
 
     cpu = args.cpu_workload
+    # QFEC_BENCH_SHARE_DEVICE=1 (tests only): every rank on cuda:0, so the N>1
+    # path runs on a one-GPU box (weak scaling is then not meaningful).
+    share = os.environ.get("QFEC_BENCH_SHARE_DEVICE") == "1"
     if world > 1:
+        # The shards exchange nothing (independent FEC groups): the control
+        # plane — the timing barrier, the max of the elapsed time, the gather
+        # of per-rank results — runs over gloo on CPU tensors, so the path
+        # needs no RCCL (north_star: no collective).
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if cpu:
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    elif not cpu:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    if not cpu:
+        torch.cuda.set_device(0 if (world == 1 or share) else local)
     dev = None if cpu else torch.device("cuda", torch.cuda.current_device())
 
     def barrier():
@@ -494,7 +502,7 @@ def main(argv=None):
     def reduce_max(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -516,7 +524,9 @@ def main(argv=None):
     enc_s, rec_s = work.kernel_seconds(events)
     verified = None if args.no_verify else work.verify()
     per_rank = gather({"rank": rank, "g0": g0, "groups": G, "enc_s": enc_s, "rec_s": rec_s,
-                       "verified": verified, "digests": work.digests() if cpu else None})
+                       "verified": verified,
+                       "digests": work.digests() if (cpu or args.digests) else None,
+                       "device": None if cpu else torch.cuda.current_device()})
     if enc_s:  # the roofline of the slowest rank's encode launch
         enc_s = max(r["enc_s"] for r in per_rank)
         rec_s = max(r["rec_s"] for r in per_rank)
@@ -532,11 +542,18 @@ def main(argv=None):
     if world > 1 and line["roofline"]:
         fr = [work.bytes_encode / r["enc_s"] / 1e9 / HBM_PEAK_GBS for r in per_rank]
         line["roofline"]["per_rank_frac"] = {"min": round(min(fr), 4), "max": round(max(fr), 4)}
+    if world > 1:
+        line["control_plane"] = "gloo (CPU tensors): barrier, max, gather; no data collective"
     if cpu:
         line["data"] = "synthetic; --cpu-workload numpy stand-in (test of the rank path, not a measurement)"
         line["dtype"] = "u8"
+    if cpu or args.digests:
         line["shards"] = [{"rank": r["rank"], "g0": r["g0"], "groups": r["groups"],
+                           "device": r["device"], "verified": r["verified"],
                            "digests": r["digests"]} for r in per_rank]
+    if share and world > 1:
+        line["note_shared_device"] = ("QFEC_BENCH_SHARE_DEVICE: all ranks on cuda:0 (a test of the "
+                                      "N>1 path, not a scaling measurement)")
 
     extras = rank == 0 and world == 1 and not cpu and not args.profile_only
     if rank == 0 and world == 1 and not cpu and args.profile_only and not args.no_ragged:
@@ -864,8 +881,13 @@ def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
 
 
 def _cpu_aead_baseline(aead, hdr, L, n, seconds):
-    """Oracle (vector-pinned scalar C) AEAD seal on the host cores."""
+    """AEAD seal on the host cores: the reference's own Aes128Gcm12Encrypter /
+    ChaCha20Poly1305Encrypter over BoringSSL built WITH its x86-64 assembly
+    (oracle/_ref/libref_aead_asm.so: AES-NI + PCLMULQDQ, SIMD ChaCha20 and
+    Poly1305), or the vector-pinned scalar C restatement where that build is
+    absent (kind "port")."""
     from oracle import oracle_c as OC
+    from oracle import ref_quic
     threads = _cpu_share()
     rec = hdr + L
     rng = np.random.default_rng(2)
@@ -877,33 +899,40 @@ def _cpu_aead_baseline(aead, hdr, L, n, seconds):
     out_off = ar * np.uint64(L + 12)
     keys = np.arange(32 if aead == "chacha20poly1305" else 16, dtype=np.uint8)
     kind, what = "port", "scalar C restatement pinned by BoringSSL's vectors"
-    if aead == "chacha20poly1305":
-        seal = OC.quic_c20p1305_encrypt_batch
-    else:
-        seal = OC.quic_aes128gcm_encrypt_batch
-        from oracle import ref_quic
-        if ref_quic.available():  # the reference's own aes.c + gcm.c (oracle/_ref)
-            kind, what = "reference", "BoringSSL aes.c + gcm.c from the reference tree, C build"
+    seal = OC.quic_c20p1305_encrypt_batch if aead == "chacha20poly1305" \
+        else OC.quic_aes128gcm_encrypt_batch
+    feats = None
+    if ref_quic.asm_available():
+        feats = ref_quic.asm_cpu_features()
+        kind = "reference"
+        what = ("the reference's EncryptPacket over BoringSSL with its x86-64 assembly, "
+                f"CPU features {sorted(k for k, v in feats.items() if v)}")
 
-            def seal(keys, pre, kidx, pn, path, *rest, threads, out):
-                return ref_quic.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, *rest,
-                                                             threads=threads, out=out)
+        def seal(keys, pre, kidx, pn, path, *rest, threads, out):
+            return ref_quic.asm_seal_batch(aead, keys, pre, kidx, pn, *rest, threads=threads,
+                                           out=out)
     name = "ChaCha20-Poly1305" if aead == "chacha20poly1305" else "AES-128-GCM-12"
     obuf = np.zeros(n * (L + 12), np.uint8)  # reused: no page faults in the timed loop
     pre = np.arange(4, dtype=np.uint8)
     kidx = np.zeros(n, np.uint32)
     pn = ar + np.uint64(1)
-    t0, reps = time.perf_counter(), 0
-    while time.perf_counter() - t0 < seconds / 2:
+
+    def run(th, budget):
         seal(keys, pre, kidx, pn, None, data, ad_off, ad_len, pt_off, pt_len, out_off,
-             n * (L + 12), threads=threads, out=obuf)
-        reps += 1
-    el = time.perf_counter() - t0
-    return {"value": round(reps * n * (hdr + L + L + 12) / el / 2**30, 3), "unit": "GiB/s",
-            "cores": threads, "kind": kind,
+             n * (L + 12), threads=th, out=obuf)  # untimed
+        t0, reps = time.perf_counter(), 0
+        while time.perf_counter() - t0 < budget:
+            seal(keys, pre, kidx, pn, None, data, ad_off, ad_len, pt_off, pt_len, out_off,
+                 n * (L + 12), threads=th, out=obuf)
+            reps += 1
+        el = time.perf_counter() - t0
+        return reps * n * (hdr + L + L + 12) / el / 2**30, reps
+    mt, reps = run(threads, seconds / 2)
+    st, _ = run(1, seconds / 4)
+    return {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "threads": threads,
+            "kind": kind, "single_core_value": round(st, 3),
             "sample": f"{name} seal of {n} packets ({hdr}+{L} B), {reps} passes on {threads} "
-                      f"threads ({what}; BoringSSL's SIMD/AES-NI assembly, not buildable "
-                      f"here, would be faster on the CPU)"}
+                      f"threads ({what})"}
 
 
 def _cpu_null_baseline(hdr, L, n, seconds):
@@ -1227,12 +1256,14 @@ def _cpu_fused_baseline(k, L, hdr, n=4096, seconds=4.0):
     obuf = np.zeros(npk * (L + 12), np.uint8)
     kind, what = "port", "oracle FEC + scalar C AES-GCM restatement"
     seal = OC.quic_aes128gcm_encrypt_batch
-    if ref_quic.available():
-        kind, what = "reference", "oracle FEC + the reference's BoringSSL aes.c + gcm.c (C build)"
+    if ref_quic.asm_available():
+        kind = "reference"
+        what = ("oracle FEC + the reference's Aes128Gcm12Encrypter over BoringSSL with its "
+                "x86-64 assembly (AES-NI, PCLMULQDQ)")
 
         def seal(keys, pre, kidx, pn, path, *rest, threads, out):
-            return ref_quic.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, *rest,
-                                                         threads=threads, out=out)
+            return ref_quic.asm_seal_batch("aes128gcm", keys, pre, kidx, pn, *rest,
+                                           threads=threads, out=out)
     lib = OC.lib()
 
     def once():
@@ -1248,8 +1279,7 @@ def _cpu_fused_baseline(k, L, hdr, n=4096, seconds=4.0):
     return {"value": round(reps * n * k * L / el / 2**30, 3), "unit": "GiB/s of payload",
             "cores": threads, "kind": kind,
             "sample": f"{n} groups x {k} x {L} B: FEC encode + seal of {npk} packets, {reps} "
-                      f"passes on {threads} threads ({what}; BoringSSL's AES-NI/PCLMUL assembly "
-                      f"is not buildable here and would be faster)"}
+                      f"passes on {threads} threads ({what})"}
 
 
 def bench_e2e(ctx, torch, k, L, G=1 << 18):

@@ -94,6 +94,21 @@ extern "C" {
                                parity writes in separate grid-wide phases, which
                                keeps its rate independent of where the buffers
                                sit in the DRAM.  Same results either way. */
+#define QFEC_ASYNC 16u      /* with QFEC_PTR_MAPPED, ragged calls: return as soon
+                               as the work is queued (index arrays staged, kernel
+                               launched) instead of when it is done; the outputs
+                               (payload bytes and parity_len_out) are valid once
+                               qfec_complete() has returned QFEC_OK, and every
+                               buffer stays borrowed until then.  A batch whose
+                               index tables exceed one staging slot (64 MiB) runs
+                               synchronously.  Up to 3 calls may be in flight on
+                               a context; any other call that stages through the
+                               context completes them first.  Ignored by other
+                               calls.  (The event-loop form: launch the turn's
+                               FEC work, serve sockets, complete it next turn.) */
+
+/* qfec_complete() with wait == 0: the QFEC_ASYNC work is still running. */
+#define QFEC_PENDING 1
 
 typedef struct qfec_ctx qfec_ctx;
 
@@ -113,6 +128,11 @@ void* qfec_own_stream(qfec_ctx* ctx);
  * (e.g. a missing index >= k or a ragged length > kMaxPacketSize found on the
  * device) since the previous qfec_sync, then clears it. */
 int qfec_sync(qfec_ctx* ctx);
+/* Finish the context's QFEC_ASYNC calls in issue order.  wait != 0 blocks
+ * until all are done; wait == 0 returns QFEC_PENDING while one is still
+ * running.  Returns the first error of the calls it finished (the same codes
+ * the synchronous call would have returned), else QFEC_OK. */
+int qfec_complete(qfec_ctx* ctx, int wait);
 const char* qfec_strerror(int code);
 /* Pinned, device-mapped host memory for QFEC_PTR_MAPPED payloads (the
  * registered receive / send buffers of a QUIC server: the GPU reads packets
@@ -334,6 +354,21 @@ int qfec_stream_probe(qfec_ctx* ctx, const uint8_t* src, uint64_t n, uint8_t* ds
  * work, so not every workgroup was resident) and ran to the end without them
  * — same results, one-pass-like speed.  Waits for the context's stream. */
 int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count);
+/* Large fixed-shape batches left to run with the one-pass kernel because a
+ * phased launch of this context was abandoned (the GPU is contended: the
+ * context then uses the one-pass kernel for the next 16 such batches and
+ * tries the phased one again).  -1 for a null context. */
+int qfec_phase_backoff(qfec_ctx* ctx);
+/* Test hook: launch `extra` workgroups beyond one per CU in phased launches
+ * (0..64; they cannot all be resident, so the first meeting times out — the
+ * abandon path; the backoff does not apply while extra > 0), and with
+ * reset_backoff clear the contention backoff (forgetting abandoned launches
+ * so far).  Waits for the stream. */
+int qfec_debug_phase(qfec_ctx* ctx, uint32_t extra, int reset_backoff);
+/* Test hook: fail != 0 makes every ragged call on this context fail with
+ * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
+ * connection integration: groups go without FEC). */
+int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

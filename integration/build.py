@@ -10,11 +10,14 @@ build them together with the MI355X FEC host code — the drop-in check
      src/net/quic/core/ next to them, as a maintainer would;
   3. `g++ -fsyntax-only` every patched translation unit and the FEC host code
      (-DQFEC_WITH_LIBQUIC: the reference's own QuicPacketHeader, StringPiece,
-     EncryptionLevel) against the reference headers — including
-     quic_connection.cc, which needs too much of libquic to link;
-  4. link the patched framer + packet creator + the FEC host code + what they
-     need from the reference tree into integration/_build/libquic_fec_patched.so
-     (C API: integration/patched_shim.cc), GPU work through libqfec.so.
+     EncryptionLevel) against the reference headers;
+  4. link the patched framer + packet creator + QuicConnection + the FEC host
+     code + what they reach in the reference tree (packet generator, packet
+     managers, congestion control, config, base/metrics: -z defs, no
+     stand-ins) into integration/_build/libquic_fec_patched.so (C API:
+     integration/patched_shim.cc — creator + framer — and
+     integration/connection_shim.cc — QuicConnection pairs over a lossy
+     in-memory writer), GPU work through libqfec.so.
 
 Only where /root/reference exists (this container); the built .so travels to
 the GPU box with the tree (git-ignored, not gpurun-ignored) for the
@@ -38,6 +41,7 @@ PATCH = os.path.join(HERE, "libquic_fec.patch")
 LIB = os.path.join(OUT, "libquic_fec_patched.so")
 
 PATCHED = ["quic_protocol.h", "quic_protocol.cc", "quic_framer.h", "quic_framer.cc",
+           "quic_connection_stats.h", "quic_connection_stats.cc",
            "quic_packet_creator.h", "quic_packet_creator.cc", "quic_packet_generator.h",
            "quic_connection.h", "quic_connection.cc"]
 FEC_HOST = ["quic_fec_group.h", "quic_fec_group.cc", "quic_fec_wire.h", "quic_fec_wire.cc",
@@ -49,6 +53,7 @@ SYNTAX_UNITS = ["quic_protocol.cc", "quic_framer.cc", "quic_packet_creator.cc",
 # linked: the patched units + the FEC host code (from _build) and, unmodified
 # from the reference tree, what the framer and the packet creator reach
 LINK_PATCHED = ["quic_protocol.cc", "quic_framer.cc", "quic_packet_creator.cc",
+                "quic_connection.cc", "quic_connection_stats.cc",
                 "quic_fec_group.cc", "quic_fec_wire.cc", "quic_fec_connection.cc"]
 LINK_REF = [
     "net/quic/core/crypto/quic_decrypter.cc", "net/quic/core/crypto/quic_encrypter.cc",
@@ -74,7 +79,37 @@ LINK_REF = [
     "base/sequence_token.cc", "base/lazy_instance.cc", "base/at_exit.cc",
     "base/callback_internal.cc", "base/vlog.cc", "base/strings/stringprintf.cc",
     "base/strings/string_number_conversions.cc", "base/memory/singleton.cc", "base/rand_util.cc",
-    "base/rand_util_posix.cc"]
+    "base/rand_util_posix.cc",
+    # what the patched QuicConnection reaches (quic_connection.cc: packet
+    # generator, sent / received packet managers, congestion control, config,
+    # UMA histograms), found by linking with -z defs until nothing is missing
+    "net/quic/core/quic_alarm.cc", "net/quic/core/quic_bandwidth.cc",
+    "net/quic/core/quic_clock.cc", "net/quic/core/quic_types.cc",
+    "net/quic/core/quic_packet_generator.cc", "net/quic/core/quic_received_packet_manager.cc",
+    "net/quic/core/quic_sent_entropy_manager.cc", "net/quic/core/quic_sent_packet_manager.cc",
+    "net/quic/core/quic_multipath_sent_packet_manager.cc",
+    "net/quic/core/quic_unacked_packet_map.cc", "net/quic/core/quic_time.cc",
+    "net/quic/core/quic_sustained_bandwidth_recorder.cc", "net/quic/core/quic_config.cc",
+    "net/quic/core/congestion_control/general_loss_algorithm.cc",
+    "net/quic/core/congestion_control/pacing_sender.cc",
+    "net/quic/core/congestion_control/rtt_stats.cc",
+    "net/quic/core/congestion_control/send_algorithm_interface.cc",
+    "net/quic/core/congestion_control/cubic.cc", "net/quic/core/congestion_control/cubic_bytes.cc",
+    "net/quic/core/congestion_control/hybrid_slow_start.cc",
+    "net/quic/core/congestion_control/prr_sender.cc",
+    "net/quic/core/congestion_control/tcp_cubic_sender_base.cc",
+    "net/quic/core/congestion_control/tcp_cubic_sender_bytes.cc",
+    "net/quic/core/congestion_control/tcp_cubic_sender_packets.cc",
+    "net/base/address_family.cc", "net/base/net_errors.cc", "base/metrics/histogram.cc",
+    "base/metrics/histogram_base.cc", "base/metrics/bucket_ranges.cc",
+    "base/metrics/histogram_samples.cc", "base/metrics/sample_vector.cc",
+    "base/metrics/statistics_recorder.cc", "base/metrics/metrics_hashes.cc",
+    "base/metrics/persistent_histogram_allocator.cc",
+    "base/metrics/persistent_memory_allocator.cc", "base/metrics/persistent_sample_map.cc",
+    "base/metrics/sample_map.cc", "base/metrics/sparse_histogram.cc", "base/values.cc",
+    "base/md5.cc", "base/pickle.cc", "base/posix/safe_strerror.cc", "base/strings/string16.cc",
+    "base/strings/utf_string_conversions.cc", "base/strings/string_util.cc",
+    "base/strings/utf_string_conversion_utils.cc", "base/third_party/icu/icu_utf.cc"]
 LINK_BSSL = [
     "crypto/cipher/aead.c", "crypto/cipher/e_aes.c", "crypto/cipher/e_chacha20poly1305.c",
     "crypto/err/err.c", "crypto/mem.c", "crypto/crypto.c", "crypto/cpu-intel.c",
@@ -124,9 +159,9 @@ def syntax_check() -> list:
         return list(ex.map(one, SYNTAX_UNITS))
 
 
-def _obj(src, flags, name):
+def _obj(src, flags, name, always=False):
     o = os.path.join(OUT, "obj", name + ".o")
-    if not os.path.exists(o) or os.path.getmtime(o) < os.path.getmtime(src):
+    if always or not os.path.exists(o) or os.path.getmtime(o) < os.path.getmtime(src):
         os.makedirs(os.path.dirname(o), exist_ok=True)
         subprocess.run([*flags, "-c", src, "-o", o], check=True)
     return o
@@ -141,7 +176,9 @@ def build_lib() -> str:
     jobs += [(os.path.join(REF, "src", u), cxx, "ref_" + u.replace("/", "_")) for u in LINK_REF]
     jobs += [(os.path.join(REF, "boringssl", u), cc, "bssl_" + u.replace("/", "_"))
              for u in LINK_BSSL]
-    jobs += [(os.path.join(HERE, "patched_shim.cc"), cxx, "patched_shim")]
+    # the shims include the patched headers (fresh copies every build)
+    jobs += [(os.path.join(HERE, "patched_shim.cc"), cxx, "patched_shim", True),
+             (os.path.join(HERE, "connection_shim.cc"), cxx, "connection_shim", True)]
     with ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(lambda j: _obj(*j), jobs))
     libdir = os.path.join(ROOT, "libquic_amd")

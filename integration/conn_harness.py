@@ -1,0 +1,59 @@
+"""ctypes binding of integration/connection_shim.cc (fec_conn_run): client /
+server pairs of the patched reference QuicConnection at QUIC_VERSION_31 over
+a lossy in-memory writer, FEC on the GPU.  Test / bench infrastructure: the
+library is integration/_build/libquic_fec_patched.so (integration/build.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libquic_fec_patched.so")
+
+
+class Params(C.Structure):
+    _fields_ = [("version", C.c_int32), ("n_pairs", C.c_int32), ("group_size", C.c_int32),
+                ("drop_every", C.c_int32), ("stream_len", C.c_uint64), ("batched", C.c_int32),
+                ("max_turns", C.c_int32), ("fail_encode", C.c_int32),
+                ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("pad", C.c_int32)]
+
+
+_U64 = ("data_packets_sent fec_packets_sent dropped revived groups_one_loss fec_groups_skipped "
+        "retransmitted stream_bytes turns launches groups_encoded groups_revived").split()
+
+
+class Result(C.Structure):
+    _fields_ = ([(n, C.c_uint64) for n in _U64] +
+                [("fec_wall_us", C.c_double), ("cpu_xor_us", C.c_double),
+                 ("cpu_xor_groups", C.c_uint64), ("streams_ok", C.c_int32),
+                 ("connected", C.c_int32), ("status", C.c_int32), ("detail", C.c_char * 256)])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: build it with python integration/build.py")
+        _lib = C.CDLL(LIB)
+        _lib.fec_conn_run.restype = C.c_int
+        _lib.fec_conn_run.argtypes = [C.POINTER(Params), C.POINTER(Result)]
+    return _lib
+
+
+def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True,
+        max_turns=20_000, fail_encode=False, require_gpu=False, version=31,
+        end_flush=True) -> dict:
+    """One simulated run; returns the result fields as a dict."""
+    p = Params(version=version, n_pairs=n_pairs, group_size=group_size, drop_every=drop_every,
+               stream_len=stream_len, batched=int(batched), max_turns=max_turns,
+               fail_encode=int(fail_encode), require_gpu=int(require_gpu),
+               no_end_flush=int(not end_flush))
+    r = Result()
+    lib().fec_conn_run(C.byref(p), C.byref(r))
+    out = {n: getattr(r, n) for n, _ in Result._fields_}
+    out["detail"] = r.detail.decode(errors="replace")
+    return out

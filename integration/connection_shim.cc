@@ -1,0 +1,573 @@
+// connection_shim.cc — end-to-end drop-in check of integration/libquic_fec.patch
+// through the REFERENCE's QuicConnection (patched): the real
+// ProcessUdpPacket -> ProcessValidatedPacket -> MaybeProcessRevivedPackets
+// receive path (quic_connection.cc:1286-1392) and the real send path
+// (SendStreamData -> QuicPacketGenerator -> QuicPacketCreator::SerializePacket
+// -> the FEC hooks -> SendOrQueuePacket -> QuicPacketWriter), with the XOR on
+// the GPU (libqfec.so).
+//
+// Built by integration/build.py into integration/_build/libquic_fec_patched.so
+// with quic_connection.cc and everything it reaches compiled from
+// /root/reference (no stand-ins).  What the harness supplies is what a
+// libquic embedder supplies (quic_connection.h:275-287, quic_alarm_factory.h,
+// quic_packet_writer.h:36-67): a simulated clock, an alarm factory whose
+// alarms the loop fires, and an in-memory packet writer per direction that
+// drops chosen client->server data packets (at most one per FEC group, never
+// an FEC packet).
+//
+//   n_pairs client/server connection pairs at QUIC_VERSION_31; every client
+//   sends stream 5 (stream_len bytes, FEC groups of group_size packets) with
+//   NULL encryption at ENCRYPTION_FORWARD_SECURE; every server reassembles it.
+//   Loop turn: complete the previous turn's batched FEC work (emits FEC
+//   packets, re-injects revived packets) -> deliver the packets written last
+//   turn -> fire due alarms -> launch this turn's FEC work (one encode + one
+//   revive GPU launch for every connection) -> advance the clock 1 ms.
+//   batched = 0 leaves the batcher out: each connection flushes one group per
+//   launch, synchronously (the latency path).
+//
+// The historical connection-thread cost of the same FEC work is timed beside
+// it: every FEC-protected packet the clients write is XORed into its group's
+// 1452-byte accumulator word by word (QuicFecGroupInterface::XorBuffers, the
+// removed reference code: SURVEY.md Appendix A), on this thread.
+#include <execinfo.h>
+#include <signal.h>
+#include <time.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "net/base/ip_address.h"
+#include "net/base/ip_endpoint.h"
+#include "net/quic/core/crypto/null_decrypter.h"
+#include "net/quic/core/crypto/null_encrypter.h"
+#include "net/quic/core/crypto/quic_random.h"
+#include "net/quic/core/quic_alarm.h"
+#include "net/quic/core/quic_alarm_factory.h"
+#include "net/quic/core/quic_clock.h"
+#include "net/quic/core/quic_connection.h"
+#include "net/quic/core/quic_fec_connection.h"
+#include "net/quic/core/quic_flags.h"
+#include "net/quic/core/quic_framer.h"
+#include "net/quic/core/quic_packet_writer.h"
+#include "net/quic/core/quic_simple_buffer_allocator.h"
+
+using namespace net;
+
+extern "C" {
+struct fec_conn_params {
+  int32_t version;      // QuicVersion (31)
+  int32_t n_pairs;      // client/server connection pairs
+  int32_t group_size;   // packets per FEC group (EnableFecSending); 0: FEC off
+  int32_t drop_every;   // drop one data packet in about one group of drop_every; 0: none
+  uint64_t stream_len;  // bytes each client sends on stream 5
+  int32_t batched;      // 1: one QuicFecBatcher for all connections
+  int32_t max_turns;
+  int32_t fail_encode;  // 1: every FEC launch fails (GPU failure path)
+  int32_t require_gpu;  // 1: fail (status 3) without a HIP device
+  int32_t no_end_flush; // 1: no SendFecPacketNow at the end (partial groups: FEC alarm only)
+  int32_t pad;
+};
+
+struct fec_conn_result {
+  uint64_t data_packets_sent;   // client->server FEC-protected data packets written
+  uint64_t fec_packets_sent;    // client FEC packets written (clients' stats agree)
+  uint64_t dropped;             // data packets the channel dropped
+  uint64_t revived;             // servers' packets_revived
+  uint64_t groups_one_loss;     // groups that lost exactly one data packet
+  uint64_t fec_groups_skipped;  // clients' fec_groups_skipped
+  uint64_t retransmitted;       // clients' packets_retransmitted
+  uint64_t stream_bytes;        // per connection
+  uint64_t turns;
+  uint64_t launches;            // batcher launches (0 unbatched)
+  uint64_t groups_encoded;      // batcher deliveries
+  uint64_t groups_revived;
+  double fec_wall_us;           // wall time inside the batcher's Launch + Complete
+  double cpu_xor_us;            // the historical per-packet XOR of the same packets, one core
+  uint64_t cpu_xor_groups;      // groups XORed by it
+  int32_t streams_ok;           // connections whose stream arrived complete and identical
+  int32_t connected;            // connections still connected at the end
+  int32_t status;               // 0 ok, else a failure code
+  char detail[256];
+};
+}
+
+namespace {
+
+double now_us() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+class SimClock : public QuicClock {
+ public:
+  QuicTime ApproximateNow() const override { return now_; }
+  QuicTime Now() const override { return now_; }
+  QuicWallTime WallNow() const override {
+    return QuicWallTime::FromUNIXMicroseconds((now_ - QuicTime::Zero()).ToMicroseconds());
+  }
+  void Advance(QuicTime::Delta d) { now_ = now_ + d; }
+
+ private:
+  QuicTime now_ = QuicTime::Zero() + QuicTime::Delta::FromMilliseconds(1000);
+};
+
+class SimAlarm;
+
+class SimAlarmFactory : public QuicAlarmFactory {
+ public:
+  QuicAlarm* CreateAlarm(QuicAlarm::Delegate* delegate) override;
+  QuicArenaScopedPtr<QuicAlarm> CreateAlarm(QuicArenaScopedPtr<QuicAlarm::Delegate> delegate,
+                                            QuicConnectionArena* arena) override;
+  // Fires every alarm due at `now` (alarms set while firing wait for the next call).
+  int FireDue(QuicTime now);
+  std::vector<SimAlarm*> alarms;
+};
+
+class SimAlarm : public QuicAlarm {
+ public:
+  SimAlarm(QuicArenaScopedPtr<Delegate> d, SimAlarmFactory* f) : QuicAlarm(std::move(d)), f_(f) {
+    f_->alarms.push_back(this);
+  }
+  ~SimAlarm() override {
+    auto& v = f_->alarms;
+    v.erase(std::remove(v.begin(), v.end(), this), v.end());
+  }
+  void FireNow() { Fire(); }
+
+ protected:
+  void SetImpl() override {}
+  void CancelImpl() override {}
+
+ private:
+  SimAlarmFactory* f_;
+};
+
+QuicAlarm* SimAlarmFactory::CreateAlarm(QuicAlarm::Delegate* delegate) {
+  return new SimAlarm(QuicArenaScopedPtr<QuicAlarm::Delegate>(delegate), this);
+}
+
+QuicArenaScopedPtr<QuicAlarm> SimAlarmFactory::CreateAlarm(
+    QuicArenaScopedPtr<QuicAlarm::Delegate> delegate, QuicConnectionArena* arena) {
+  if (arena != nullptr) return arena->New<SimAlarm>(std::move(delegate), this);
+  return QuicArenaScopedPtr<QuicAlarm>(new SimAlarm(std::move(delegate), this));
+}
+
+int SimAlarmFactory::FireDue(QuicTime now) {
+  std::vector<SimAlarm*> due;
+  for (SimAlarm* a : alarms)
+    if (a->IsSet() && a->deadline() <= now) due.push_back(a);
+  int n = 0;
+  for (SimAlarm* a : due) {
+    // an earlier alarm's callback may have cancelled or deleted this one
+    if (std::find(alarms.begin(), alarms.end(), a) == alarms.end()) continue;
+    if (!a->IsSet() || a->deadline() > now) continue;
+    a->FireNow();
+    ++n;
+  }
+  return n;
+}
+
+class SimHelper : public QuicConnectionHelperInterface {
+ public:
+  explicit SimHelper(const SimClock* clock) : clock_(clock) {}
+  const QuicClock* GetClock() const override { return clock_; }
+  QuicRandom* GetRandomGenerator() override { return QuicRandom::GetInstance(); }
+  QuicBufferAllocator* GetBufferAllocator() override { return &allocator_; }
+
+ private:
+  const SimClock* clock_;
+  SimpleBufferAllocator allocator_;
+};
+
+// Parses the packets one direction writes (in write order: the framer expands
+// truncated packet numbers against the last one it saw) for the drop policy.
+class HeaderProbe : public QuicFramerVisitorInterface {
+ public:
+  explicit HeaderProbe(QuicVersion v)
+      : framer_(QuicVersionVector{v}, QuicTime::Zero(), Perspective::IS_SERVER) {
+    framer_.set_version(v);
+    framer_.set_visitor(this);
+    framer_.SetDecrypter(ENCRYPTION_FORWARD_SECURE, new NullDecrypter());
+  }
+  // false if the packet could not be parsed (header is then invalid)
+  bool Parse(const char* p, size_t n, QuicPacketHeader* h, std::string* payload) {
+    ok_ = false;
+    payload_ = payload;
+    QuicEncryptedPacket pkt(p, n, false);
+    framer_.ProcessPacket(pkt);
+    if (ok_) *h = header_;
+    return ok_;
+  }
+
+  void OnError(QuicFramer*) override {}
+  bool OnProtocolVersionMismatch(QuicVersion) override { return false; }
+  void OnPacket() override {}
+  void OnPublicResetPacket(const QuicPublicResetPacket&) override {}
+  void OnVersionNegotiationPacket(const QuicVersionNegotiationPacket&) override {}
+  bool OnUnauthenticatedPublicHeader(const QuicPacketPublicHeader&) override { return true; }
+  bool OnUnauthenticatedHeader(const QuicPacketHeader&) override { return true; }
+  void OnDecryptedPacket(EncryptionLevel) override {}
+  bool OnPacketHeader(const QuicPacketHeader& h) override {
+    header_ = h;
+    ok_ = true;
+    return true;  // go on: the FEC callbacks hand over the protected payload
+  }
+  bool OnStreamFrame(const QuicStreamFrame&) override { return true; }
+  bool OnAckFrame(const QuicAckFrame&) override { return true; }
+  bool OnStopWaitingFrame(const QuicStopWaitingFrame&) override { return true; }
+  bool OnPaddingFrame(const QuicPaddingFrame&) override { return true; }
+  bool OnPingFrame(const QuicPingFrame&) override { return true; }
+  bool OnRstStreamFrame(const QuicRstStreamFrame&) override { return true; }
+  bool OnConnectionCloseFrame(const QuicConnectionCloseFrame&) override { return true; }
+  bool OnGoAwayFrame(const QuicGoAwayFrame&) override { return true; }
+  bool OnWindowUpdateFrame(const QuicWindowUpdateFrame&) override { return true; }
+  bool OnBlockedFrame(const QuicBlockedFrame&) override { return true; }
+  bool OnPathCloseFrame(const QuicPathCloseFrame&) override { return true; }
+  void OnPacketComplete() override {}
+  void OnFecProtectedPayload(base::StringPiece payload) override {
+    if (payload_) payload_->assign(payload.data(), payload.size());
+  }
+
+ private:
+  QuicFramer framer_;
+  QuicPacketHeader header_;
+  std::string* payload_ = nullptr;
+  bool ok_ = false;
+};
+
+struct Wire {
+  std::vector<std::string> now, next;  // packets in flight (delivered next turn)
+};
+
+struct Run;
+
+class SimWriter : public QuicPacketWriter {
+ public:
+  SimWriter(Run* run, Wire* wire, bool client, QuicVersion v)
+      : run_(run), wire_(wire), client_(client), probe_(v) {}
+  WriteResult WritePacket(const char* buffer, size_t buf_len, const IPAddress&,
+                          const IPEndPoint&, PerPacketOptions*) override;
+  bool IsWriteBlockedDataBuffered() const override { return false; }
+  bool IsWriteBlocked() const override { return false; }
+  void SetWritable() override {}
+  QuicByteCount GetMaxPacketSize(const IPEndPoint&) const override { return kMaxPacketSize; }
+
+  // historical connection-thread XOR state per open group
+  std::map<QuicFecGroupNumber, std::vector<uint64_t>> xor_acc;
+  std::map<QuicFecGroupNumber, int> dropped_in_group;
+
+ private:
+  Run* run_;
+  Wire* wire_;
+  bool client_;
+  HeaderProbe probe_;
+  std::string payload_;
+};
+
+class Endpoint : public QuicConnectionVisitorInterface {
+ public:
+  Endpoint(Run* run, bool client, size_t stream_len) : run_(run), client_(client) {
+    if (!client) {
+      received.assign(stream_len, '\0');
+      have.assign(stream_len, 0);
+    }
+  }
+  // client: push stream data while the connection takes it
+  void Pump();
+
+  void OnStreamFrame(const QuicStreamFrame& f) override {
+    if (client_ || f.stream_id != 5) return;
+    if (f.offset + f.data_length > received.size()) {
+      bad_frame = true;
+      return;
+    }
+    std::memcpy(&received[f.offset], f.data_buffer, f.data_length);
+    std::memset(&have[f.offset], 1, f.data_length);
+    if (f.fin) fin = true;
+  }
+  void OnWindowUpdateFrame(const QuicWindowUpdateFrame&) override {}
+  void OnBlockedFrame(const QuicBlockedFrame&) override {}
+  void OnRstStream(const QuicRstStreamFrame&) override {}
+  void OnGoAway(const QuicGoAwayFrame&) override {}
+  void OnConnectionClosed(QuicErrorCode error, const std::string& details,
+                          ConnectionCloseSource) override {
+    closed = true;
+    close_error = error;
+    close_details = details;
+  }
+  void OnWriteBlocked() override {}
+  void OnSuccessfulVersionNegotiation(const QuicVersion&) override {}
+  void OnCanWrite() override { Pump(); }
+  void OnCongestionWindowChange(QuicTime) override {}
+  void OnConnectionMigration(PeerAddressChangeType) override {}
+  void OnPathDegrading() override {}
+  void PostProcessAfterData() override {}
+  bool WillingAndAbleToWrite() const override { return client_ && sent < run_data_len(); }
+  bool HasPendingHandshake() const override { return false; }
+  bool HasOpenDynamicStreams() const override { return WillingAndAbleToWrite(); }
+
+  size_t run_data_len() const;
+
+  QuicConnection* conn = nullptr;
+  uint64_t sent = 0;  // client: stream bytes consumed
+  std::string received;
+  std::vector<uint8_t> have;
+  bool fin = false, bad_frame = false, closed = false;
+  QuicErrorCode close_error = QUIC_NO_ERROR;
+  std::string close_details;
+
+ private:
+  Run* run_;
+  bool client_;
+};
+
+struct Run {
+  fec_conn_params p;
+  fec_conn_result* r;
+  std::string data;  // the stream every client sends
+  QuicVersion version;
+};
+
+size_t Endpoint::run_data_len() const { return run_->data.size(); }
+
+void Endpoint::Pump() {
+  if (!client_ || closed) return;
+  while (sent < run_->data.size() && conn->CanWriteStreamData()) {
+    struct iovec iov;
+    iov.iov_base = const_cast<char*>(run_->data.data() + sent);
+    iov.iov_len = run_->data.size() - sent;
+    QuicIOVector io(&iov, 1, iov.iov_len);
+    const QuicConsumedData c = conn->SendStreamData(5, io, sent, /*fin=*/true, nullptr);
+    sent += c.bytes_consumed;
+    if (c.bytes_consumed == 0) break;
+  }
+}
+
+// About one group in drop_every loses the data packet at a per-group offset.
+bool DropPolicy(const fec_conn_params& p, QuicFecGroupNumber g, QuicPacketNumber pn) {
+  if (p.drop_every <= 0) return false;
+  const uint64_t h = (g + 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+  if ((h >> 33) % (uint64_t)p.drop_every != 0) return false;
+  // one of the group's first 8 packets (a short last group has them too)
+  return pn - g == (h >> 17) % (uint64_t)std::min(8, std::max(1, p.group_size));
+}
+
+WriteResult SimWriter::WritePacket(const char* buffer, size_t buf_len, const IPAddress&,
+                                   const IPEndPoint&, PerPacketOptions*) {
+  if (client_) {
+    QuicPacketHeader h;
+    payload_.clear();
+    const bool parsed = probe_.Parse(buffer, buf_len, &h, &payload_);
+    if (parsed && h.is_in_fec_group != IN_FEC_GROUP && run_->p.group_size <= 0 &&
+        DropPolicy(run_->p, h.packet_number & ~uint64_t(7), h.packet_number)) {
+      ++run_->r->dropped;  // FEC off: the reference's loss recovery alone
+      return WriteResult(WRITE_STATUS_OK, static_cast<int>(buf_len));
+    }
+    if (parsed && h.is_in_fec_group == IN_FEC_GROUP) {
+      if (h.fec_flag) {
+        ++run_->r->fec_packets_sent;
+        if (dropped_in_group[h.fec_group] == 1) ++run_->r->groups_one_loss;
+        dropped_in_group.erase(h.fec_group);
+        auto it = xor_acc.find(h.fec_group);
+        if (it != xor_acc.end()) {
+          ++run_->r->cpu_xor_groups;
+          xor_acc.erase(it);
+        }
+      } else {
+        ++run_->r->data_packets_sent;
+        // the historical sender: XorBuffers of this packet's protected
+        // plaintext into the group's accumulator, on the connection thread
+        const double t0 = now_us();
+        std::vector<uint64_t>& acc = xor_acc[h.fec_group];
+        if (acc.empty()) acc.assign(kMaxPacketSize / 8 + 1, 0);
+        const size_t nw = payload_.size() / 8;
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(payload_.data());
+        uint64_t* a = acc.data();
+        for (size_t i = 0; i < nw; ++i) a[i] ^= w[i];
+        uint8_t* ab = reinterpret_cast<uint8_t*>(a);
+        for (size_t i = nw * 8; i < payload_.size(); ++i) ab[i] ^= (uint8_t)payload_[i];
+        run_->r->cpu_xor_us += now_us() - t0;
+        if (DropPolicy(run_->p, h.fec_group, h.packet_number) &&
+            dropped_in_group[h.fec_group] == 0) {
+          ++dropped_in_group[h.fec_group];
+          ++run_->r->dropped;
+          return WriteResult(WRITE_STATUS_OK, static_cast<int>(buf_len));
+        }
+      }
+    }
+  }
+  wire_->next.emplace_back(buffer, buf_len);
+  return WriteResult(WRITE_STATUS_OK, static_cast<int>(buf_len));
+}
+
+void crash_trace(int sig) {
+  void* f[64];
+  const int n = backtrace(f, 64);
+  backtrace_symbols_fd(f, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+}  // namespace
+
+#define SHIM_API extern "C" __attribute__((visibility("default")))
+
+SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
+  std::memset(r, 0, sizeof(*r));
+  signal(SIGSEGV, crash_trace);
+  signal(SIGABRT, crash_trace);
+  FLAGS_quic_disable_pre_32 = false;  // QUIC_VERSION_31 carries FEC
+  Run run;
+  run.p = *params;
+  run.r = r;
+  run.version = static_cast<QuicVersion>(params->version);
+  run.data.resize(params->stream_len);
+  for (uint64_t i = 0; i < params->stream_len; ++i)
+    run.data[i] = static_cast<char>((i * 2654435761u) >> 13);
+  const int n = params->n_pairs;
+  const QuicVersionVector versions{run.version};
+
+  SimClock clock;
+  SimHelper helper(&clock);
+  SimAlarmFactory alarms;
+  // Without a device every FEC launch fails (QuicFecGroup has no CPU path):
+  // the groups go without FEC and the reference's loss recovery delivers the
+  // stream — the GPU-failure path, runnable on the CPU.  fail_encode forces
+  // that path on a GPU (qfec_debug_fail_launches on the batcher's context).
+  qfec_ctx* ctx = params->group_size > 0 ? qfec_create(0) : nullptr;
+  if (!ctx && params->require_gpu) {
+    std::snprintf(r->detail, sizeof(r->detail), "qfec_create: %s", qfec_last_error(nullptr));
+    return r->status = 3;
+  }
+  if (ctx && params->fail_encode) qfec_debug_fail_launches(ctx, 1);
+  std::unique_ptr<QuicFecBatcher> batcher;
+  if (params->batched) batcher.reset(new QuicFecBatcher(ctx));
+  if (!params->batched && params->fail_encode) {
+    std::snprintf(r->detail, sizeof(r->detail), "fail_encode needs batched (the batcher's context)");
+    return r->status = 4;
+  }
+
+  std::vector<std::unique_ptr<Wire>> c2s(n), s2c(n);
+  std::vector<std::unique_ptr<SimWriter>> cw(n), sw(n);
+  std::vector<std::unique_ptr<Endpoint>> ce(n), se(n);
+  std::vector<std::unique_ptr<QuicConnection>> cc(n), sc(n);
+  const IPEndPoint client_addr(IPAddress(10, 0, 0, 1), 4433);
+  for (int i = 0; i < n; ++i) {
+    c2s[i].reset(new Wire());
+    s2c[i].reset(new Wire());
+    cw[i].reset(new SimWriter(&run, c2s[i].get(), true, run.version));
+    sw[i].reset(new SimWriter(&run, s2c[i].get(), false, run.version));
+    ce[i].reset(new Endpoint(&run, true, params->stream_len));
+    se[i].reset(new Endpoint(&run, false, params->stream_len));
+    const QuicConnectionId cid = 0x5100000000ull + i;
+    const IPEndPoint server_addr(IPAddress(10, 0, 1, (uint8_t)(1 + i % 250)), 443);
+    cc[i].reset(new QuicConnection(cid, server_addr, &helper, &alarms, cw[i].get(), false,
+                                   Perspective::IS_CLIENT, versions));
+    sc[i].reset(new QuicConnection(cid, client_addr, &helper, &alarms, sw[i].get(), false,
+                                   Perspective::IS_SERVER, versions));
+    for (QuicConnection* c : {cc[i].get(), sc[i].get()}) {
+      c->SetEncrypter(ENCRYPTION_FORWARD_SECURE, new NullEncrypter());
+      c->SetDefaultEncryptionLevel(ENCRYPTION_FORWARD_SECURE);
+      c->SetDecrypter(ENCRYPTION_FORWARD_SECURE, new NullDecrypter());
+      if (batcher) c->set_fec_batcher(batcher.get());
+    }
+    cc[i]->set_visitor(ce[i].get());
+    sc[i]->set_visitor(se[i].get());
+    ce[i]->conn = cc[i].get();
+    se[i]->conn = sc[i].get();
+    if (params->group_size > 0) cc[i]->EnableFecSending(params->group_size);
+  }
+  for (int i = 0; i < n; ++i) ce[i]->Pump();
+
+  const IPEndPoint server_self(IPAddress(10, 0, 1, 1), 443);
+  int turn = 0;
+  bool flushed = false;
+  for (; turn < params->max_turns; ++turn) {
+    if (batcher) {
+      const double t0 = now_us();
+      batcher->Complete(true);  // emits FEC packets, re-injects revived ones
+      r->fec_wall_us += now_us() - t0;
+    }
+    bool in_flight = false;
+    for (int i = 0; i < n; ++i) {
+      c2s[i]->now.swap(c2s[i]->next);
+      s2c[i]->now.swap(s2c[i]->next);
+      for (const std::string& pk : c2s[i]->now)
+        sc[i]->ProcessUdpPacket(server_self, client_addr,
+                                QuicReceivedPacket(pk.data(), pk.size(), clock.Now()));
+      for (const std::string& pk : s2c[i]->now)
+        cc[i]->ProcessUdpPacket(client_addr, server_self,
+                                QuicReceivedPacket(pk.data(), pk.size(), clock.Now()));
+      in_flight = in_flight || !c2s[i]->now.empty() || !s2c[i]->now.empty();
+      c2s[i]->now.clear();
+      s2c[i]->now.clear();
+    }
+    alarms.FireDue(clock.Now());
+    if (batcher) {
+      const double t0 = now_us();
+      batcher->Launch();  // the GPU works while the next turn starts
+      r->fec_wall_us += now_us() - t0;
+    }
+    clock.Advance(QuicTime::Delta::FromMilliseconds(1));
+    bool done = true;
+    for (int i = 0; i < n && done; ++i) {
+      const bool complete = se[i]->fin && std::all_of(se[i]->have.begin(), se[i]->have.end(),
+                                                      [](uint8_t b) { return b != 0; });
+      done = (complete || ce[i]->closed || se[i]->closed) && !cc[i]->HasQueuedData() &&
+             !(params->no_end_flush && cc[i]->connected() && cc[i]->IsFecGroupOpen());
+    }
+    bool wire_busy = false;
+    for (int i = 0; i < n; ++i)
+      wire_busy = wire_busy || !c2s[i]->next.empty() || !s2c[i]->next.empty();
+    if (done && !wire_busy && !(batcher && (batcher->InFlight() || batcher->NumQueued()))) {
+      // the end of the data: close every partial group now (as the FEC alarm
+      // would), so that every group's FEC packet is sent and counted
+      if (!flushed && params->group_size > 0 && !params->no_end_flush) {
+        flushed = true;
+        for (int i = 0; i < n; ++i)
+          if (cc[i]->connected()) cc[i]->SendFecPacketNow();
+        continue;
+      }
+      break;
+    }
+    (void)in_flight;
+  }
+  if (batcher) {
+    batcher->Complete(true);
+    r->launches = batcher->stats().launches;
+    r->groups_encoded = batcher->stats().groups_encoded;
+    r->groups_revived = batcher->stats().groups_revived;
+  }
+  r->turns = turn;
+  r->stream_bytes = params->stream_len;
+  std::string first_close;
+  for (int i = 0; i < n; ++i) {
+    const QuicConnectionStats& cs = cc[i]->GetStats();
+    const QuicConnectionStats& ss = sc[i]->GetStats();
+    r->revived += ss.packets_revived;
+    r->fec_groups_skipped += cs.fec_groups_skipped;
+    r->retransmitted += cs.packets_retransmitted;
+    const bool ok = se[i]->fin && !se[i]->bad_frame && se[i]->received == run.data;
+    r->streams_ok += ok ? 1 : 0;
+    r->connected += (cc[i]->connected() && sc[i]->connected()) ? 1 : 0;
+    if (first_close.empty() && (ce[i]->closed || se[i]->closed))
+      first_close = (ce[i]->closed ? "client " + ce[i]->close_details
+                                   : "server " + se[i]->close_details);
+  }
+  if (!first_close.empty())
+    std::snprintf(r->detail, sizeof(r->detail), "closed: %s", first_close.c_str());
+  // connections before the batcher (they Forget themselves), the batcher
+  // before its contexts
+  cc.clear();
+  sc.clear();
+  batcher.reset();
+  if (ctx) qfec_destroy(ctx);
+  return r->status;
+}

@@ -62,9 +62,40 @@ struct qfec_ctx {
   // sync words of the phased fixed-shape kernel (20 x 256 B; words 0-18 zero
   // between launches, word 19 counts abandoned launches)
   uint32_t* d_phase = nullptr;
+  // phased launches of this context share d_phase, so they must not overlap:
+  // after each one phase_done is recorded on its stream, and a phased launch
+  // on another stream first waits for it
+  hipEvent_t phase_done = nullptr;
+  hipStream_t phase_stream = nullptr;
+  bool phase_recorded = false;
+  // contention policy: the last workgroup of a phased launch copies the
+  // abandoned-launch count into h_phase (pinned, mapped); a launch that finds
+  // it grown (another context / process kept CUs busy) runs the
+  // next kPhaseBackoff large batches with the one-pass kernel, then tries the
+  // phased one again
+  uint32_t* h_phase = nullptr;
+  uint32_t* h_phase_dev = nullptr;
+  uint32_t phase_seen = 0;
+  uint32_t phase_backoff = 0;
+  uint32_t ncu = 0;          // CU count, queried once
+  uint32_t phase_extra = 0;  // test hook (qfec_debug_phase)
+  bool debug_fail = false;   // test hook (qfec_debug_fail_launches)
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
   uint32_t flag_token = 0;
+  // QFEC_ASYNC mapped ragged calls still running, one per staging slot
+  // (qfec_complete finishes them in issue order)
+  struct AsyncOp {
+    bool live = false;
+    bool direct = false;   // completion by the host-mapped flag (token)
+    bool recover = false;
+    uint32_t token = 0;
+    uint64_t cnt = 0;
+    uint16_t* parity_len_out = nullptr;  // encode: the caller's lengths, filled at completion
+    uint64_t seq = 0;
+  } async_ops[kSlots];
+  int async_next = 0;
+  uint64_t async_seq = 0;
   // device scratch of the host-pointer xor / protection / entropy calls:
   // grow-only buffers kept for the context's life (no allocation per call)
   std::vector<void*> scratch_p;
@@ -150,6 +181,57 @@ int wait_flag(qfec_ctx* ctx, int si, uint32_t token) {
   }
 }
 
+int collect_error(qfec_ctx* ctx, hipStream_t stream);
+
+// Finish the QFEC_ASYNC op of slot `si`: QFEC_PENDING if it is still running
+// and !wait; otherwise its encode lengths are copied out and its error word
+// collected (batches above kDirectGroups latch kernel-side errors).
+int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
+  qfec_ctx::AsyncOp& op = ctx->async_ops[si];
+  if (!op.live) return QFEC_OK;
+  Slot& s = ctx->slots[si];
+  if (op.direct) {
+    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
+      const hipError_t q = hipEventQuery(s.done);
+      if (q == hipErrorNotReady) return QFEC_PENDING;
+      if (q != hipSuccess) {
+        op.live = false;
+        QFEC_HIP(ctx, q);
+      }
+    }
+    op.live = false;
+    const int wrc = wait_flag(ctx, si, op.token);
+    if (wrc) return wrc;
+  } else {
+    if (!wait) {
+      const hipError_t q = hipEventQuery(s.done);
+      if (q == hipErrorNotReady) return QFEC_PENDING;
+    }
+    op.live = false;
+    QFEC_HIP(ctx, hipEventSynchronize(s.done));
+  }
+  if (!op.recover && op.parity_len_out)
+    std::memcpy(op.parity_len_out, s.h_out, op.cnt * sizeof(uint16_t));
+  return op.direct ? QFEC_OK : collect_error(ctx, s.stream);
+}
+
+// Complete every outstanding QFEC_ASYNC op in issue order; the first error
+// is returned after all have been finished (or QFEC_PENDING when !wait and
+// one is still running: the ones before it are finished).
+int complete_async(qfec_ctx* ctx, bool wait) {
+  int first = QFEC_OK;
+  for (;;) {
+    int si = -1;
+    for (int i = 0; i < kSlots; ++i)
+      if (ctx->async_ops[i].live && (si < 0 || ctx->async_ops[i].seq < ctx->async_ops[si].seq))
+        si = i;
+    if (si < 0) return first;
+    const int rc = complete_async_op(ctx, si, wait);
+    if (rc == QFEC_PENDING) return first ? first : QFEC_PENDING;
+    if (rc && !first) first = rc;
+  }
+}
+
 int check_fixed(qfec_ctx* ctx, uint32_t k, uint32_t L, uint64_t row_stride,
                 uint64_t group_stride, uint64_t parity_stride, uint64_t out_stride) {
   if (k < 1 || k > QFEC_MAX_GROUP_PACKETS)
@@ -199,6 +281,7 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
                uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
+  if ((rc = complete_async(ctx, true))) return rc;
   const bool recover = parity != nullptr;
   const bool rows_pinned = is_pinned_or_device(rows);
   const bool par_pinned = recover && is_pinned_or_device(parity);
@@ -342,6 +425,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
                  uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
+  if ((rc = complete_async(ctx, true))) return rc;
   const bool recover = parity != nullptr;
   if ((rc = check_mapped(ctx, rows, "rows")) || (rc = check_mapped(ctx, out, "out")) ||
       (recover && (rc = check_mapped(ctx, parity, "parity"))))
@@ -395,6 +479,46 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream);
 }
 
+
+// A device-pointer fixed-shape launch on the context stream.  Phased launches
+// (large nt batches) share the context's sync words: one on a different stream
+// than the previous phased launch first waits for that one's completion event
+// (they would otherwise update the same counters concurrently and zero each
+// other's meetings).  A phased launch that was abandoned since the last look
+// (h_phase, copied by the kernel) switches the next kPhaseBackoff large
+// batches to the one-pass kernel: a contended GPU runs the phased kernel
+// without its meetings anyway, at 4 waves per CU.
+constexpr uint32_t kPhaseBackoff = 16;
+
+int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
+  const bool nt = (flags & QFEC_CACHED) == 0;
+  a.ncu = ctx->ncu;
+  a.phase_extra = ctx->phase_extra;
+  a.phase_host = ctx->h_phase_dev;
+  a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
+  if (a.phase_sync && qfec::fixed_uses_phases(a, nt)) {
+    const uint32_t seen = __atomic_load_n(ctx->h_phase, __ATOMIC_ACQUIRE);
+    if (seen != ctx->phase_seen) {
+      ctx->phase_seen = seen;
+      ctx->phase_backoff = kPhaseBackoff;
+    }
+    if (ctx->phase_backoff > 0 && ctx->phase_extra == 0) {
+      --ctx->phase_backoff;
+      a.phase_sync = nullptr;  // one-pass while contention persists
+    } else {
+      if (ctx->phase_recorded && ctx->phase_stream != ctx->stream)
+        QFEC_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->phase_done, 0));
+      QFEC_HIP(ctx, qfec::launch_fixed(a, nt, ctx->stream));
+      QFEC_HIP(ctx, hipEventRecord(ctx->phase_done, ctx->stream));
+      ctx->phase_stream = ctx->stream;
+      ctx->phase_recorded = true;
+      return QFEC_OK;
+    }
+  }
+  QFEC_HIP(ctx, qfec::launch_fixed(a, nt, ctx->stream));
+  return QFEC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -407,6 +531,17 @@ void* qfec_host_alloc(size_t bytes) {
       hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable);
   if (e != hipSuccess) {
     fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_alloc(%zu): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  // QFEC_PTR_MAPPED hands host pointers to the kernels unchanged (as for
+  // qfec_host_register): refuse memory the device addresses elsewhere
+  void* dev = nullptr;
+  const hipError_t d = hipHostGetDevicePointer(&dev, p, 0);
+  if (d != hipSuccess || dev != p) {
+    (void)hipHostFree(p);
+    fail(nullptr, QFEC_ERR_INTERNAL,
+         "qfec_host_alloc(%zu): device address %p differs from the host address %p (%s); "
+         "QFEC_PTR_MAPPED needs them equal", bytes, dev, p, hipGetErrorString(d));
     return nullptr;
   }
   return p;
@@ -543,12 +678,22 @@ qfec_ctx* qfec_create(int device) {
             hipMemset(ctx->d_err, 0, sizeof(uint32_t)) == hipSuccess &&
             hipMalloc(&ctx->d_phase, kPhaseSyncBytes) == hipSuccess &&
             hipMemset(ctx->d_phase, 0, kPhaseSyncBytes) == hipSuccess &&
-            hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+            hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&ctx->h_phase, sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->h_phase_dev), ctx->h_phase,
+                                    0) == hipSuccess &&
+            hipEventCreateWithFlags(&ctx->phase_done, hipEventDisableTiming) == hipSuccess;
+  int ncu = 0;
+  ok = ok && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) ==
+                 hipSuccess;
   if (!ok) {
     fail(nullptr, QFEC_ERR_INTERNAL, "HIP initialisation failed on device %d", device);
     qfec_destroy(ctx);
     return nullptr;
   }
+  *ctx->h_phase = 0;
+  ctx->ncu = ncu > 0 ? (uint32_t)ncu : 0;
   ctx->stream = ctx->own_stream;
   return ctx;
 }
@@ -574,6 +719,8 @@ void qfec_destroy(qfec_ctx* ctx) {
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->h_err) (void)hipHostFree(ctx->h_err);
+  if (ctx->h_phase) (void)hipHostFree(ctx->h_phase);
+  if (ctx->phase_done) (void)hipEventDestroy(ctx->phase_done);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -592,6 +739,12 @@ int qfec_sync(qfec_ctx* ctx) {
   int rc = bind(ctx);
   if (rc) return rc;
   return collect_error(ctx, ctx->stream);
+}
+
+int qfec_complete(qfec_ctx* ctx, int wait) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  return complete_async(ctx, wait != 0);
 }
 
 int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
@@ -621,9 +774,7 @@ int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, ui
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
-  a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
-  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
-  return QFEC_OK;
+  return fixed_device(ctx, a, flags);
 }
 
 int qfec_encode_batch(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
@@ -670,9 +821,7 @@ int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t
   a.k = k;
   a.L = L;
   a.err = ctx->d_err;
-  a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
-  QFEC_HIP(ctx, qfec::launch_fixed(a, (flags & QFEC_CACHED) == 0, ctx->stream));
-  return QFEC_OK;
+  return fixed_device(ctx, a, flags);
 }
 
 int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity,
@@ -783,6 +932,7 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
                 uint8_t* out, const uint64_t* out_off) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
+  if ((rc = complete_async(ctx, true))) return rc;
   if ((rc = validate_ragged(ctx, recover, pkt_len, grp_ptr, n, parity_len, missing))) return rc;
 
   const uint64_t in_cap = kStageBytes, out_cap = kStageBytes / 4;
@@ -916,7 +1066,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
                   const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n,
                   const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
                   const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
-                  uint8_t* out, const uint64_t* out_off) {
+                  uint8_t* out, const uint64_t* out_off, bool async) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
   if ((rc = check_mapped(ctx, bytes, "bytes")) ||
@@ -958,13 +1108,23 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     return QFEC_OK;
   };
   const uint64_t out_cap = mapped_chunk_groups((kStageBytes / 4) / sizeof(uint16_t));
+  // QFEC_ASYNC: a batch whose tables fit one slot returns once it is queued
+  // and completes in qfec_complete; a larger one runs synchronously.  The
+  // other calls that use the slots finish the async ones first.
+  async = async && n <= out_cap && Tab(grp_ptr[n] - grp_ptr[0], n, recover).total <= kStageBytes;
+  int slot = 0;
+  if (async) {
+    slot = ctx->async_next;
+    if ((rc = complete_async_op(ctx, slot, true))) return rc;
+  } else if ((rc = complete_async(ctx, true))) {
+    return rc;
+  }
   // A small batch (the connection thread's flush of a few groups) is
   // latency-bound: the kernel reads the tables from the mapped slot buffer and
   // writes the encode lengths straight into the mapped output buffer — no
   // copies, one launch and one synchronisation — and the error word is not
   // fetched: validate_ragged checked every condition the kernel latches.
   const bool direct = n <= std::min<uint64_t>(out_cap, kDirectGroups);
-  int slot = 0;
   uint64_t g = 0;
   while (g < n) {
     const uint64_t g0 = g;
@@ -1024,6 +1184,18 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
                                    hipMemcpyDeviceToHost, s.stream));
     QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    if (async) {  // the whole batch in this slot: completed by qfec_complete
+      qfec_ctx::AsyncOp& op = ctx->async_ops[slot];
+      op.live = true;
+      op.direct = direct;
+      op.recover = recover;
+      op.token = token;
+      op.cnt = cnt;
+      op.parity_len_out = recover ? nullptr : parity_len_out;
+      op.seq = ++ctx->async_seq;
+      ctx->async_next = (slot + 1) % kSlots;
+      return QFEC_OK;
+    }
     pend[slot].g0 = g0;
     pend[slot].cnt = cnt;
     pend[slot].token = token;
@@ -1043,6 +1215,8 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
                        uint16_t* parity_len_out, uint32_t flags) {
   int rc = bind(ctx);
   if (rc) return rc;
+  if (ctx->debug_fail)
+    return fail(ctx, QFEC_ERR_INTERNAL, "launch failure injected (qfec_debug_fail_launches)");
   if (n_groups == 0) return QFEC_OK;
   if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity_out || !parity_off || !parity_len_out)
     return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
@@ -1051,7 +1225,7 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
   if (flags & QFEC_PTR_MAPPED)
     return ragged_mapped(ctx, false, bytes, pkt_off, pkt_len, grp_ptr, n_groups, nullptr,
                          parity_out, parity_off, nullptr, parity_len_out, nullptr, nullptr,
-                         nullptr);
+                         nullptr, (flags & QFEC_ASYNC) != 0);
   if (flags & QFEC_PTR_HOST)
     return ragged_host(ctx, false, bytes, pkt_off, pkt_len, grp_ptr, n_groups, nullptr,
                        parity_out, parity_off, nullptr, parity_len_out, nullptr, nullptr,
@@ -1077,6 +1251,8 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
                         const uint64_t* out_off, uint32_t flags) {
   int rc = bind(ctx);
   if (rc) return rc;
+  if (ctx->debug_fail)
+    return fail(ctx, QFEC_ERR_INTERNAL, "launch failure injected (qfec_debug_fail_launches)");
   if (n_groups == 0) return QFEC_OK;
   if (!bytes || !pkt_off || !pkt_len || !grp_ptr || !parity || !parity_off || !parity_len ||
       !missing_idx || !out || !out_off)
@@ -1098,7 +1274,8 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
     }
     if (flags & QFEC_PTR_MAPPED)
       return ragged_mapped(ctx, true, bytes, pkt_off, pkt_len, grp_ptr, n_groups, parity,
-                           nullptr, parity_off, parity_len, nullptr, missing_idx, out, out_off);
+                           nullptr, parity_off, parity_len, nullptr, missing_idx, out, out_off,
+                           (flags & QFEC_ASYNC) != 0);
     return ragged_host(ctx, true, bytes, pkt_off, pkt_len, grp_ptr, n_groups, parity, nullptr,
                        parity_off, parity_len, nullptr, missing_idx, out, out_off);
   }
@@ -1386,6 +1563,26 @@ int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count) {
   if (!count) return fail(ctx, QFEC_ERR_INTERNAL, "null count");
   QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   QFEC_HIP(ctx, hipMemcpy(count, ctx->d_phase + 64 * 19, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return QFEC_OK;
+}
+
+int qfec_phase_backoff(qfec_ctx* ctx) { return ctx ? (int)ctx->phase_backoff : -1; }
+
+int qfec_debug_fail_launches(qfec_ctx* ctx, int on) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  ctx->debug_fail = on != 0;
+  return QFEC_OK;
+}
+
+int qfec_debug_phase(qfec_ctx* ctx, uint32_t extra, int reset_backoff) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  QFEC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->phase_extra = std::min<uint32_t>(extra, 64u);
+  if (reset_backoff) {
+    ctx->phase_seen = __atomic_load_n(ctx->h_phase, __ATOMIC_ACQUIRE);
+    ctx->phase_backoff = 0;
+  }
   return QFEC_OK;
 }
 

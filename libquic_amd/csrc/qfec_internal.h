@@ -36,7 +36,18 @@ struct FixedArgs {
   // large nt batches: 19 x 256 B of zeroed sync words for the phased kernel
   // (phase_xor_kernel); nullptr: always the one-pass fixed kernel
   uint32_t* phase_sync = nullptr;
+  // phased kernel: the device's CU count (cached by the context: one
+  // workgroup per CU), extra workgroups beyond it (test hook: forces the
+  // abandon path), and a host-mapped word the last workgroup out copies the
+  // abandoned-launch count into (nullable) — the context reads it at the next
+  // launch without a synchronisation
+  uint32_t ncu = 0;
+  uint32_t phase_extra = 0;
+  uint32_t* phase_host = nullptr;
 };
+
+// True if launch_fixed(a, nontemporal, ...) runs the phased kernel.
+bool fixed_uses_phases(const FixedArgs& a, bool nontemporal);
 
 struct RaggedArgs {
   const uint8_t* bytes;

@@ -237,14 +237,20 @@ __device__ __forceinline__ void phase_meet(uint32_t* ps, uint32_t epoch) {
 }
 
 // The last workgroup out zeroes the sync words for the next launch on the
-// stream (vector atomics; the launch boundary orders them before it).
-__device__ __forceinline__ void phase_exit(uint32_t* ps) {
+// stream (vector atomics; the launch boundary orders them before it) and
+// copies the abandoned-launch count into the context's host-mapped word
+// (a vector store at system scope), where the host reads it at the next
+// launch without waiting for this one.
+__device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
   __syncthreads();
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(ph_word(ps, 17), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
           gridDim.x - 1u) {
     for (uint32_t i = 0; i < 19u; ++i)
       __hip_atomic_store(ph_word(ps, i), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host)
+      __hip_atomic_store(host, ph_load(ph_word(ps, 19)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -434,7 +440,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     }
     if constexpr (MEET2) phase_meet(a.phase_sync, 2u * p + 2u);
   }
-  phase_exit(a.phase_sync);
+  phase_exit(a.phase_sync, a.phase_host);
 }
 
 // Fixed shape, L < 16 (degenerate tiny packets): one lane per output byte.
@@ -1427,25 +1433,28 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
 // than they do.  Returns false when it does not apply.
 constexpr uint32_t kPhMinPhases = 8;
 
+// The CU count comes cached from the context (FixedArgs::ncu); the test hook
+// phase_extra (tests/test_hip_phase.py) adds workgroups beyond one per CU,
+// which cannot all be resident, so the first meeting times out — the abandon
+// path.
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      ncu <= 0)
-    return false;
-  // test hook (tests/test_hip_phase.py): extra workgroups beyond one per CU
-  // cannot all be resident, so the first meeting times out — the abandon path
-  const char* extra = std::getenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS");
-  const int ex = extra ? std::max(0, std::min(64, std::atoi(extra))) : 0;
-  const uint64_t per = (uint64_t)(ncu + ex) * kPhSteps * gpb;
+  if (a.ncu == 0) return false;
+  const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
+  const uint64_t per = (uint64_t)wg * kPhSteps * gpb;
   const uint64_t np = (a.n_groups + per - 1) / per;
   if (np < kPhMinPhases || np > 0xFFFFFFFFull) return false;
-  *grid = (uint32_t)(ncu + ex);
+  *grid = wg;
   *nphase = (uint32_t)np;
   return true;
 }
 
 }  // namespace
+
+bool fixed_uses_phases(const FixedArgs& a, bool nontemporal) {
+  if (!a.phase_sync || !nontemporal || a.L < 16u || a.n_groups == 0) return false;
+  uint32_t grid = 0, nphase = 0;
+  return phase_plan(a, kBlock / ((a.L + 15u) / 16u), &grid, &nphase);
+}
 
 hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   const bool recover = a0.parity != nullptr;

@@ -81,6 +81,14 @@ bool QuicFecSender::CloseFecGroup(QuicPacketNumber fec_packet_number, QuicFecEnc
   return true;
 }
 
+bool QuicFecSender::CloseFecGroup(QuicPacketNumber fec_packet_number,
+                                  std::unique_ptr<QuicFecGroup>* group) {
+  QuicFecEncodeBatch batch;
+  if (!group || !CloseFecGroup(fec_packet_number, &batch)) return false;
+  *group = std::move(batch.entries().back().group);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // QuicFecEncodeBatch
 // ---------------------------------------------------------------------------
@@ -183,6 +191,21 @@ size_t QuicFecReceiver::CollectRevivable(QuicFecReviveBatch* batch, void* tag) {
   return n;
 }
 
+size_t QuicFecReceiver::CollectRevivable(std::vector<std::unique_ptr<QuicFecGroup>>* groups) {
+  size_t n = 0;
+  for (auto it = group_map_.begin(); it != group_map_.end();) {
+    if (it->second->CanRevive()) {
+      MarkClosed(it->first);
+      groups->push_back(std::move(it->second));
+      it = group_map_.erase(it);
+      ++n;
+    } else {
+      ++it;
+    }
+  }
+  return n;
+}
+
 const QuicFecGroup* QuicFecReceiver::GetGroup(QuicFecGroupNumber n) const {
   auto it = group_map_.find(n);
   return it == group_map_.end() ? nullptr : it->second.get();
@@ -212,6 +235,103 @@ int QuicFecReviveBatch::Flush(qfec_ctx* ctx, std::vector<Revived>* revived) {
   flushed_.swap(groups_);
   groups_.clear();
   return QFEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// QuicFecBatcher
+// ---------------------------------------------------------------------------
+QuicFecBatcher::~QuicFecBatcher() {
+  QuicFecGroup::Finish(&enc_pending_, true);
+  QuicFecGroup::Finish(&rev_pending_, true);
+}
+
+void QuicFecBatcher::AddClosedGroup(Visitor* v, const QuicPacketHeader& fec_header,
+                                    std::unique_ptr<QuicFecGroup> group) {
+  enc_.push_back(EncodeItem{v, fec_header, std::move(group)});
+}
+
+void QuicFecBatcher::AddRevivable(Visitor* v, std::unique_ptr<QuicFecGroup> group) {
+  rev_.push_back(ReviveItem{v, std::move(group)});
+}
+
+void QuicFecBatcher::Forget(Visitor* v) {
+  enc_.erase(std::remove_if(enc_.begin(), enc_.end(),
+                            [v](const EncodeItem& e) { return e.v == v; }),
+             enc_.end());
+  rev_.erase(std::remove_if(rev_.begin(), rev_.end(),
+                            [v](const ReviveItem& e) { return e.v == v; }),
+             rev_.end());
+  for (EncodeItem& e : enc_live_)  // launched: the groups stay until completion
+    if (e.v == v) e.v = nullptr;
+  for (ReviveItem& e : rev_live_)
+    if (e.v == v) e.v = nullptr;
+}
+
+int QuicFecBatcher::Launch() {
+  int rc = QFEC_OK;
+  if (InFlight()) rc = Complete(true);
+  if (enc_.empty() && rev_.empty()) return rc;
+  enc_live_.swap(enc_);
+  rev_live_.swap(rev_);
+  std::vector<QuicFecGroup*> gs;
+  gs.reserve(std::max(enc_live_.size(), rev_live_.size()));
+  for (EncodeItem& e : enc_live_) gs.push_back(e.group.get());
+  const int erc = QuicFecGroup::Launch(ctx_, gs, &enc_pending_, /*async=*/true);
+  gs.clear();
+  for (ReviveItem& e : rev_live_) gs.push_back(e.group.get());
+  const int rrc = QuicFecGroup::Launch(ctx_, gs, &rev_pending_, /*async=*/true);
+  ++stats_.launches;
+  return erc ? erc : rrc;
+}
+
+int QuicFecBatcher::Complete(bool wait) {
+  if (!InFlight()) return QFEC_OK;
+  // one qfec_complete finishes both launches (same context)
+  const int erc = QuicFecGroup::Finish(&enc_pending_, wait);
+  if (erc == QFEC_PENDING) return QFEC_PENDING;
+  const int rrc = QuicFecGroup::Finish(&rev_pending_, wait);
+  if (rrc == QFEC_PENDING) return QFEC_PENDING;  // enc_pending_ keeps its result
+  // callbacks may add new work (an emitted FEC packet lets the next packets
+  // out, which may close the next group): hand over local copies
+  std::vector<EncodeItem> enc;
+  std::vector<ReviveItem> rev;
+  enc.swap(enc_live_);
+  rev.swap(rev_live_);
+  for (EncodeItem& e : enc) {
+    if (!e.v) continue;
+    StringPiece red;
+    const bool ok = erc == QFEC_OK;
+    if (ok) red = e.group->PayloadParity();
+    ok ? ++stats_.groups_encoded : ++stats_.groups_failed;
+    e.v->OnFecRedundancy(e.header, red, ok);
+  }
+  // revived packets, grouped per visitor in the order added
+  std::vector<QuicFecReviveBatch::Revived> out;
+  for (size_t i = 0; i < rev.size();) {
+    Visitor* v = rev[i].v;
+    size_t j = i;
+    out.clear();
+    for (; j < rev.size() && rev[j].v == v; ++j) {
+      if (rrc != QFEC_OK) {
+        ++stats_.groups_failed;
+        continue;
+      }
+      QuicFecReviveBatch::Revived r;
+      r.tag = v;
+      if (rev[j].group->ReviveInPlace(&r.header, &r.payload) == 0) continue;
+      out.push_back(r);
+      ++stats_.groups_revived;
+    }
+    if (v && !out.empty()) v->OnRevivedPackets(out);
+    i = j;
+  }
+  return erc ? erc : rrc;
+}
+
+int QuicFecBatcher::Flush() {
+  const int lrc = Launch();
+  const int crc = Complete(true);
+  return lrc ? lrc : crc;
 }
 
 }  // namespace net

@@ -89,6 +89,9 @@ class QuicFecSender {
   // come from the batch's Flush.  `tag` identifies the connection there.
   bool CloseFecGroup(QuicPacketNumber fec_packet_number, QuicFecEncodeBatch* batch,
                      void* tag = nullptr);
+  // The same, handing the closed group to the caller (e.g. for a
+  // QuicFecBatcher): its redundancy is group->PayloadParity() once computed.
+  bool CloseFecGroup(QuicPacketNumber fec_packet_number, std::unique_ptr<QuicFecGroup>* group);
 
   const std::string& detailed_error() const { return detailed_error_; }
 
@@ -153,6 +156,8 @@ class QuicFecReceiver {
   // Move every group that can revive now into `batch` (they leave the map;
   // later packets of a revived group are ignored as finished).
   size_t CollectRevivable(QuicFecReviveBatch* batch, void* tag = nullptr);
+  // The same, appending the groups to `groups` (e.g. for a QuicFecBatcher).
+  size_t CollectRevivable(std::vector<std::unique_ptr<QuicFecGroup>>* groups);
 
   size_t NumGroups() const { return group_map_.size(); }
   const QuicFecGroup* GetGroup(QuicFecGroupNumber n) const;
@@ -195,6 +200,83 @@ class QuicFecReviveBatch {
  private:
   std::vector<std::pair<void*, std::unique_ptr<QuicFecGroup>>> groups_;
   std::vector<std::pair<void*, std::unique_ptr<QuicFecGroup>>> flushed_;
+};
+
+// ---------------------------------------------------------------------------
+// Event-loop batching across connections (embedder-owned, one per thread).
+// ---------------------------------------------------------------------------
+// The connections of one event loop hand it their closed send-side groups
+// (with the FEC packet's header, whose number they reserved) and their
+// revivable receive-side groups; once per loop turn the embedder calls
+// Launch() — ONE encode and ONE revive ragged launch for everything collected,
+// queued asynchronously (QFEC_ASYNC: the payloads are read in place from the
+// mapped arena) — goes on serving sockets, and calls Complete() (next turn,
+// or when it polls done), which hands every result to its connection:
+// OnFecRedundancy emits the FEC packet, OnRevivedPackets re-injects the
+// revived packets.  A failed launch is reported per group (ok == false): the
+// group then goes without FEC and loss recovery retransmits as without FEC.
+class QuicFecBatcher {
+ public:
+  class Visitor {  // a connection
+   public:
+    virtual ~Visitor() {}
+    // The redundancy of a group handed over with AddClosedGroup (a view valid
+    // during the call), or ok == false and an empty view.
+    virtual void OnFecRedundancy(const QuicPacketHeader& fec_header, StringPiece redundancy,
+                                 bool ok) = 0;
+    // The packets revived from this visitor's groups, in the order added
+    // (payload views valid during the call).
+    virtual void OnRevivedPackets(const std::vector<QuicFecReviveBatch::Revived>& revived) = 0;
+  };
+
+  struct Stats {
+    uint64_t launches = 0;         // Launch() calls that queued GPU work
+    uint64_t groups_encoded = 0;   // FEC redundancies delivered
+    uint64_t groups_revived = 0;   // revived packets delivered
+    uint64_t groups_failed = 0;    // groups whose GPU work failed
+  };
+
+  explicit QuicFecBatcher(qfec_ctx* ctx = nullptr) : ctx_(ctx) {}
+  // Waits for launched work; delivers nothing.
+  ~QuicFecBatcher();
+  QuicFecBatcher(const QuicFecBatcher&) = delete;
+  QuicFecBatcher& operator=(const QuicFecBatcher&) = delete;
+
+  void AddClosedGroup(Visitor* v, const QuicPacketHeader& fec_header,
+                      std::unique_ptr<QuicFecGroup> group);
+  void AddRevivable(Visitor* v, std::unique_ptr<QuicFecGroup> group);
+  // A visitor going away: its queued groups are dropped and its launched
+  // ones complete without a callback.
+  void Forget(Visitor* v);
+
+  size_t NumQueued() const { return enc_.size() + rev_.size(); }
+  bool InFlight() const { return !enc_live_.empty() || !rev_live_.empty(); }
+  // Queue the collected work as one encode + one revive launch (completing a
+  // previous launch first).  Returns a qfec_* code (a failure is also
+  // delivered per group by the next Complete).
+  int Launch();
+  // Deliver the launched work to the visitors: wait blocks; otherwise
+  // QFEC_PENDING while the GPU is still on it.
+  int Complete(bool wait);
+  // Launch + Complete(true).
+  int Flush();
+  const Stats& stats() const { return stats_; }
+
+ private:
+  struct EncodeItem {
+    Visitor* v;
+    QuicPacketHeader header;
+    std::unique_ptr<QuicFecGroup> group;
+  };
+  struct ReviveItem {
+    Visitor* v;
+    std::unique_ptr<QuicFecGroup> group;
+  };
+  qfec_ctx* ctx_;
+  std::vector<EncodeItem> enc_, enc_live_;
+  std::vector<ReviveItem> rev_, rev_live_;
+  QuicFecGroup::Pending enc_pending_, rev_pending_;
+  Stats stats_;
 };
 
 }  // namespace net

@@ -283,14 +283,23 @@ size_t QuicFecGroup::Revive(QuicPacketHeader* header, char* decrypted_payload, s
 }
 
 int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups) {
+  Pending p;
+  Launch(ctx, groups, &p, /*async=*/false);
+  return Finish(&p, /*wait=*/true);
+}
+
+int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* pend,
+                         bool async) {
+  *pend = Pending();
   std::vector<QuicFecGroup*> work;
   for (QuicFecGroup* g : groups)
     if (g && g->dirty_) work.push_back(g);
   if (work.empty()) return QFEC_OK;
   if (!ctx) ctx = thread_default_ctx();
+  pend->ctx = ctx;
   if (!ctx) {
     for (QuicFecGroup* g : work) g->detailed_error_ = qfec_last_error(nullptr);
-    return QFEC_ERR_INTERNAL;
+    return pend->rc = QFEC_ERR_INTERNAL;
   }
   // Ragged CSR over every folded payload of every group, addressed IN PLACE:
   // the C-ABI takes one base pointer plus 64-bit offsets, so the base is the
@@ -300,7 +309,7 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   // (QFEC_PTR_MAPPED); otherwise the host path gathers them into the
   // context's pinned staging (QFEC_PTR_HOST).
   size_t npk = 0;
-  std::vector<QuicFecGroup*> launched;
+  std::vector<QuicFecGroup*>& launched = pend->launched;
   launched.reserve(work.size());
   uintptr_t in_base = UINTPTR_MAX, out_base = UINTPTR_MAX;
   bool mapped = true;
@@ -314,7 +323,8 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
       g->parity_ = ArenaAlloc(kMaxPacketSize);
       if (!g->parity_.p) {
         g->detailed_error_ = "out of payload memory";
-        return QFEC_ERR_INTERNAL;
+        launched.clear();
+        return pend->rc = QFEC_ERR_INTERNAL;
       }
     }
     mapped = mapped && static_cast<ArenaSlab*>(g->parity_.slab)->mapped;
@@ -328,8 +338,9 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   }
   if (launched.empty()) return QFEC_OK;
   // index tables: per-thread buffers that keep their capacity between flushes
+  // (the call stages them, so they are free again when it returns)
   static thread_local std::vector<uint64_t> pkt_off, parity_off;
-  static thread_local std::vector<uint16_t> pkt_len, plen;
+  static thread_local std::vector<uint16_t> pkt_len;
   static thread_local std::vector<uint32_t> grp_ptr;
   pkt_off.clear();
   pkt_off.reserve(npk);
@@ -347,21 +358,35 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
     grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));
     parity_off.push_back(reinterpret_cast<uintptr_t>(g->parity_.p) - out_base);
   }
-  plen.assign(launched.size(), 0);
-  int rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
-                              pkt_len.data(), grp_ptr.data(), launched.size(),
-                              reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
-                              plen.data(), mapped ? QFEC_PTR_MAPPED : QFEC_PTR_HOST);
-  if (rc != QFEC_OK) {
-    for (QuicFecGroup* g : launched) g->detailed_error_ = qfec_last_error(ctx);
-    return rc;
+  pend->plen.assign(launched.size(), 0);
+  const uint32_t flags = mapped ? (QFEC_PTR_MAPPED | (async ? QFEC_ASYNC : 0u)) : QFEC_PTR_HOST;
+  pend->rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
+                                pkt_len.data(), grp_ptr.data(), launched.size(),
+                                reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
+                                pend->plen.data(), flags);
+  pend->live = pend->rc == QFEC_OK && (flags & QFEC_ASYNC);
+  return pend->rc;
+}
+
+int QuicFecGroup::Finish(Pending* pend, bool wait) {
+  if (pend->live) {
+    const int rc = qfec_complete(pend->ctx, wait ? 1 : 0);
+    if (rc == QFEC_PENDING) return QFEC_PENDING;
+    pend->rc = rc;
+    pend->live = false;
   }
-  for (size_t i = 0; i < launched.size(); ++i) {
-    QuicFecGroup* g = launched[i];
-    g->payload_parity_len_ = plen[i];
-    g->dirty_ = false;
+  if (pend->rc != QFEC_OK) {
+    const char* why = qfec_last_error(pend->ctx);
+    for (QuicFecGroup* g : pend->launched) g->detailed_error_ = why;
+  } else {
+    for (size_t i = 0; i < pend->launched.size(); ++i) {
+      QuicFecGroup* g = pend->launched[i];
+      g->payload_parity_len_ = pend->plen[i];
+      g->dirty_ = false;
+    }
   }
-  return QFEC_OK;
+  pend->launched.clear();
+  return pend->rc;
 }
 
 }  // namespace net

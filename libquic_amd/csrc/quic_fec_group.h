@@ -139,6 +139,24 @@ class QuicFecGroup {
   // code; afterwards PayloadParity()/Revive() of every group are free.
   static int ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups);
 
+  // ComputeAll in two halves, for an event loop that overlaps the GPU work
+  // with its other work: Launch queues the ONE ragged launch (QFEC_ASYNC when
+  // every payload sits in mapped arena memory, else it completes at once) and
+  // Finish completes it (qfec_complete) and sets every group's parity.  The
+  // groups must stay alive and take no packets in between.
+  struct Pending {
+    qfec_ctx* ctx = nullptr;
+    std::vector<QuicFecGroup*> launched;
+    std::vector<uint16_t> plen;  // parity_len_out, filled at completion
+    int rc = QFEC_OK;            // a synchronous failure at launch
+    bool live = false;
+  };
+  static int Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* p,
+                    bool async);
+  // wait: block; otherwise QFEC_PENDING while the work runs.  Returns the
+  // launch's qfec_* code (also in every launched group's detailed_error).
+  static int Finish(Pending* p, bool wait);
+
   // Detailed reason of the last failure (QuicFramer::detailed_error style).
   const std::string& detailed_error() const { return detailed_error_; }
 

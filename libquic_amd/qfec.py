@@ -26,6 +26,8 @@ QFEC_PTR_HOST = 1
 QFEC_CACHED = 2
 QFEC_PTR_MAPPED = 4
 QFEC_ONE_PASS = 8
+QFEC_ASYNC = 16
+QFEC_PENDING = 1
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
 MAX_GROUP_PACKETS = 255
@@ -89,6 +91,10 @@ SIGNATURES = [
       C.c_uint32]),
     ("qfec_stream_probe", C.c_int, [_vp, _u8p, C.c_uint64, _u8p, C.c_int]),
     ("qfec_phase_abandons", C.c_int, [_vp, _vp]),
+    ("qfec_phase_backoff", C.c_int, [_vp]),
+    ("qfec_debug_phase", C.c_int, [_vp, C.c_uint32, C.c_int]),
+    ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
+    ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -284,20 +290,21 @@ class Context:
 
     # -- ragged ------------------------------------------------------------
     def encode_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity_out, parity_off,
-                      parity_len_out, *, host=False, mapped=False):
+                      parity_len_out, *, host=False, mapped=False, async_=False):
         rc = self.lib.qfec_encode_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                          _ptr(grp_ptr), n_groups, _ptr(parity_out),
                                          _ptr(parity_off), _ptr(parity_len_out),
-                                         _fl(host, mapped))
+                                         _fl(host, mapped) | (QFEC_ASYNC if async_ else 0))
         return self._check(rc)
 
     def recover_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity, parity_off,
-                       parity_len, missing, out, out_off, *, host=False, mapped=False):
+                       parity_len, missing, out, out_off, *, host=False, mapped=False,
+                       async_=False):
         rc = self.lib.qfec_recover_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                           _ptr(grp_ptr), n_groups, _ptr(parity),
                                           _ptr(parity_off), _ptr(parity_len), _ptr(missing),
                                           _ptr(out), _ptr(out_off),
-                                          _fl(host, mapped))
+                                          _fl(host, mapped) | (QFEC_ASYNC if async_ else 0))
         return self._check(rc)
 
     def xor_into(self, src, n, dst, *, host=False, mapped=False):
@@ -363,6 +370,20 @@ class Context:
                                                       1 if copy else 0))
 
     # -- synthetic inputs ----------------------------------------------------
+    def phase_backoff(self):
+        """Large fixed batches left on the one-pass kernel (contention backoff)."""
+        return self.lib.qfec_phase_backoff(self.ctx)
+
+    def debug_phase(self, extra, reset_backoff=True):
+        """Test hook: extra workgroups in phased launches (forces the abandon
+        path); reset_backoff clears the contention backoff."""
+        return self._check(self.lib.qfec_debug_phase(self.ctx, extra, int(reset_backoff)))
+
+    def complete(self, wait=True):
+        """Finish QFEC_ASYNC calls: 0 done, QFEC_PENDING (1) still running."""
+        rc = self.lib.qfec_complete(self.ctx, 1 if wait else 0)
+        return rc if rc == 1 else self._check(rc)
+
     def phase_abandons(self):
         """Phased fixed-shape launches that gave up their grid-wide meetings."""
         n = C.c_uint32(0)

@@ -179,3 +179,50 @@ def sent_entropy_run(entropy, first_pn, largest, claimed, range_ptr, lo, hi):
     lib().ref_sent_entropy_run(_pa(e), n, first_pn, _pa(cum), largest.size, _pa(largest),
                                _pa(claimed), _pa(range_ptr), _pa(lo), _pa(hi), _pa(ok))
     return cum[:n - first_pn + 1], ok[:largest.size]
+
+
+# ---- oracle/_ref/libref_aead_asm.so: the reference's encrypter classes over
+# BoringSSL WITH its x86-64 assembly (oracle/ref/Makefile, ref_aead_shim.cc):
+# the CPU speed the GPU protection kernels are compared with in bench.py.
+ASM_SO = os.path.join(_HERE, "_ref", "libref_aead_asm.so")
+_asm = None
+
+
+def asm_available() -> bool:
+    return os.path.exists(ASM_SO)
+
+
+def asm_lib():
+    global _asm
+    if _asm is None:
+        L = C.CDLL(ASM_SO)
+        L.ref_aead_asm_seal_batch.restype = C.c_uint64
+        L.ref_aead_asm_seal_batch.argtypes = [C.c_int] + [C.c_void_p] * 9 + \
+            [C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.ref_aead_asm_ia32cap.restype = None
+        L.ref_aead_asm_ia32cap.argtypes = [C.c_void_p]
+        _asm = L
+    return _asm
+
+
+def asm_cpu_features() -> dict:
+    """What BoringSSL detected (OPENSSL_ia32cap_P) and so which code it runs."""
+    cap = (C.c_uint32 * 4)()
+    asm_lib().ref_aead_asm_ia32cap(cap)
+    return {"aesni": bool(cap[1] >> 25 & 1), "pclmulqdq": bool(cap[1] >> 1 & 1),
+            "avx": bool(cap[1] >> 28 & 1), "avx2": bool(cap[2] >> 5 & 1),
+            "ssse3": bool(cap[1] >> 9 & 1)}
+
+
+def asm_seal_batch(aead, keys, prefixes, key_idx, packet_number, data, ad_off, ad_len, pt_off,
+                   pt_len, out_off, out_size, threads=1, out=None):
+    """Aes128Gcm12Encrypter (aead "aes128gcm") / ChaCha20Poly1305Encrypter
+    ("chacha20poly1305") ::EncryptPacket per packet, BoringSSL assembly."""
+    out = np.zeros(out_size, np.uint8) if out is None else out
+    bad = asm_lib().ref_aead_asm_seal_batch(
+        0 if aead == "aes128gcm" else 1, _pa(keys), _pa(prefixes), _pa(key_idx),
+        _pa(packet_number), _pa(data), _pa(ad_off), _pa(ad_len), _pa(pt_off), _pa(pt_len),
+        pt_len.size, _pa(out), _pa(out_off), threads)
+    if bad:
+        raise RuntimeError(f"reference EncryptPacket failed for {bad} packets")
+    return out

@@ -15,6 +15,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -98,3 +99,42 @@ def test_shard_ranges_disjoint_for_8_ranks():
     a = bench.drop_indices(3 * 1000, 1000, 10)
     b = bench.drop_indices(0, 4000, 10)[3000:]
     assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_bench_cli_two_ranks_on_one_gpu():
+    """the N>1 bench path on the GPU.  `python
+    bench.py --gpus 2` starts two ranks that both use cuda:0
+    (QFEC_BENCH_SHARE_DEVICE, test only) with the control plane over gloo; each
+    runs the HIP kernels on its own shard (65,536 groups: below the phased
+    threshold, so the two ranks do not compete for whole-CU residency).  The
+    line says n_gpus 2, both ranks verified, and each shard's parity / revived
+    digests equal the oracle's over its group range."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    G = 1 << 16
+    p = _bench_cli(["--gpus", "2", "--groups", str(G), "--steps", "3", "--warmup", "1",
+                    "--one-pass", "--digests", "--no-cpu-baseline"],
+                   env_extra={"QFEC_BENCH_SHARE_DEVICE": "1"}, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified"] is True
+    assert line["control_plane"].startswith("gloo")
+    import hashlib
+    from oracle import oracle_c as OC
+    import bench
+    k, L = 10, 1350
+    shards = sorted(line["shards"], key=lambda s: s["rank"])
+    assert [s["g0"] for s in shards] == [0, G]
+    assert all(s["verified"] and s["device"] == 0 for s in shards)
+    for s in shards:
+        rows = OC.synth_fixed(bench.SEED_FIXED, s["g0"], G, k, L)
+        rc, par = OC.encode_fixed(rows, k, L, G)
+        miss = bench.drop_indices(s["g0"], G, k)
+        rc2, out = OC.recover_fixed(rows, par, miss, k, L, G)
+        assert rc == 0 and rc2 == 0
+        assert s["digests"][0] == hashlib.sha256(par.tobytes()).hexdigest()[:32]
+        assert s["digests"][1] == hashlib.sha256(out.tobytes()).hexdigest()[:32]

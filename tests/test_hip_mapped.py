@@ -241,3 +241,71 @@ def test_registered_host_memory(ctx):
     # unregistered pageable memory is refused again
     with pytest.raises(qfec.QfecError, match="QFEC_PTR_MAPPED"):
         ctx.encode(rows, k, L, n, par, mapped=True)
+
+
+@pytest.mark.parametrize("n", [3, 256, 2000])
+def test_ragged_mapped_async(ctx, n):
+    """QFEC_ASYNC (the event-loop form): an encode and a recover are queued on
+    one context without waiting (n <= 256: the flag-completed latency path;
+    2000: the staged-table path), polled with qfec_complete(wait=0), then
+    completed; the outputs — bytes and the encode lengths, which arrive only
+    at completion — equal the oracle's, and equal a synchronous call's."""
+    z, want_l = _mapped_case(n, g0=4000 + n, kmin=2, kmax=40, lmin=1, lmax=1452)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(n * 1452)
+    par.array[:] = 0xA5
+    par_in = qfec.HostBuffer(n * 1452)
+    par_in.array[:] = z["parity"]
+    out = qfec.HostBuffer(n * 1452)
+    out.array[:] = 0x5A
+    plen = np.zeros(n, dtype=np.uint16)
+    try:
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        ctx.recover_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n,
+                           par_in.array, z["parity_off"], want_l, z["missing"], out.array,
+                           z["out_off"], mapped=True, async_=True)
+        polls = 0
+        while ctx.complete(wait=False) == qfec.QFEC_PENDING:
+            polls += 1
+            assert polls < 10_000_000
+        assert ctx.complete(wait=True) == 0  # nothing left: returns at once
+        assert np.array_equal(plen, want_l)
+        for g in range(n):
+            o, m = int(z["parity_off"][g]), int(want_l[g])
+            assert np.array_equal(par.array[o:o + m], z["parity"][o:o + m]), g
+            assert np.array_equal(out.array[o:o + m], z["recovered"][o:o + m]), g
+        # a synchronous call after async ones completes them first; same bytes
+        plen2 = np.zeros(n, dtype=np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, out.array,
+                          z["parity_off"], plen2, mapped=True)
+        assert np.array_equal(plen, want_l) and np.array_equal(plen2, want_l)
+    finally:
+        for b in (data, par, par_in, out):
+            b.close()
+
+
+def test_ragged_mapped_async_error_at_completion(ctx):
+    """An invalid batch refused by the host-side checks fails at the call
+    (nothing queued); a valid async call after it completes normally."""
+    z, want_l = _mapped_case(4, g0=9000, kmin=2, kmax=5, lmin=20, lmax=100)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(4 * 1452)
+    plen = np.zeros(4, dtype=np.uint16)
+    bad_len = z["pkt_len"].copy()
+    bad_len[0] = 1453
+    try:
+        with pytest.raises(qfec.InvalidFecData):
+            ctx.encode_ragged(data.array, z["pkt_off"], bad_len, z["grp_ptr"], 4, par.array,
+                              z["parity_off"], plen, mapped=True, async_=True)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 4, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        assert ctx.complete(wait=True) == 0
+        assert np.array_equal(plen, want_l)
+    finally:
+        data.close()
+        par.close()

@@ -195,7 +195,9 @@ def test_phased_concurrent_launches(ctx):
         for o in outs:
             assert torch.equal(o, want)
         print(f"abandoned launches: {ctx.phase_abandons() - a0} + {ctx2.phase_abandons() - b0}")
-        # alone again: meets normally
+        # alone again: meets normally (the backoff a contended launch may
+        # have engaged is cleared first)
+        ctx.debug_phase(0, reset_backoff=True)
         a1 = ctx.phase_abandons()
         ctx.encode(rows, k, L, n, outs[0])
         ctx.sync()
@@ -205,31 +207,91 @@ def test_phased_concurrent_launches(ctx):
     finally:
         ctx.set_stream(torch.cuda.current_stream())
         ctx2.close()
+        ctx.debug_phase(0, reset_backoff=True)  # contention over: phased again
 
 
-def test_phased_abandon_path(ctx, monkeypatch):
-    """More workgroups than CUs (test hook): the extra one is not resident
-    until another exits, so the first meeting times out, the launch raises its
-    abandon flag and runs to the end without meetings — same bytes as the
-    one-pass kernel, counted once by qfec_phase_abandons; the next launch
-    (sync words reset by the last workgroup out) meets normally."""
+def test_phased_abandon_path_and_backoff(ctx):
+    """More workgroups than CUs (test hook qfec_debug_phase): the extra one is
+    not resident until another exits, so the first meeting times out, the
+    launch raises its abandon flag and runs to the end without meetings — same
+    bytes as the one-pass kernel, counted by qfec_phase_abandons.  The next
+    large batch without the hook sees the grown count (copied to host-mapped
+    memory by the last workgroup out, read without a synchronisation) and runs
+    one-pass: the contention backoff (16 batches).  Cleared, the phased kernel
+    meets normally again.  Also times an abandoned launch against the one-pass
+    kernel."""
     k, L, n = 10, 1350, 1 << 19
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
     ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
     want = torch.empty(n * L, dtype=torch.uint8, device=DEV)
     ctx.encode(rows, k, L, n, want, one_pass=True)
     out = torch.zeros(n * L, dtype=torch.uint8, device=DEV)
+    ctx.debug_phase(0, reset_backoff=True)
     a0 = ctx.phase_abandons()
-    monkeypatch.setenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS", "1")
-    ctx.encode(rows, k, L, n, out)
-    ctx.sync()
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    try:
+        ctx.debug_phase(1, reset_backoff=False)
+        ctx.encode(rows, k, L, n, out)  # warm
+        ev[0].record(s)
+        ctx.encode(rows, k, L, n, out)
+        ev[1].record(s)
+        ctx.sync()
+        torch.cuda.synchronize()
+        assert ctx.phase_abandons() == a0 + 2
+        assert torch.equal(out, want)
+    finally:
+        ctx.debug_phase(0, reset_backoff=False)
+    ev[2].record(s)
+    ctx.encode(rows, k, L, n, out, one_pass=True)
+    ev[3].record(s)
     torch.cuda.synchronize()
-    assert ctx.phase_abandons() == a0 + 1
-    assert torch.equal(out, want)
-    monkeypatch.delenv("QFEC_DEBUG_PHASE_EXTRA_WORKGROUPS")
+    t_ab, t_one = ev[0].elapsed_time(ev[1]), ev[2].elapsed_time(ev[3])
+    print(f"abandoned phased launch {t_ab:.3f} ms vs one-pass {t_one:.3f} ms "
+          f"(one-pass / abandoned = {t_one / t_ab:.2f})")
+    # the backoff engages at the next large batch: one-pass, no new abandon
     out.zero_()
     ctx.encode(rows, k, L, n, out)
     ctx.sync()
     torch.cuda.synchronize()
-    assert ctx.phase_abandons() == a0 + 1
+    assert ctx.phase_backoff() == 15
+    assert ctx.phase_abandons() == a0 + 2
     assert torch.equal(out, want)
+    # cleared: phased again, meeting normally
+    ctx.debug_phase(0, reset_backoff=True)
+    out.zero_()
+    ctx.encode(rows, k, L, n, out)
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert ctx.phase_backoff() == 0
+    assert ctx.phase_abandons() == a0 + 2
+    assert torch.equal(out, want)
+
+
+def test_phased_one_context_two_streams(ctx):
+    """phased launches of ONE context on two streams share its sync
+    words; the context orders them (a phased launch on another stream waits
+    for the previous one's event), so no launch is abandoned by the other's
+    counters and every output equals the one-pass kernel's."""
+    k, L, n = 10, 1350, 1 << 19
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    want = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    ctx.encode(rows, k, L, n, want, one_pass=True)
+    ctx.debug_phase(0, reset_backoff=True)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros(n * L, dtype=torch.uint8, device=DEV) for _ in range(6)]
+    torch.cuda.synchronize()
+    a0 = ctx.phase_abandons()
+    try:
+        for i, o in enumerate(outs):
+            ctx.set_stream(s1 if i % 2 == 0 else s2)
+            ctx.encode(rows, k, L, n, o)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_stream(torch.cuda.current_stream())
+    for o in outs:
+        assert torch.equal(o, want)
+    assert ctx.phase_abandons() == a0
+    assert ctx.phase_backoff() == 0

@@ -42,7 +42,8 @@ def test_patch_names_only_the_hook_files():
     assert sorted(files) == sorted(core + f for f in (
         "quic_protocol.h", "quic_protocol.cc", "quic_framer.h", "quic_framer.cc",
         "quic_packet_creator.h", "quic_packet_creator.cc", "quic_packet_generator.h",
-        "quic_connection.h", "quic_connection.cc"))
+        "quic_connection.h", "quic_connection.cc", "quic_connection_stats.h",
+        "quic_connection_stats.cc"))
 
 
 def test_patch_applies_and_every_unit_compiles():

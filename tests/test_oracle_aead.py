@@ -167,3 +167,39 @@ def test_quic_gcm_batch_vs_reference(ref):
     b = OC.quic_aes128gcm_encrypt_batch(keys, pre, kidx, pn, None, data, ad_off, A, pt_off, L,
                                         out_off, tot)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("aead", ["aes128gcm", "chacha20poly1305"])
+def test_reference_asm_encrypters_match_oracle(aead):
+    """The CPU baseline's library (oracle/_ref/libref_aead_asm.so: the
+    reference's Aes128Gcm12Encrypter / ChaCha20Poly1305Encrypter over
+    BoringSSL built WITH its x86-64 assembly) seals exactly what the oracle
+    does — so the baseline times the same work — on multi-key batches of
+    0..1452-byte payloads, on 1 and 4 threads."""
+    if not R.asm_available():
+        if not R.build() or not R.asm_available():
+            pytest.skip("reference build oracle/_ref absent (no /root/reference here)")
+    feats = R.asm_cpu_features()
+    print(feats)
+    rng = np.random.default_rng(11)
+    n = 300
+    ad_len = rng.integers(0, 40, n).astype(np.uint16)
+    pt_len = rng.integers(0, 1453, n).astype(np.uint16)
+    rec = ad_len.astype(np.uint64) + pt_len.astype(np.uint64)
+    ad_off = np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.uint64)
+    pt_off = ad_off + ad_len.astype(np.uint64)
+    data = rng.integers(0, 256, int(rec.sum()), dtype=np.uint8)
+    out_len = pt_len.astype(np.uint64) + np.uint64(12)
+    out_off = np.concatenate([[0], np.cumsum(out_len)[:-1]]).astype(np.uint64)
+    kl = 16 if aead == "aes128gcm" else 32
+    keys = rng.integers(0, 256, 5 * kl, dtype=np.uint8)
+    pre = rng.integers(0, 256, 5 * 4, dtype=np.uint8)
+    kidx = rng.integers(0, 5, n).astype(np.uint32)
+    pn = rng.integers(1, 1 << 40, n).astype(np.uint64)
+    size = int(out_len.sum())
+    seal = OC.quic_aes128gcm_encrypt_batch if aead == "aes128gcm" else OC.quic_c20p1305_encrypt_batch
+    want = seal(keys, pre, kidx, pn, None, data, ad_off, ad_len, pt_off, pt_len, out_off, size)
+    for th in (1, 4):
+        got = R.asm_seal_batch(aead, keys, pre, kidx, pn, data, ad_off, ad_len, pt_off, pt_len,
+                               out_off, size, threads=th)
+        assert np.array_equal(got, want), th

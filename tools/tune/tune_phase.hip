@@ -280,6 +280,7 @@ int main(int argc, char** argv) {
     a.L = kL;
     a.err = d_err;
     a.phase_sync = psync;
+    a.ncu = (uint32_t)ncu;
     CK(qfec::launch_fixed(a, true, 0));
   };
   // the product's phase_xor_kernel instantiated directly: MEET2 x FLAT
@@ -316,6 +317,7 @@ int main(int argc, char** argv) {
     a.L = kL;
     a.err = d_err;
     a.phase_sync = psync;
+    a.ncu = (uint32_t)ncu;
     if (pks[w].first.find("recover") != std::string::npos) {
       a.parity = par[(j + 1) % NP];
       a.missing = d_miss;
