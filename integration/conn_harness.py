@@ -25,7 +25,8 @@ _U64 = ("data_packets_sent fec_packets_sent dropped revived groups_one_loss fec_
 
 class Result(C.Structure):
     _fields_ = ([(n, C.c_uint64) for n in _U64] +
-                [("fec_wall_us", C.c_double), ("cpu_xor_us", C.c_double),
+                [("fec_wall_us", C.c_double), ("fec_host_us", C.c_double),
+                 ("cpu_xor_us", C.c_double),
                  ("cpu_xor_groups", C.c_uint64), ("streams_ok", C.c_int32),
                  ("connected", C.c_int32), ("status", C.c_int32), ("detail", C.c_char * 256)])
 

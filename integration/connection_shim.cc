@@ -87,7 +87,8 @@ struct fec_conn_result {
   uint64_t launches;            // batcher launches (0 unbatched)
   uint64_t groups_encoded;      // batcher deliveries
   uint64_t groups_revived;
-  double fec_wall_us;           // wall time inside the batcher's Launch + Complete
+  double fec_wall_us;           // wall time inside the batcher's Launch + Complete (with callbacks)
+  double fec_host_us;           // of which the FEC work itself (batcher launch_us + complete_us)
   double cpu_xor_us;            // the historical per-packet XOR of the same packets, one core
   uint64_t cpu_xor_groups;      // groups XORed by it
   int32_t streams_ok;           // connections whose stream arrived complete and identical
@@ -384,9 +385,9 @@ WriteResult SimWriter::WritePacket(const char* buffer, size_t buf_len, const IPA
         ++run_->r->data_packets_sent;
         // the historical sender: XorBuffers of this packet's protected
         // plaintext into the group's accumulator, on the connection thread
-        const double t0 = now_us();
         std::vector<uint64_t>& acc = xor_acc[h.fec_group];
-        if (acc.empty()) acc.assign(kMaxPacketSize / 8 + 1, 0);
+        if (acc.empty()) acc.assign(kMaxPacketSize / 8 + 1, 0);  // the group's accumulator
+        const double t0 = now_us();
         const size_t nw = payload_.size() / 8;
         const uint64_t* w = reinterpret_cast<const uint64_t*>(payload_.data());
         uint64_t* a = acc.data();
@@ -544,6 +545,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     r->launches = batcher->stats().launches;
     r->groups_encoded = batcher->stats().groups_encoded;
     r->groups_revived = batcher->stats().groups_revived;
+    r->fec_host_us = batcher->stats().launch_us + batcher->stats().complete_us;
   }
   r->turns = turn;
   r->stream_bytes = params->stream_len;

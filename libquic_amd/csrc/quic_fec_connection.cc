@@ -2,6 +2,7 @@
 #include "quic_fec_connection.h"
 
 #include <algorithm>
+#include <chrono>
 
 namespace net {
 
@@ -271,6 +272,7 @@ int QuicFecBatcher::Launch() {
   int rc = QFEC_OK;
   if (InFlight()) rc = Complete(true);
   if (enc_.empty() && rev_.empty()) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
   enc_live_.swap(enc_);
   rev_live_.swap(rev_);
   std::vector<QuicFecGroup*> gs;
@@ -281,16 +283,24 @@ int QuicFecBatcher::Launch() {
   for (ReviveItem& e : rev_live_) gs.push_back(e.group.get());
   const int rrc = QuicFecGroup::Launch(ctx_, gs, &rev_pending_, /*async=*/true);
   ++stats_.launches;
+  stats_.launch_us += std::chrono::duration<double, std::micro>(
+                          std::chrono::steady_clock::now() - t0).count();
   return erc ? erc : rrc;
 }
 
 int QuicFecBatcher::Complete(bool wait) {
   if (!InFlight()) return QFEC_OK;
   // one qfec_complete finishes both launches (same context)
+  const auto t0 = std::chrono::steady_clock::now();
+  auto spent = [&] {
+    stats_.complete_us += std::chrono::duration<double, std::micro>(
+                              std::chrono::steady_clock::now() - t0).count();
+  };
   const int erc = QuicFecGroup::Finish(&enc_pending_, wait);
-  if (erc == QFEC_PENDING) return QFEC_PENDING;
+  if (erc == QFEC_PENDING) return spent(), QFEC_PENDING;
   const int rrc = QuicFecGroup::Finish(&rev_pending_, wait);
-  if (rrc == QFEC_PENDING) return QFEC_PENDING;  // enc_pending_ keeps its result
+  if (rrc == QFEC_PENDING) return spent(), QFEC_PENDING;  // enc_pending_ keeps its result
+  spent();
   // callbacks may add new work (an emitted FEC packet lets the next packets
   // out, which may close the next group): hand over local copies
   std::vector<EncodeItem> enc;

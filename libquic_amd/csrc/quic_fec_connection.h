@@ -234,6 +234,12 @@ class QuicFecBatcher {
     uint64_t groups_encoded = 0;   // FEC redundancies delivered
     uint64_t groups_revived = 0;   // revived packets delivered
     uint64_t groups_failed = 0;    // groups whose GPU work failed
+    // connection-thread time spent on the FEC work itself: building the index
+    // tables and queueing the launches (Launch), and completing them
+    // (Complete: waiting, if the GPU is not done yet, plus the parity
+    // lengths) — not the visitors' callbacks
+    double launch_us = 0;
+    double complete_us = 0;
   };
 
   explicit QuicFecBatcher(qfec_ctx* ctx = nullptr) : ctx_(ctx) {}
