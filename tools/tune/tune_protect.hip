@@ -3,7 +3,6 @@
 // VALU microbenchmark of the FNV-1a-128 byte step.  One process, interleaved.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_protect.hip -o tools/tune/build/tune_protect
 #include "../../libquic_amd/csrc/qpp_kernels.hip"
-#include "prev_protect.inc"
 
 #include <algorithm>
 #include <cstdio>
@@ -258,10 +257,6 @@ int main(int argc, char** argv) {
          hipLaunchKernelGGL(qfec::null_encrypt_staged_kernel<4>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
       {"null encrypt staged SC=8", enc_b, hashed, [&] {
          hipLaunchKernelGGL(qfec::null_encrypt_staged_kernel<8>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
-      {"null encrypt direct (lane loads)", enc_b, hashed, [&] {
-         hipLaunchKernelGGL(qfec::null_encrypt_direct_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
-      {"null decrypt direct (lane loads)", dec_b, hashed, [&] {
-         hipLaunchKernelGGL(qfec::null_decrypt_direct_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
       {"FNV step VALU-only (4 KiB/lane)", 0.0, (double)vgrid * 256 * vb,
        [&] { hipLaunchKernelGGL(fnv_valu_kernel, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
       {"FNV chunk VALU-only R3", 0.0, (double)vgrid * 256 * vb,
