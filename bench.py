@@ -1120,6 +1120,10 @@ def bench_connection_e2e():
         return {"error": f"{h.LIB} not built (built where /root/reference is)"}
     res = {"workload": "reference QuicConnection pairs, v31, groups of 10, ~1 loss per 2 "
                        "groups, NULL encryption, simulated 1 ms turns", "runs": []}
+    # one untimed run first: the process's first launches and the pinned
+    # payload arena's first slabs are not per-group costs
+    h.run(n_pairs=4, group_size=10, drop_every=2, stream_len=50_000, batched=True,
+          require_gpu=True)
     for n, stream in ((1, 400_000), (64, 100_000), (4096, 20_000)):
         t0 = time.perf_counter()
         r = h.run(n_pairs=n, group_size=10, drop_every=2, stream_len=stream, batched=True,
@@ -1133,7 +1137,11 @@ def bench_connection_e2e():
             "groups_encoded": r["groups_encoded"], "groups_revived": r["groups_revived"],
             "dropped": r["dropped"], "retransmitted": r["retransmitted"],
             "groups_per_launch": round(groups / max(1, r["launches"]), 1),
-            "gpu_host_us_per_group": round(r["fec_host_us"] / max(1, groups), 3),
+            # connection-thread work per group: the launch (index tables +
+            # queueing) and the completion, without the time blocked waiting
+            # for the device (a polling loop does other work then)
+            "gpu_host_us_per_group": round((r["fec_host_us"] - r["fec_wait_us"]) / max(1, groups), 3),
+            "gpu_wait_us_per_launch": round(r["fec_wait_us"] / max(1, r["launches"]), 2),
             "cpu_1core_us_per_group": round(r["cpu_xor_us"] / enc, 3),
             "callbacks_incl_us_per_group": round(r["fec_wall_us"] / max(1, groups), 3),
             "run_s": round(wall, 2), "status": r["status"], "detail": r["detail"]})

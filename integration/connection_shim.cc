@@ -95,6 +95,7 @@ struct fec_conn_result {
   int32_t connected;            // connections still connected at the end
   int32_t status;               // 0 ok, else a failure code
   char detail[256];
+  double fec_wait_us;           // of fec_host_us: blocked waiting for the device (Complete(true))
 };
 }
 
@@ -546,6 +547,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     r->groups_encoded = batcher->stats().groups_encoded;
     r->groups_revived = batcher->stats().groups_revived;
     r->fec_host_us = batcher->stats().launch_us + batcher->stats().complete_us;
+    r->fec_wait_us = batcher->stats().wait_us;
   }
   r->turns = turn;
   r->stream_bytes = params->stream_len;

@@ -296,9 +296,21 @@ int QuicFecBatcher::Complete(bool wait) {
     stats_.complete_us += std::chrono::duration<double, std::micro>(
                               std::chrono::steady_clock::now() - t0).count();
   };
-  const int erc = QuicFecGroup::Finish(&enc_pending_, wait);
+  // poll first; a blocking wait for the device is timed on its own (wait_us:
+  // the GPU's latency, not connection-thread work)
+  auto finish = [&](QuicFecGroup::Pending* p) {
+    int r = QuicFecGroup::Finish(p, false);
+    if (r == QFEC_PENDING && wait) {
+      const auto w0 = std::chrono::steady_clock::now();
+      r = QuicFecGroup::Finish(p, true);
+      stats_.wait_us += std::chrono::duration<double, std::micro>(
+                            std::chrono::steady_clock::now() - w0).count();
+    }
+    return r;
+  };
+  const int erc = finish(&enc_pending_);
   if (erc == QFEC_PENDING) return spent(), QFEC_PENDING;
-  const int rrc = QuicFecGroup::Finish(&rev_pending_, wait);
+  const int rrc = finish(&rev_pending_);
   if (rrc == QFEC_PENDING) return spent(), QFEC_PENDING;  // enc_pending_ keeps its result
   spent();
   // callbacks may add new work (an emitted FEC packet lets the next packets

@@ -240,6 +240,9 @@ class QuicFecBatcher {
     // lengths) — not the visitors' callbacks
     double launch_us = 0;
     double complete_us = 0;
+    // of complete_us: blocked in a waiting Complete(true) until the device
+    // finished (a connection thread that polls with Complete(false) skips it)
+    double wait_us = 0;
   };
 
   explicit QuicFecBatcher(qfec_ctx* ctx = nullptr) : ctx_(ctx) {}

@@ -135,6 +135,171 @@ __global__ __launch_bounds__(kBlock) void null_enc_timed(ProtectArgs a, uint64_t
     r[0] = t0; r[1] = t1; r[2] = t2; r[3] = th; r[4] = tw; r[5] = tx;
   }
 }
+// ---------------------------------------------------------------------------
+// LDS-DMA form: the payload slabs go global -> LDS by
+// global_load_lds_dwordx4 (no VGPR staging: the 2 x SC u32x4 register slabs
+// and the ds_write transpose disappear), NB slab buffers per wave, one wave
+// per workgroup.  Instruction I of a slab: lane L loads packet
+// P = (64/SC) I + L/SC, slot m = L % SC holds chunk m ^ swz(P) — the swizzle
+// on the SOURCE address keeps the hashing lanes' row reads (lane q: chunk j of
+// packet q at slot j ^ swz(q)) on distinct 16-B bank slots in every
+// ds_read_b128 lane group.  The payload copy reads the slab back lane-linear
+// (conflict-free) and stores it from the loading lane.  Waits are counted:
+// per slab the wave issues exactly n_ld (loads) and n_st (stores) VMEM
+// instructions (wave-uniform ballot branches), vmcnt(n) retires slab s while
+// the later slabs' loads and the earlier slabs' stores stay in flight.
+// ---------------------------------------------------------------------------
+template <uint32_t N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15u) | ((N >> 4) << 14) | 0x0F70u);
+}
+template <uint32_t LO, uint32_t HI>
+__device__ __forceinline__ void wait_vm_range(uint32_t n) {
+  if constexpr (LO == HI) {
+    wait_vm<LO>();
+  } else {
+    constexpr uint32_t M = (LO + HI) / 2;
+    if (n <= M) wait_vm_range<LO, M>(n);
+    else wait_vm_range<M + 1, HI>(n);
+  }
+}
+// vmcnt(min(n, MAXN)) (stricter when clamped), n wave-uniform: a binary tree
+// of scalar branches over the immediate forms
+template <uint32_t MAXN>
+__device__ __forceinline__ void wait_vm_dyn(uint32_t n) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  wait_vm_range<0, MAXN>(n < MAXN ? n : MAXN);
+}
+
+template <uint32_t SC>
+__device__ __forceinline__ uint32_t glds_swz(uint32_t P) { return (P / (16u / SC)) & (SC - 1u); }
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <uint32_t SC, uint32_t NB>
+__global__ __launch_bounds__(64) void null_encrypt_glds_kernel(ProtectArgs a) {
+  static_assert(NB >= 2 && SC >= 4 && SC <= 16, "shape");
+  __shared__ __attribute__((aligned(16))) u32x4 s_buf[NB][64 * SC];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
+  const bool valid = p < a.n;
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = a.bytes;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  if (valid) {
+    ad = a.bytes + a.ad_off[p];
+    pt = a.bytes + a.in_off[p];
+    alen = a.ad_len[p];
+    plen = a.in_len[p];
+    o = a.out + a.out_off[p];
+  }
+  const uint32_t nfull = plen >> 4;
+  uint8_t* dst = valid ? o + kTag : nullptr;
+  const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  Fnv128 h = fnv_init();
+  if (valid) fnv_span<true>(h, ad, alen);
+  const bool overlap = valid && o + kTag < pt + plen && pt < o + kTag + plen;
+  const bool inplace = wave_any_qpp(overlap);
+  // this lane's loader roles
+  const uint8_t* lsrc[SC];
+  uint8_t* ldst[SC];
+  uint32_t lnf[SC], lch[SC];
+#pragma unroll
+  for (uint32_t I = 0; I < SC; ++I) {
+    const uint32_t P = (64u / SC) * I + lane / SC;
+    lsrc[I] = (const uint8_t*)shfl64((uint64_t)pt, P);
+    ldst[I] = (uint8_t*)shfl64((uint64_t)dst, P);
+    lnf[I] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(P << 2), (int)nfull);
+    lch[I] = (lane % SC) ^ glds_swz<SC>(P);
+  }
+  const uint32_t nslab = (wave_max_u32(nfull) + SC - 1) / SC;
+  const uint32_t myswz = glds_swz<SC>(lane);
+  uint32_t nld[NB];  // VMEM loads issued per buffered slab
+#pragma unroll
+  for (uint32_t b = 0; b < NB; ++b) nld[b] = 0;
+  auto load = [&](uint32_t sl, uint32_t b) {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t I = 0; I < SC; ++I) {
+      const uint32_t c = sl * SC + lch[I];
+      const bool act = c < lnf[I];
+      if (__ballot(act)) {
+        ++cnt;
+        if (act)
+          __builtin_amdgcn_global_load_lds((const void*)(lsrc[I] + 16u * c),
+                                           (__attribute__((address_space(3))) void*)&s_buf[b][64 * I],
+                                           16, 0, 0);
+      }
+    }
+    return cnt;
+  };
+  // prologue: slabs 0 .. NB-2 in flight
+#pragma unroll
+  for (uint32_t s = 0; s + 1 < NB; ++s)
+    if (s < nslab) nld[s] = load(s, s);
+  uint32_t nsth[NB];  // stores issued per slab (ring; the NB-1 latest count)
+#pragma unroll
+  for (uint32_t b = 0; b < NB; ++b) nsth[b] = 0;
+  for (uint32_t sl = 0; sl < nslab; ++sl) {
+    const uint32_t b = sl % NB;
+    // issue slab sl + NB - 1 into the buffer slab sl - 1 used
+    const uint32_t nx = sl + NB - 1u;
+    const uint32_t bn = nx % NB;
+    nld[bn] = nx < nslab ? load(nx, bn) : 0u;
+    // VMEM instructions issued after slab sl's loads (iteration sl-NB+1):
+    // the later slabs' loads and the stores of slabs sl-NB+1 .. sl-1
+    uint32_t after = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < NB; ++k) after += nld[(sl + k) % NB] + nsth[(sl + k) % NB];
+    constexpr uint32_t kMaxAfter = 2u * (NB - 1) * SC < 63u ? 2u * (NB - 1) * SC : 63u;
+    wait_vm_dyn<kMaxAfter>(after);
+    __builtin_amdgcn_wave_barrier();
+    // hash this lane's row (all SC reads issued before the first use)
+    {
+      u32x4 r[SC];
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j) r[j] = s_buf[b][lane * SC + (j ^ myswz)];
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j)
+        if (sl * SC + j < nfull) fnv_chunk<true>(h, r[j]);
+    }
+    // in place: the next slab's loads must have landed before these stores
+    if (inplace) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (uint32_t k = 0; k < NB; ++k) nsth[k] = 0;
+    }
+    uint32_t nst = 0;
+    {
+      u32x4 w[SC];
+#pragma unroll
+      for (uint32_t I = 0; I < SC; ++I) w[I] = s_buf[b][64 * I + lane];
+#pragma unroll
+      for (uint32_t I = 0; I < SC; ++I) {
+        const uint32_t c = sl * SC + lch[I];
+        const bool act = c < lnf[I] && ldst[I] != nullptr;
+        if (__ballot(act)) {
+          ++nst;
+          if (act) st16g(ldst[I] + 16u * c, w[I]);
+        }
+      }
+    }
+    nsth[b] = nst;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!valid) return;
+  fnv_tail(h, tail, plen);
+  store_tail(o + kTag, tail, plen);
+  const uint32_t tag[3] = {h.x0, h.x1, h.x2};
+  __builtin_memcpy(o, tag, kTag);
+}
+
 }  // namespace
 }  // namespace qfec
 
@@ -229,6 +394,31 @@ int main(int argc, char** argv) {
   }
   uint32_t* sink;
   CK(hipMalloc(&sink, 4));
+  // LDS-DMA variants: bit-identical output to the product kernel
+  uint8_t* d_outg;
+  CK(hipMalloc(&d_outg, n * (L + 12)));
+  qfec::ProtectArgs eg = e;
+  eg.out = d_outg;
+  const uint32_t gblocks = (uint32_t)((n + 63) / 64);
+  std::vector<std::pair<std::string, std::function<void()>>> glds = {
+      {"glds SC=16 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds SC=8 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds SC=8 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds SC=4 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<4, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds SC=4 NB=4", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<4, 4>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+  };
+  {
+    std::vector<uint8_t> ref(n * (L + 12)), got(n * (L + 12));
+    CK(qfec::launch_null_protect(e, false, 0));
+    CK(hipMemcpy(ref.data(), d_out, ref.size(), hipMemcpyDeviceToHost));
+    for (auto& g : glds) {
+      CK(hipMemset(d_outg, 0xA5, ref.size()));
+      g.second();
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), d_outg, got.size(), hipMemcpyDeviceToHost));
+      std::printf("%-24s output %s\n", g.first.c_str(), got == ref ? "IDENTICAL" : "DIFFERS");
+    }
+  }
   struct V {
     std::string name;
     double bytes;  // algorithmic bytes (HBM) per launch
@@ -276,6 +466,11 @@ int main(int argc, char** argv) {
        [&] { hipLaunchKernelGGL(fnv_valu_chunk_kernel<false>, dim3(vgrid), dim3(256), 0, 0, vb, sink); }},
       {"null encrypt staged serial FNV", enc_b, hashed, [&] {
          hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, e); }},
+      {"glds SC=16 NB=2", enc_b, hashed, glds[0].second},
+      {"glds SC=8 NB=2", enc_b, hashed, glds[1].second},
+      {"glds SC=8 NB=3", enc_b, hashed, glds[2].second},
+      {"glds SC=4 NB=3", enc_b, hashed, glds[3].second},
+      {"glds SC=4 NB=4", enc_b, hashed, glds[4].second},
       {"null decrypt staged serial FNV", dec_b, hashed, [&] {
          hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
   };
