@@ -155,6 +155,13 @@ typedef const __attribute__((address_space(1))) u32x4_a1* gld_ptr;
 typedef __attribute__((address_space(1))) u32x4_a1* gst_ptr;
 __device__ __forceinline__ u32x4 ld16g(const uint8_t* p) { return *(gld_ptr)p; }
 __device__ __forceinline__ void st16g(uint8_t* p, u32x4 v) { *(gst_ptr)p = v; }
+// nontemporal forms (streamed once: no L2 retention)
+__device__ __forceinline__ u32x4 ld16gn(const uint8_t* p) {
+  return __builtin_nontemporal_load((gld_ptr)p);
+}
+__device__ __forceinline__ void st16gn(uint8_t* p, u32x4 v) {
+  __builtin_nontemporal_store(v, (gst_ptr)p);
+}
 
 // The last len % 16 bytes of a span as the upper bytes of one 16-byte chunk
 // (len >= 16: the 16 bytes ending at the span end) or, for len < 16, the
@@ -197,16 +204,6 @@ __device__ __forceinline__ void fnv_span(Fnv128& h, const uint8_t* p, uint32_t l
   fnv_tail(h, tail, len);
 }
 
-// Store the tail bytes of a span (counterpart of load_tail).
-__device__ __forceinline__ void store_tail(uint8_t* d, u32x4 v, uint32_t len) {
-  if ((len & 15u) == 0u) return;
-  if (len >= 16u) {
-    st16(d + len - 16u, v);  // overlaps the last full chunk with identical bytes
-    return;
-  }
-  for (uint32_t i = 0; i < len; ++i) d[i] = (uint8_t)byte_of(v, i);
-}
-
 // ---------------------------------------------------------------------------
 // LDS-staged forms: a wave owns 64 packets (lane q hashes packet q) but the
 // payload bytes are moved by coalesced wave loads — lane 8i+m of load
@@ -226,9 +223,10 @@ constexpr uint32_t kSlabChunks = 16;
 constexpr int kWaves = kBlock / 64;
 
 struct StageMeta {
-  const uint8_t* src;  // payload start
+  const uint8_t* src;  // payload start (chunk c at src + 16 c)
   uint8_t* dst;        // payload copy destination (nullptr: no copy)
-  uint32_t nfull;      // full 16-B chunks
+  uint32_t nfull;      // chunks [lo, nfull) are the packet's
+  uint32_t lo;         // (0 when omitted; > 0: slabs start on a 128-B line, line_meta)
 };
 
 // The staged rows pass data between lanes of one wave through LDS: the LDS
@@ -245,7 +243,7 @@ __device__ __forceinline__ void wave_lds_order() {
 // Cooperative load of slab `sl` (SC chunks per packet) for the wave's 64
 // packets: lane (SC*i + m) of instruction I takes chunk m of packet
 // (64/SC)*I + i; SC instructions cover the 64 packets.
-template <uint32_t SC, bool G = true>
+template <uint32_t SC, bool G = true, bool NT = false>
 __device__ __forceinline__ void stage_load(const StageMeta* meta, uint32_t lane, uint32_t sl,
                                            u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
@@ -254,12 +252,13 @@ __device__ __forceinline__ void stage_load(const StageMeta* meta, uint32_t lane,
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
-    if (c < q.nfull) v[I] = G ? ld16g(q.src + 16u * c) : ld16(q.src + 16u * c);
+    if (c >= q.lo && c < q.nfull)
+      v[I] = NT ? ld16gn(q.src + 16u * c) : G ? ld16g(q.src + 16u * c) : ld16(q.src + 16u * c);
   }
   wave_lds_order();
 }
 
-template <uint32_t SC, bool G = true>
+template <uint32_t SC, bool G = true, bool NT = false>
 __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane, uint32_t sl,
                                             const u32x4 (&v)[SC]) {
   const uint32_t i = lane / SC, m = lane % SC;
@@ -268,8 +267,9 @@ __device__ __forceinline__ void stage_store(const StageMeta* meta, uint32_t lane
 #pragma unroll
   for (uint32_t I = 0; I < SC; ++I) {
     const StageMeta& q = meta[(64u / SC) * I + i];
-    if (c < q.nfull && q.dst) {
-      if (G) st16g(q.dst + 16u * c, v[I]);
+    if (c >= q.lo && c < q.nfull && q.dst) {
+      if (NT) st16gn(q.dst + 16u * c, v[I]);
+      else if (G) st16g(q.dst + 16u * c, v[I]);
       else st16(q.dst + 16u * c, v[I]);
     }
   }
@@ -299,30 +299,124 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // payloads.  In-place safe for dst == src + 12: slab s is stored only after
 // slab s+1 has been loaded AND the loads have completed (waitcnt), so no store
 // overtakes a load of the 12 bytes it overwrites.
-template <bool COPY, uint32_t SC, bool R3 = true, bool INPLACE = true>
+template <bool COPY, uint32_t SC, bool R3 = true, bool INPLACE = true, bool NT = false>
 __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32x4* rows,
-                                           uint32_t lane, uint32_t my_nfull) {
+                                           uint32_t lane, uint32_t my_nfull,
+                                           uint32_t my_lo = 0u) {
   const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
   u32x4 cur[SC], nxt[SC];
-  if (nslab) stage_load<SC>(meta, lane, 0, cur);
+  if (nslab) stage_load<SC, true, NT>(meta, lane, 0, cur);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
     stage_to_lds<SC>(rows, lane, cur);
-    if (sl + 1u < nslab) stage_load<SC>(meta, lane, sl + 1u, nxt);
+    if (sl + 1u < nslab) stage_load<SC, true, NT>(meta, lane, sl + 1u, nxt);
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j)
-      if (sl * SC + j < my_nfull) fnv_chunk<R3>(h, rows[lane * (SC + 1u) + j]);
+      if (sl * SC + j >= my_lo && sl * SC + j < my_nfull)
+        fnv_chunk<R3>(h, rows[lane * (SC + 1u) + j]);
     if constexpr (COPY) {
       // in place: vmcnt(0), the next slab's loads are done before this slab's
       // stores overwrite them; out of place the stores go out at once
       if constexpr (INPLACE) __builtin_amdgcn_s_waitcnt(0x0F70);
-      stage_store<SC>(meta, lane, sl, cur);
+      stage_store<SC, true, NT>(meta, lane, sl, cur);
     }
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
   }
 }
 
-template <uint32_t SC, bool R3 = true>
+// Destination-aligned chunking.  A 16-B store that straddles a 16-B boundary
+// costs the memory pipeline about as much as two: with the payload copy's
+// destination unaligned (the tag shifts it by 12 from wherever the output
+// sits), encrypt ran 1.86 ms on 2^21 packets against 1.45 with the output
+// 16-B aligned and the input still unaligned (1.33 with both aligned;
+// profiles/round3/null_align/).  So the coalesced chunks are cut where the
+// DESTINATION is 16-B aligned: the first hd = (16 - dst % 16) % 16 payload
+// bytes (the head) and the last (plen - hd) % 16 (the tail) are hashed and
+// stored by the packet's own lane; the hash is byte-serial, so cutting the
+// bytes differently changes nothing in the tag.
+__device__ __forceinline__ uint32_t word_sel(u32x4 v, uint32_t w) {
+  return w == 0u ? v.x : w == 1u ? v.y : w == 2u ? v.z : w == 3u ? v.w : 0u;
+}
+// bytes [i, i + 4) of a chunk (zero past byte 15)
+__device__ __forceinline__ uint32_t bytes4_at(u32x4 v, uint32_t i) {
+  return __builtin_amdgcn_alignbyte(word_sel(v, (i >> 2) + 1u), word_sel(v, i >> 2), i & 3u);
+}
+__device__ __forceinline__ void fnv_bytes(Fnv128& h, u32x4 v, uint32_t from, uint32_t n) {
+  for (uint32_t i = from; i < from + n; ++i) fnv_step(h, byte_of(v, i));
+}
+// bytes [from, from + n) of v to p, n < 16, p + n 16-B aligned: peeled 1, 2, 4, 8
+// (each piece lands on its own alignment)
+__device__ __forceinline__ void store_to_aligned_end(uint8_t* p, u32x4 v, uint32_t from,
+                                                     uint32_t n) {
+  uint32_t i = 0;
+  if (n & 1u) {
+    p[0] = (uint8_t)byte_of(v, from);
+    i = 1;
+  }
+  if (n & 2u) {
+    *(uint16_t*)(p + i) = (uint16_t)bytes4_at(v, from + i);
+    i += 2;
+  }
+  if (n & 4u) {
+    *(uint32_t*)(p + i) = bytes4_at(v, from + i);
+    i += 4;
+  }
+  if (n & 8u) {
+    const uint64_t lo = bytes4_at(v, from + i), hi = bytes4_at(v, from + i + 4u);
+    *(uint64_t*)(p + i) = lo | (hi << 32);
+  }
+}
+// bytes [from, from + n) of v to p, n < 16, p 16-B aligned: 8, 4, 2, 1
+__device__ __forceinline__ void store_from_aligned_start(uint8_t* p, u32x4 v, uint32_t from,
+                                                         uint32_t n) {
+  uint32_t i = 0;
+  if (n & 8u) {
+    const uint64_t lo = bytes4_at(v, from), hi = bytes4_at(v, from + 4u);
+    *(uint64_t*)p = lo | (hi << 32);
+    i = 8;
+  }
+  if (n & 4u) {
+    *(uint32_t*)(p + i) = bytes4_at(v, from + i);
+    i += 4;
+  }
+  if (n & 2u) {
+    *(uint16_t*)(p + i) = (uint16_t)bytes4_at(v, from + i);
+    i += 2;
+  }
+  if (n & 1u) p[i] = (uint8_t)byte_of(v, from + i);
+}
+// the first min(16, len) bytes of a span at bytes [0, ..) of a chunk
+__device__ __forceinline__ u32x4 load_head(const uint8_t* p, uint32_t len) {
+  return len >= 16u ? ld16(p) : load_tail(p, len);
+}
+
+// Split of a payload of plen bytes copied to dst: head hd bytes, nmid
+// 16-B chunks starting at dst + hd (16-B aligned), tail tl bytes.
+struct DstSplit {
+  uint32_t hd, nmid, tl;
+};
+__device__ __forceinline__ DstSplit dst_split(const uint8_t* dst, uint32_t plen) {
+  const uint32_t u = (uint32_t)(uintptr_t)dst & 15u;
+  const uint32_t hd = min((16u - u) & 15u, plen);
+  const uint32_t nmid = (plen - hd) >> 4;
+  return DstSplit{hd, nmid, plen - hd - 16u * nmid};
+}
+// position in the load_tail chunk of payload byte x
+__device__ __forceinline__ uint32_t tail_pos(uint32_t x, uint32_t plen) {
+  return plen >= 16u ? x - (plen - 16u) : x;
+}
+// nmid 16-B chunks at src / dst, `al` (src or dst) 16-B aligned: the slab
+// grid is shifted back to al's 128-B line (chunks [lo, lo + nmid) of the
+// shifted grid), so every slab's run of a packet covers whole lines and a
+// wave instruction touches 8 lines for 1 KiB instead of up to 12 (2^21
+// packets: 1.79 -> see profiles/round3/null_align/).
+__device__ __forceinline__ StageMeta line_meta(const uint8_t* src, uint8_t* dst, uint32_t nmid,
+                                               const uint8_t* al) {
+  const uint32_t lo = ((uint32_t)(uintptr_t)al & 127u) >> 4;
+  return StageMeta{src - 16u * lo, dst ? dst - 16u * lo : nullptr, lo + nmid, lo};
+}
+
+template <uint32_t SC, bool R3 = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -340,25 +434,33 @@ __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs
     plen = a.in_len[p];
     o = a.out + a.out_off[p];
   }
-  s_meta[wv][lane] = StageMeta{pt, o + kTag, plen >> 4};
-  // the payload's last len % 16 bytes, before any store (in place)
+  const DstSplit sp = dst_split(o + kTag, plen);
+  const StageMeta m = line_meta(pt + sp.hd, o + kTag + sp.hd, sp.nmid, o + kTag + sp.hd);
+  s_meta[wv][lane] = m;
+  // head and tail bytes, before any store (in place)
+  const u32x4 head = valid ? load_head(pt, plen) : u32x4{0u, 0u, 0u, 0u};
   const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
   Fnv128 h = fnv_init();
-  if (valid) fnv_span<R3>(h, ad, alen);
+  if (valid) {
+    fnv_span<R3>(h, ad, alen);
+    fnv_bytes(h, head, 0u, sp.hd);
+  }
   // does any packet of the wave write over its own payload (EncryptInPlace)?
   const bool overlap = valid && o + kTag < pt + plen && pt < o + kTag + plen;
   if (wave_any_qpp(overlap))
-    stage_hash<true, SC, R3, true>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+    stage_hash<true, SC, R3, true, NT>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
   else
-    stage_hash<true, SC, R3, false>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+    stage_hash<true, SC, R3, false, NT>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
   if (!valid) return;
-  fnv_tail(h, tail, plen);
-  store_tail(o + kTag, tail, plen);
+  const uint32_t t0 = tail_pos(sp.hd + 16u * sp.nmid, plen);
+  fnv_bytes(h, tail, t0, sp.tl);
+  store_from_aligned_start(o + kTag + sp.hd + 16u * sp.nmid, tail, t0, sp.tl);
+  store_to_aligned_end(o + kTag, head, 0u, sp.hd);
   const uint32_t tag[3] = {h.x0, h.x1, h.x2};
   __builtin_memcpy(o, tag, kTag);
 }
 
-template <uint32_t SC, bool R3 = true>
+template <uint32_t SC, bool R3 = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -369,6 +471,7 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   if (p < a.n && !valid) a.ok[p] = 0;  // ReadHash fails (null_decrypter.cc:48-50)
   const uint8_t* ad = nullptr;
   const uint8_t* ct = nullptr;
+  uint8_t* o = nullptr;
   uint32_t alen = 0, plen = 0;
   uint32_t tag[3] = {0u, 0u, 0u};
   if (valid) {
@@ -376,36 +479,51 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
     ct = a.bytes + a.in_off[p];
     alen = a.ad_len[p];
     plen = clen - kTag;
+    o = a.out + a.out_off[p];
     __builtin_memcpy(tag, ct, kTag);
   }
-  s_meta[wv][lane] = StageMeta{ct + kTag, nullptr, plen >> 4};
+  // the hash pass: chunks cut where the SOURCE is 16-B aligned (aligned loads)
+  const DstSplit hs = dst_split(ct + kTag, plen);
+  const StageMeta hm = line_meta(ct + kTag + hs.hd, nullptr, hs.nmid, ct + kTag + hs.hd);
+  s_meta[wv][lane] = hm;
+  const u32x4 head = valid ? load_head(ct + kTag, plen) : u32x4{0u, 0u, 0u, 0u};
   const u32x4 tail = valid ? load_tail(ct + kTag, plen) : u32x4{0u, 0u, 0u, 0u};
   Fnv128 h = fnv_init();
-  if (valid) fnv_span<R3>(h, ad, alen);
-  stage_hash<false, SC, R3>(h, s_meta[wv], s_rows[wv], lane, plen >> 4);
+  if (valid) {
+    fnv_span<R3>(h, ad, alen);
+    fnv_bytes(h, head, 0u, hs.hd);
+  }
+  stage_hash<false, SC, R3, true, NT>(h, s_meta[wv], s_rows[wv], lane, hm.nfull, hm.lo);
   // ComputeHash keeps the low 96 bits (null_decrypter.cc:97-106)
   bool ok = false;
   if (valid) {
-    fnv_tail(h, tail, plen);
+    fnv_bytes(h, tail, tail_pos(hs.hd + 16u * hs.nmid, plen), hs.tl);
     ok = h.x0 == tag[0] && h.x1 == tag[1] && h.x2 == tag[2];
     a.ok[p] = ok ? 1 : 0;
   }
-  // copy after the check (null_decrypter.cc:60-62), coalesced, verified packets only
-  uint8_t* o = ok ? a.out + a.out_off[p] : nullptr;
-  s_meta[wv][lane] = StageMeta{ct + kTag, o, ok ? plen >> 4 : 0u};
+  // copy after the check (null_decrypter.cc:60-62), coalesced, verified
+  // packets only, chunks cut where the DESTINATION is 16-B aligned
+  const DstSplit sp = dst_split(o, ok ? plen : 0u);
+  const StageMeta cm = line_meta(ct + kTag + sp.hd, ok ? o + sp.hd : nullptr, ok ? sp.nmid : 0u,
+                                 o + sp.hd);
+  s_meta[wv][lane] = cm;
   // Slab s+1's loads are in flight while slab s is stored (out of place: no
   // load/store ordering hazard); a load-then-store loop parked the waves on
   // every slab's round trip (SQ_WAIT_ANY 0.76 of the decrypt's wave cycles).
-  const uint32_t nslab = (wave_max_u32(ok ? plen >> 4 : 0u) + SC - 1) / SC;
+  const uint32_t nslab = (wave_max_u32(ok ? cm.nfull : 0u) + SC - 1) / SC;
   u32x4 cur[SC], nxt[SC];
-  if (nslab) stage_load<SC>(s_meta[wv], lane, 0, cur);
+  if (nslab) stage_load<SC, true, NT>(s_meta[wv], lane, 0, cur);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
-    if (sl + 1u < nslab) stage_load<SC>(s_meta[wv], lane, sl + 1u, nxt);
-    stage_store<SC>(s_meta[wv], lane, sl, cur);
+    if (sl + 1u < nslab) stage_load<SC, true, NT>(s_meta[wv], lane, sl + 1u, nxt);
+    stage_store<SC, true, NT>(s_meta[wv], lane, sl, cur);
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
   }
-  if (ok) store_tail(o, tail, plen);
+  if (ok) {
+    store_to_aligned_end(o, head, 0u, sp.hd);
+    store_from_aligned_start(o + sp.hd + 16u * sp.nmid, tail,
+                             tail_pos(sp.hd + 16u * sp.nmid, plen), sp.tl);
+  }
 }
 
 // ===========================================================================

@@ -172,3 +172,46 @@ def test_short_payloads(ctx, lmax):
     got = encrypt_dev(ctx, data, ad_off, ad_len, pt_off, pt_len, out_off, size)
     want = OC.null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, size)
     assert np.array_equal(got, want)
+    # and back: every head / tail split of the destination-aligned copy
+    hdr = np.concatenate([data[int(o):int(o) + int(l)] for o, l in zip(ad_off, ad_len)])
+    h_off = offsets(ad_len.astype(np.uint64))
+    ct_len = (pt_len.astype(np.uint64) + TAG).astype(np.uint16)
+    buf = np.concatenate([hdr, got])
+    ct_off = out_off + np.uint64(hdr.size)
+    dout_off = offsets(pt_len.astype(np.uint64)) + np.uint64(3)
+    dsize = int(pt_len.astype(np.int64).sum()) + 4
+    out, ok = decrypt_dev(ctx, buf, h_off, ad_len, ct_off, ct_len, dout_off, dsize)
+    want_out, want_ok = OC.null_decrypt_batch(buf, h_off, ad_len, ct_off, ct_len, dout_off, dsize)
+    assert ok.all() and np.array_equal(ok, want_ok)
+    assert np.array_equal(out, want_out)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_encrypt_in_place_random(ctx, seed):
+    """EncryptInPlace on scattered records of random lengths: every alignment
+    of the payload (and so of the destination, payload + 12) against the
+    destination-aligned head / chunk / tail split."""
+    rng = np.random.default_rng(100 + seed)
+    n = 6000
+    ad_len = rng.integers(0, 48, n).astype(np.uint16)
+    pt_len = rng.integers(0, 1453, n).astype(np.uint16)
+    gaps = rng.integers(0, 19, n).astype(np.uint64)
+    rec = ad_len.astype(np.uint64) + pt_len.astype(np.uint64) + TAG + gaps
+    ad_off = offsets(rec) + gaps
+    pt_off = ad_off + ad_len.astype(np.uint64)
+    size = int(ad_off[-1] + ad_len[-1] + pt_len[-1]) + TAG
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    want = OC.null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, pt_off, size)
+    d = dv(data)
+    ctx.null_encrypt(d, dv(ad_off), dv(ad_len), dv(pt_off), dv(pt_len), n, d, dv(pt_off))
+    ctx.sync()
+    torch.cuda.synchronize()
+    res = d.cpu().numpy()
+    for p in range(0, n, 7):
+        o, c = int(pt_off[p]), int(pt_len[p]) + TAG
+        assert np.array_equal(res[o:o + c], want[o:o + c]), p
+    mask = np.zeros(size, bool)
+    for o, c in zip(pt_off, pt_len.astype(np.int64) + TAG):
+        mask[int(o):int(o) + int(c)] = True
+    assert np.array_equal(res[mask], want[mask])
+    assert np.array_equal(res[~mask], data[~mask])  # headers and gaps untouched

@@ -68,6 +68,20 @@ __global__ void fnv_valu_chunk2_kernel(uint32_t bytes, uint32_t* sink) {
   if ((h.x0 ^ h.x1 ^ h.x2 ^ h.x3 ^ g.x0 ^ g.x3) == 0x12345678u) sink[0] = h.x0;
 }
 
+namespace qfec {
+namespace {
+// the round-2 tail store (the tune kernels below keep source-relative chunks)
+__device__ __forceinline__ void store_tail(uint8_t* d, u32x4 v, uint32_t len) {
+  if ((len & 15u) == 0u) return;
+  if (len >= 16u) {
+    st16(d + len - 16u, v);
+    return;
+  }
+  for (uint32_t i = 0; i < len; ++i) d[i] = (uint8_t)byte_of(v, i);
+}
+}  // namespace
+}  // namespace qfec
+
 // null_encrypt_staged_kernel<16> with a per-wave timeline (s_memrealtime,
 // 10 ns ticks): where does a wave's life go?
 namespace qfec {
@@ -419,6 +433,32 @@ int main(int argc, char** argv) {
       std::printf("%-24s output %s\n", g.first.c_str(), got == ref ? "IDENTICAL" : "DIFFERS");
     }
   }
+  // the same packets with every payload and every output payload on a 128-B
+  // line (record stride 1408 = 11 lines): what is unaligned loading worth?
+  std::vector<uint64_t> aad(n), ain(n), aout(n);
+  for (uint64_t p = 0; p < n; ++p) {
+    aad[p] = p * 1408 + 106;
+    ain[p] = p * 1408 + 128;
+    aout[p] = p * 1408 + 116;
+  }
+  uint8_t *d_ain, *d_aout;
+  CK(hipMalloc(&d_ain, n * 1408 + 4096));
+  CK(hipMalloc(&d_aout, n * 1408 + 4096));
+  CK(hipMemset(d_ain, 0x3C, n * 1408 + 4096));
+  qfec::ProtectArgs ea = e;
+  ea.bytes = d_ain; ea.ad_off = up(aad); ea.in_off = up(ain); ea.out = d_aout; ea.out_off = up(aout);
+  const uint32_t sblocks = (uint32_t)((n + 255) / 256);
+  // (a) payload aligned, output payload at +4 mod 16; (b) payload at +6 mod 16, output aligned
+  std::vector<uint64_t> bad_(n), bin(n), aout2(n);
+  for (uint64_t p = 0; p < n; ++p) {
+    aout2[p] = p * 1408 + 120;  // dst = +132
+    bad_[p] = p * 1408 + 112;
+    bin[p] = p * 1408 + 134;    // src = +134 (6 mod 16)
+  }
+  qfec::ProtectArgs eA = ea, eB = ea;
+  eA.out_off = up(aout2);
+  eB.ad_off = up(bad_);
+  eB.in_off = up(bin);
   struct V {
     std::string name;
     double bytes;  // algorithmic bytes (HBM) per launch
@@ -471,6 +511,18 @@ int main(int argc, char** argv) {
       {"glds SC=8 NB=3", enc_b, hashed, glds[2].second},
       {"glds SC=4 NB=3", enc_b, hashed, glds[3].second},
       {"glds SC=4 NB=4", enc_b, hashed, glds[4].second},
+      {"ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(ea, false, 0)); }},
+      {"ALIGNED staged SC=8", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<8>), dim3(sblocks), dim3(256), 0, 0, ea); }},
+      {"ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
+      {"ALIGNED glds SC=8 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
+      {"ALIGNED glds SC=8 NB=3", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, ea); }},
+      {"nt staged enc SC=16", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, e); }},
+      {"nt staged dec SC=16", dec_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, d); }},
+      {"SRC-ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eA, false, 0)); }},
+      {"SRC-ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eA); }},
+      {"DST-ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eB, false, 0)); }},
+      {"DST-ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eB); }},
+      {"ALIGNED glds SC=4 NB=3", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<4, 3>), dim3(gblocks), dim3(64), 0, 0, ea); }},
       {"null decrypt staged serial FNV", dec_b, hashed, [&] {
          hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, false>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, d); }},
   };
