@@ -110,6 +110,49 @@ def build_cpp_tests(force: bool = False) -> list:
     return outs
 
 
+# the host C++ (payload arena, group bookkeeping, receive
+# map, CSR builders, batcher) under AddressSanitizer + UBSan on the CPU,
+# against tests/cpp/cpu_qfec_stub.c (test infrastructure: a CPU restatement of
+# the C-ABI calls the host code makes; never part of libqfec.so).
+# (ThreadSanitizer as well for the group test: worker threads fill groups
+# whose arena slabs outlive them.)
+SAN_TESTS = [("san", "test_quic_fec_group"), ("san", "test_quic_fec_connection"),
+             ("tsan", "test_quic_fec_group")]
+HOST_SRCS = ["quic_fec_group.cc", "quic_fec_wire.cc", "quic_fec_connection.cc"]
+SAN_FLAGS = {
+    "san": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+            "-fno-omit-frame-pointer", "-g", "-O1"],
+    "tsan": ["-fsanitize=thread", "-g", "-O1"],
+}
+
+
+def build_cpp_sanitized(force: bool = False) -> list:
+    outs = []
+    bdir = os.path.join(ROOT, "tests", "cpp", "build")
+    stub = os.path.join(ROOT, "tests", "cpp", "cpu_qfec_stub.c")
+    oracle_c = os.path.join(ROOT, "oracle", "qfec_oracle.c")
+    hosts = [os.path.join(CSRC, f) for f in HOST_SRCS]
+    for kind, name in SAN_TESTS:
+        flags = SAN_FLAGS[kind]
+        src = os.path.join(ROOT, "tests", "cpp", name + ".cc")
+        out = os.path.join(bdir, f"{kind}_{name}")
+        deps = [src, stub, oracle_c] + hosts + [os.path.join(CSRC, h) for h in HEADERS]
+        if force or _stale(out, deps):
+            os.makedirs(bdir, exist_ok=True)
+            objs = []
+            for c in (stub, oracle_c):
+                o = os.path.join(bdir, f"{kind}_{os.path.basename(c)}.o")
+                _run(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "include"),
+                      "-c", c, "-o", o])
+                objs.append(o)
+            _run(["g++", "-std=c++17", "-Wall", *flags, "-I", os.path.join(ROOT, "include"),
+                  "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), src, *hosts, *objs,
+                  "-lpthread", "-o", out])
+        outs.append(out)
+    return outs
+
+
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv)
     build_cpp_tests(force="--force" in sys.argv)
+    build_cpp_sanitized(force="--force" in sys.argv)

@@ -94,6 +94,13 @@ bool QuicFecSender::CloseFecGroup(QuicPacketNumber fec_packet_number,
 // QuicFecEncodeBatch
 // ---------------------------------------------------------------------------
 int QuicFecEncodeBatch::Flush(qfec_ctx* ctx) {
+  // every entry must fit the v<=31 FEC header (uint8 group offset,
+  // quic_framer.cc:1126-1136) before anything is launched: FecPacketBody()
+  // then cannot fail after a successful Flush
+  for (const Entry& e : entries_)
+    if (!e.group || e.fec_group == 0 || e.fec_group > e.fec_packet_number ||
+        e.fec_packet_number - e.fec_group > 0xFF)
+      return QFEC_ERR_INVALID_FEC_DATA;
   std::vector<QuicFecGroup*> groups;
   groups.reserve(entries_.size());
   for (Entry& e : entries_) groups.push_back(e.group.get());

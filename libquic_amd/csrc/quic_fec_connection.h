@@ -117,7 +117,10 @@ class QuicFecEncodeBatch {
     // while the entry lives.  QuicFramer::BuildFecPacket writes the header.
     StringPiece redundancy;
     // The v<=31 FEC packet body: private header + redundancy
-    // (SerializeFecPacketBody); empty before Flush.
+    // (SerializeFecPacketBody); empty before Flush.  Flush refuses a batch
+    // with an entry outside the uint8 group-offset range
+    // (QFEC_ERR_INVALID_FEC_DATA), so after a successful Flush it is never
+    // empty.
     std::vector<uint8_t> FecPacketBody() const;
   };
 

@@ -11,18 +11,62 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
+
+#if defined(__SANITIZE_ADDRESS__)
+#include <sanitizer/asan_interface.h>
+#define QFEC_POISON(p, n) ASAN_POISON_MEMORY_REGION((p), (n))
+#define QFEC_UNPOISON(p, n) ASAN_UNPOISON_MEMORY_REGION((p), (n))
+#else
+#define QFEC_POISON(p, n) ((void)(p), (void)(n))
+#define QFEC_UNPOISON(p, n) ((void)(p), (void)(n))
+#endif
 
 namespace net {
 namespace {
 
 // Per-thread bump allocator over slabs of pinned, device-mapped host memory
-// (heap slabs when no device is present).  Slabs live for the process and
-// are reused once everything allocated in them has been released.
+// (heap slabs when no device is present).  A slab is reused once everything
+// allocated in it has been released; a thread's slabs go to a process-wide
+// pool when the thread exits (its payloads may still be alive), and any
+// thread takes a drained slab from the pool before allocating a new one, so
+// the pinned footprint is bounded by the peak of live payloads, not by the
+// number of threads that ever ran.  Under AddressSanitizer the free parts of
+// a slab are poisoned: an access past a payload's own bytes is reported.
 struct ArenaSlab {
   uint8_t* base = nullptr;
   size_t used = 0;
   std::atomic<size_t> live{0};  // bytes handed out and not yet released
   bool mapped = false;
+};
+
+class SlabPool {
+ public:
+  static SlabPool& Get() {
+    static SlabPool* p = new SlabPool();  // never destroyed: outlives thread exits
+    return *p;
+  }
+  void Put(std::vector<ArenaSlab*>* slabs) {
+    std::lock_guard<std::mutex> l(mu_);
+    slabs_.insert(slabs_.end(), slabs->begin(), slabs->end());
+    slabs->clear();
+  }
+  ArenaSlab* TakeDrained() {
+    std::lock_guard<std::mutex> l(mu_);
+    for (size_t i = 0; i < slabs_.size(); ++i) {
+      if (slabs_[i]->live.load(std::memory_order_acquire) == 0) {
+        ArenaSlab* s = slabs_[i];
+        slabs_[i] = slabs_.back();
+        slabs_.pop_back();
+        return s;
+      }
+    }
+    return nullptr;
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<ArenaSlab*> slabs_;
 };
 
 class PayloadArena {
@@ -34,19 +78,23 @@ class PayloadArena {
     return a;
   }
 
+  ~PayloadArena() { SlabPool::Get().Put(&slabs_); }
+
   // n <= kSlabBytes; returns 16-byte aligned storage.
   uint8_t* Alloc(size_t n, ArenaSlab** slab) {
-    n = (n + 15) & ~size_t(15);
-    if (!cur_ || cur_->used + n > kSlabBytes) cur_ = NextSlab();
+    const size_t r = (n + 15) & ~size_t(15);
+    if (!cur_ || cur_->used + r > kSlabBytes) cur_ = NextSlab();
     if (!cur_) return nullptr;
     uint8_t* p = cur_->base + cur_->used;
-    cur_->used += n;
-    cur_->live.fetch_add(n, std::memory_order_relaxed);
+    cur_->used += r;
+    cur_->live.fetch_add(r, std::memory_order_relaxed);
+    QFEC_UNPOISON(p, n);
     *slab = cur_;
     return p;
   }
 
-  static void Release(ArenaSlab* slab, size_t n) {
+  static void Release(ArenaSlab* slab, uint8_t* p, size_t n) {
+    QFEC_POISON(p, n);
     slab->live.fetch_sub((n + 15) & ~size_t(15), std::memory_order_acq_rel);
   }
 
@@ -57,6 +105,11 @@ class PayloadArena {
         s->used = 0;
         return s;
       }
+    }
+    if (ArenaSlab* s = SlabPool::Get().TakeDrained()) {
+      s->used = 0;
+      slabs_.push_back(s);
+      return s;
     }
     ArenaSlab* s = new ArenaSlab();
     if (mapped_ok_) {
@@ -69,11 +122,12 @@ class PayloadArena {
       delete s;
       return nullptr;
     }
+    QFEC_POISON(s->base, kSlabBytes);
     slabs_.push_back(s);
     return s;
   }
 
-  std::vector<ArenaSlab*> slabs_;  // process lifetime (outstanding payloads may outlive the thread)
+  std::vector<ArenaSlab*> slabs_;
   ArenaSlab* cur_ = nullptr;
   bool mapped_ok_ = true;
 };
@@ -113,7 +167,7 @@ QuicFecGroup::Span QuicFecGroup::ArenaAlloc(size_t n) {
 }
 
 void QuicFecGroup::ArenaFree(Span* sp) {
-  if (sp->p) PayloadArena::Release(static_cast<ArenaSlab*>(sp->slab), sp->n);
+  if (sp->p) PayloadArena::Release(static_cast<ArenaSlab*>(sp->slab), sp->p, sp->n);
   *sp = Span();
 }
 

@@ -212,6 +212,7 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
   senders[0]->set_max_packets_per_fec_group(255);
   size_t revived_total = 0, flushes = 0, batched_groups = 0;
   std::vector<QuicFecReviveBatch::Revived> revived;
+  std::vector<std::string> revived_bytes;  // owned copies (the views end with their batch)
   bool done = false;
   while (!done) {
     done = true;
@@ -305,6 +306,9 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
       const size_t before = revived.size();
       EXPECT(rb.Flush(ctx, &revived) == QFEC_OK);
       revived_total += revived.size() - before;
+      // the payload views live as long as rb's groups: copy them out
+      for (size_t i = before; i < revived.size(); ++i)
+        revived_bytes.emplace_back(revived[i].payload.data(), revived[i].payload.size());
     }
   }
   // expected revivals: exactly one data packet lost and the FEC packet received
@@ -326,13 +330,15 @@ static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double lo
   }
   EXPECT(revived_total == expect);
   size_t exact = 0;
-  for (auto& r : revived) {
+  for (size_t k = 0; k < revived.size(); ++k) {
+    const auto& r = revived[k];
+    const std::string& rp = revived_bytes[k];
     const int c = static_cast<int>(reinterpret_cast<intptr_t>(r.tag));
     EXPECT(want_revived.count({c, r.header.packet_number}) == 1);
     const std::string& p = payloads[{c, r.header.packet_number}];
     // revived payload = original, zero padded to the redundancy length
-    bool ok = r.payload.size() >= p.size() && std::memcmp(r.payload.data(), p.data(), p.size()) == 0;
-    for (size_t i = p.size(); ok && i < r.payload.size(); ++i) ok = r.payload.data()[i] == '\0';
+    bool ok = rp.size() >= p.size() && std::memcmp(rp.data(), p.data(), p.size()) == 0;
+    for (size_t i = p.size(); ok && i < rp.size(); ++i) ok = rp[i] == '\0';
     EXPECT(ok);
     exact += ok;
   }

@@ -12,7 +12,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "qfec_oracle.h"
@@ -193,6 +195,32 @@ int main() {
       StringPiece got = groups[g]->PayloadParity();
       EXPECT(got.size() == want.size() && std::memcmp(got.data(), want.data(), want.size()) == 0);
       delete groups[g];
+    }
+  }
+  // payload arena across threads: groups filled on worker threads outlive
+  // them (a thread's slabs go to the process-wide pool when it exits), are
+  // computed and destroyed here; the second round's threads take the drained
+  // slabs back from the pool
+  for (int round = 0; round < 3; ++round) {
+    const int T = 6, k = 5;
+    std::vector<std::unique_ptr<QuicFecGroup>> made(T);
+    std::vector<std::vector<std::string>> pays(T);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; ++t)
+      ts.emplace_back([&, t] {
+        pays[t] = MakePayloads(k, 0x7000 + 16 * round + t);
+        made[t].reset(new QuicFecGroup(1));  // the thread's default context
+        for (int i = 0; i < k; ++i)
+          made[t]->Update(ENCRYPTION_NONE, Header(1 + i, 1, false), pays[t][i]);
+      });
+    for (auto& th : ts) th.join();
+    std::vector<QuicFecGroup*> gs;
+    for (auto& g : made) gs.push_back(g.get());
+    EXPECT(QuicFecGroup::ComputeAll(ctx, gs) == QFEC_OK);
+    for (int t = 0; t < T; ++t) {
+      const std::string want = OracleParity(pays[t]);
+      const StringPiece got = made[t]->PayloadParity();
+      EXPECT(got.size() == want.size() && std::memcmp(got.data(), want.data(), want.size()) == 0);
     }
   }
   // wire format: FEC packet header round trip (v<=31 private flags + offset)
