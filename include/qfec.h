@@ -88,8 +88,8 @@ extern "C" {
                                are ordinary host memory, staged by the call.
                                Returns when the results are in host memory. */
 #define QFEC_ONE_PASS 8u    /* fixed-shape device calls: always the one-pass
-                               kernel.  Without it a large nt batch (>= 8 phases,
-                               about 246K groups at L = 1350 on 256 CUs) runs the
+                               kernel.  Without it a large nt batch (>= 6 phases,
+                               about 184K groups at L = 1350 on 256 CUs) runs the
                                phased kernel: one workgroup per CU, reads and
                                parity writes in separate grid-wide phases, which
                                keeps its rate independent of where the buffers
@@ -365,6 +365,11 @@ int qfec_phase_backoff(qfec_ctx* ctx);
  * reset_backoff clear the contention backoff (forgetting abandoned launches
  * so far).  Waits for the stream. */
 int qfec_debug_phase(qfec_ctx* ctx, uint32_t extra, int reset_backoff);
+/* Test hook: fixed-shape batches of at least `min_phases` phases (a phase is
+ * one workgroup per CU x 8 steps x the groups per workgroup step) run the
+ * phased kernel; 0 restores the default (6 phases, about 184K headline
+ * groups).  1 forces it for any batch, 0xFFFFFFFF never. */
+int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases);
 /* Test hook: fail != 0 makes every ragged call on this context fail with
  * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
  * connection integration: groups go without FEC). */

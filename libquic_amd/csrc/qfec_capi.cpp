@@ -79,6 +79,7 @@ struct qfec_ctx {
   uint32_t phase_backoff = 0;
   uint32_t ncu = 0;          // CU count, queried once
   uint32_t phase_extra = 0;  // test hook (qfec_debug_phase)
+  uint32_t phase_min = 0;    // test hook (qfec_debug_phase_min)
   bool debug_fail = false;   // test hook (qfec_debug_fail_launches)
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
@@ -494,6 +495,7 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
   const bool nt = (flags & QFEC_CACHED) == 0;
   a.ncu = ctx->ncu;
   a.phase_extra = ctx->phase_extra;
+  a.phase_min = ctx->phase_min;
   a.phase_host = ctx->h_phase_dev;
   a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
   if (a.phase_sync && qfec::fixed_uses_phases(a, nt)) {
@@ -1583,6 +1585,13 @@ int qfec_debug_phase(qfec_ctx* ctx, uint32_t extra, int reset_backoff) {
     ctx->phase_seen = __atomic_load_n(ctx->h_phase, __ATOMIC_ACQUIRE);
     ctx->phase_backoff = 0;
   }
+  return QFEC_OK;
+}
+
+int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  ctx->phase_min = min_phases;
   return QFEC_OK;
 }
 

@@ -44,6 +44,9 @@ struct FixedArgs {
   uint32_t ncu = 0;
   uint32_t phase_extra = 0;
   uint32_t* phase_host = nullptr;
+  // minimum phase count for the phased kernel (0: kPhMinPhases, about 184K
+  // headline groups); test hook qfec_debug_phase_min, for the band study
+  uint32_t phase_min = 0;
 };
 
 // True if launch_fixed(a, nontemporal, ...) runs the phased kernel.

@@ -22,7 +22,7 @@
 //    L2/TA handle the line crossing.
 //  * Recover reads the parity row *in place of* the lost row: k loads per lane,
 //    every one unconditional — the lost slot is never read and no lane idles.
-//  * Batches of >= 8 phases (about 246K groups at L = 1350) run
+//  * Batches of >= 6 phases (about 184K groups at L = 1350) run
 //    phase_xor_kernel instead: the same lanes and loads in a persistent
 //    one-workgroup-per-CU grid that separates the row reads and the parity
 //    writes into grid-wide phases (0.80 of 8 TB/s on any buffer placement).
@@ -1427,11 +1427,14 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
   return hipGetLastError();
 }
 
-// The phased kernel for a batch of at least kPhMinPhases phases (about 246K
+// The phased kernel for a batch of at least kPhMinPhases phases (about 184K
 // groups at L = 1350 on 256 CUs): the two meetings per phase cost ~2-3 us
 // each, and below that the one-pass kernel's placement luck matters less
-// than they do.  Returns false when it does not apply.
-constexpr uint32_t kPhMinPhases = 8;
+// than they do.  Measured crossover (tools/phase_band.py,
+// profiles/round3/phase/phase_band_r3d.txt): one-pass 0.77 vs phased 0.73 of
+// 8 TB/s at 131K groups, 0.75 vs 0.76 at 196K, 0.74 vs 0.78 at 262K.
+// Returns false when it does not apply.
+constexpr uint32_t kPhMinPhases = 6;
 
 // The CU count comes cached from the context (FixedArgs::ncu); the test hook
 // phase_extra (tests/test_hip_phase.py) adds workgroups beyond one per CU,
@@ -1442,7 +1445,7 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
   const uint64_t per = (uint64_t)wg * kPhSteps * gpb;
   const uint64_t np = (a.n_groups + per - 1) / per;
-  if (np < kPhMinPhases || np > 0xFFFFFFFFull) return false;
+  if (np < (a.phase_min ? a.phase_min : kPhMinPhases) || np > 0xFFFFFFFFull) return false;
   *grid = wg;
   *nphase = (uint32_t)np;
   return true;

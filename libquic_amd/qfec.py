@@ -93,6 +93,7 @@ SIGNATURES = [
     ("qfec_phase_abandons", C.c_int, [_vp, _vp]),
     ("qfec_phase_backoff", C.c_int, [_vp]),
     ("qfec_debug_phase", C.c_int, [_vp, C.c_uint32, C.c_int]),
+    ("qfec_debug_phase_min", C.c_int, [_vp, C.c_uint32]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
@@ -378,6 +379,11 @@ class Context:
         """Test hook: extra workgroups in phased launches (forces the abandon
         path); reset_backoff clears the contention backoff."""
         return self._check(self.lib.qfec_debug_phase(self.ctx, extra, int(reset_backoff)))
+
+    def debug_phase_min(self, min_phases):
+        """Test hook: phased kernel from `min_phases` phases on (0 default,
+        1 always, 0xFFFFFFFF never)."""
+        return self._check(self.lib.qfec_debug_phase_min(self.ctx, min_phases))
 
     def complete(self, wait=True):
         """Finish QFEC_ASYNC calls: 0 done, QFEC_PENDING (1) still running."""

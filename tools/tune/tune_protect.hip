@@ -314,6 +314,119 @@ __global__ __launch_bounds__(64) void null_encrypt_glds_kernel(ProtectArgs a) {
   __builtin_memcpy(o, tag, kTag);
 }
 
+// The LDS-DMA form with the product's destination-aligned split and 128-B
+// line grid (line_meta); meta from LDS, not per-lane register arrays.
+template <uint32_t SC, uint32_t NB>
+__global__ __launch_bounds__(64) void null_encrypt_glds2_kernel(ProtectArgs a) {
+  __shared__ __attribute__((aligned(16))) u32x4 s_buf[NB][64 * SC];
+  __shared__ StageMeta s_meta[64];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
+  const bool valid = p < a.n;
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = nullptr;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  if (valid) {
+    ad = a.bytes + a.ad_off[p];
+    pt = a.bytes + a.in_off[p];
+    alen = a.ad_len[p];
+    plen = a.in_len[p];
+    o = a.out + a.out_off[p];
+  }
+  const DstSplit sp = dst_split(o + kTag, plen);
+  const StageMeta m = line_meta(pt + sp.hd, o + kTag + sp.hd, sp.nmid, o + kTag + sp.hd);
+  s_meta[lane] = m;
+  const u32x4 head = valid ? load_head(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  Fnv128 h = fnv_init();
+  if (valid) {
+    fnv_span<true>(h, ad, alen);
+    fnv_bytes(h, head, 0u, sp.hd);
+  }
+  const bool overlap = valid && o + kTag < pt + plen && pt < o + kTag + plen;
+  const bool inplace = wave_any_qpp(overlap);
+  const uint32_t li = lane / SC, lm = lane % SC;
+  const uint32_t nslab = (wave_max_u32(m.nfull) + SC - 1) / SC;
+  const uint32_t myswz = glds_swz<SC>(lane);
+  wave_lds_order();
+  uint32_t nld[NB], nsth[NB];
+#pragma unroll
+  for (uint32_t b = 0; b < NB; ++b) nld[b] = nsth[b] = 0;
+  auto load = [&](uint32_t sl, uint32_t b) {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t I = 0; I < SC; ++I) {
+      const uint32_t P = (64u / SC) * I + li;
+      const StageMeta& q = s_meta[P];
+      const uint32_t c = sl * SC + (lm ^ glds_swz<SC>(P));
+      const bool act = c >= q.lo && c < q.nfull;
+      if (__ballot(act)) {
+        ++cnt;
+        if (act)
+          __builtin_amdgcn_global_load_lds((const void*)(q.src + 16u * c),
+                                           (__attribute__((address_space(3))) void*)&s_buf[b][64 * I],
+                                           16, 0, 0);
+      }
+    }
+    return cnt;
+  };
+#pragma unroll
+  for (uint32_t s0 = 0; s0 + 1 < NB; ++s0)
+    if (s0 < nslab) nld[s0] = load(s0, s0);
+  for (uint32_t sl = 0; sl < nslab; ++sl) {
+    const uint32_t b = sl % NB;
+    const uint32_t nx = sl + NB - 1u;
+    const uint32_t bn = nx % NB;
+    nld[bn] = nx < nslab ? load(nx, bn) : 0u;
+    uint32_t after = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < NB; ++k) after += nld[(sl + k) % NB] + nsth[(sl + k) % NB];
+    constexpr uint32_t kMaxAfter = 2u * (NB - 1) * SC < 63u ? 2u * (NB - 1) * SC : 63u;
+    wait_vm_dyn<kMaxAfter>(after);
+    __builtin_amdgcn_wave_barrier();
+    {
+      u32x4 r[SC];
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j) r[j] = s_buf[b][lane * SC + (j ^ myswz)];
+#pragma unroll
+      for (uint32_t j = 0; j < SC; ++j)
+        if (sl * SC + j >= m.lo && sl * SC + j < m.nfull) fnv_chunk<true>(h, r[j]);
+    }
+    if (inplace) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (uint32_t k = 0; k < NB; ++k) nsth[k] = 0;
+    }
+    uint32_t nst = 0;
+    {
+      u32x4 w[SC];
+#pragma unroll
+      for (uint32_t I = 0; I < SC; ++I) w[I] = s_buf[b][64 * I + lane];
+#pragma unroll
+      for (uint32_t I = 0; I < SC; ++I) {
+        const uint32_t P = (64u / SC) * I + li;
+        const StageMeta& q = s_meta[P];
+        const uint32_t c = sl * SC + (lm ^ glds_swz<SC>(P));
+        const bool act = c >= q.lo && c < q.nfull && q.dst != nullptr;
+        if (__ballot(act)) {
+          ++nst;
+          if (act) st16g(q.dst + 16u * c, w[I]);
+        }
+      }
+    }
+    nsth[b] = nst;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!valid) return;
+  const uint32_t t0 = tail_pos(sp.hd + 16u * sp.nmid, plen);
+  fnv_bytes(h, tail, t0, sp.tl);
+  store_from_aligned_start(o + kTag + sp.hd + 16u * sp.nmid, tail, t0, sp.tl);
+  store_to_aligned_end(o + kTag, head, 0u, sp.hd);
+  const uint32_t tag[3] = {h.x0, h.x1, h.x2};
+  __builtin_memcpy(o, tag, kTag);
+}
+
 }  // namespace
 }  // namespace qfec
 
@@ -420,6 +533,9 @@ int main(int argc, char** argv) {
       {"glds SC=8 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
       {"glds SC=4 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<4, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
       {"glds SC=4 NB=4", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<4, 4>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds2 SC=16 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds2 SC=8 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<8, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"glds2 SC=8 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
   };
   {
     std::vector<uint8_t> ref(n * (L + 12)), got(n * (L + 12));
@@ -455,6 +571,11 @@ int main(int argc, char** argv) {
     bad_[p] = p * 1408 + 112;
     bin[p] = p * 1408 + 134;    // src = +134 (6 mod 16)
   }
+  // (c) both 16-B aligned, the payload on a line, the output payload 48 B into one
+  std::vector<uint64_t> aout3(n);
+  for (uint64_t p = 0; p < n; ++p) aout3[p] = p * 1408 + 164;  // dst = +176 = 48 mod 128
+  qfec::ProtectArgs eC = ea;
+  eC.out_off = up(aout3);
   qfec::ProtectArgs eA = ea, eB = ea;
   eA.out_off = up(aout2);
   eB.ad_off = up(bad_);
@@ -511,6 +632,9 @@ int main(int argc, char** argv) {
       {"glds SC=8 NB=3", enc_b, hashed, glds[2].second},
       {"glds SC=4 NB=3", enc_b, hashed, glds[3].second},
       {"glds SC=4 NB=4", enc_b, hashed, glds[4].second},
+      {"glds2 SC=16 NB=2", enc_b, hashed, glds[5].second},
+      {"glds2 SC=8 NB=2", enc_b, hashed, glds[6].second},
+      {"glds2 SC=8 NB=3", enc_b, hashed, glds[7].second},
       {"ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(ea, false, 0)); }},
       {"ALIGNED staged SC=8", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<8>), dim3(sblocks), dim3(256), 0, 0, ea); }},
       {"ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
@@ -518,6 +642,7 @@ int main(int argc, char** argv) {
       {"ALIGNED glds SC=8 NB=3", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, ea); }},
       {"nt staged enc SC=16", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, e); }},
       {"nt staged dec SC=16", dec_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, d); }},
+      {"SRC128-DST48 staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eC, false, 0)); }},
       {"SRC-ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eA, false, 0)); }},
       {"SRC-ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eA); }},
       {"DST-ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eB, false, 0)); }},
