@@ -180,6 +180,17 @@ int main(int argc, char** argv) {
                                      dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0,       \
                                      0xA5A5F00Du);                                             \
                 }})
+  if (getenv("TUNE_RW_DAL")) {  // round 3: destination-aligned stores, A/B twice each
+    RG_DIAG(false, 0, "diag0 product");
+    RG_DIAG(false, 10, "diag10 dst-aligned");
+    RG_DIAG(false, 0, "diag0 product (again)");
+    RG_DIAG(false, 10, "diag10 dst-aligned (again)");
+    vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_DIAG(true, 0, "diag0 product");
+    RG_DIAG(true, 10, "diag10 dst-aligned");
+    RG_DIAG(true, 0, "diag0 product (again)");
+    RG_DIAG(true, 10, "diag10 dst-aligned (again)");
+  }
   if (getenv("TUNE_RW_DIAG")) {
     RG_DIAG(false, 0, "diag0 product");
     RG_DIAG(false, 1, "diag1 nostore (not exact)");
@@ -209,7 +220,7 @@ int main(int argc, char** argv) {
     RG_DIAG(true, 5, "diag5 xcd+wb");
   }
 #undef RG_DIAG
-  const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr;
+  const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr || getenv("TUNE_RW_DAL") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
