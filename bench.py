@@ -782,6 +782,15 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
                                                             ct_len, n, dout, d_out_off, ok), reps)
     ctx.sync()
     verified = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
+    # the one-pass decrypt (QFEC_SCRATCH_OUTPUT: a failed packet's output may
+    # hold its unverified plaintext, as in QuicFramer's scratch buffer)
+    dout.fill_(0)
+    ok.zero_()
+    ms_d1 = _time_on(torch, stream, lambda: ctx.null_decrypt(
+        cat, c_ad_off, ad_len, c_ct_off, ct_len, n, dout, d_out_off, ok, scratch_out=True), reps)
+    ctx.sync()
+    verified = verified and bool(ok.all()) and torch.equal(dout.view(n, L),
+                                                           data.view(n, rec)[:, hdr:])
     # ChaCha20-Poly1305 (one key, packet numbers 1..n): seal -> out (ct || tag),
     # open of [header | ct || tag] records
     key = torch.arange(32, dtype=torch.uint8, device=dev) * 7 + 1
@@ -798,6 +807,14 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
         ok), reps)
     ctx.sync()
     verified_c = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
+    dout.fill_(0)
+    ok.zero_()
+    ms_co1 = _time_on(torch, stream, lambda: ctx.chacha20poly1305_open(
+        key, pre, kidx, pn, None, cat, c_ad_off, ad_len, c_ct_off, ct_len, n, dout, d_out_off,
+        ok, scratch_out=True), reps)
+    ctx.sync()
+    verified_c = verified_c and bool(ok.all()) and torch.equal(dout.view(n, L),
+                                                               data.view(n, rec)[:, hdr:])
     # AES-128-GCM-12 (one key: every wave key-uniform, the Shoup-table GHASH path)
     gkey = torch.arange(16, dtype=torch.uint8, device=dev) * 11 + 3
     out = torch.empty(n * (L + 12), dtype=torch.uint8, device=dev)
@@ -811,11 +828,21 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
         ok), reps)
     ctx.sync()
     verified_g = bool(ok.all()) and torch.equal(dout.view(n, L), data.view(n, rec)[:, hdr:])
+    dout.fill_(0)
+    ok.zero_()
+    ms_go1 = _time_on(torch, stream, lambda: ctx.aes128gcm_open(
+        gkey, pre, kidx, pn, None, cat, c_ad_off, ad_len, c_ct_off, ct_len, n, dout, d_out_off,
+        ok, scratch_out=True), reps)
+    ctx.sync()
+    verified_g = verified_g and bool(ok.all()) and torch.equal(dout.view(n, L),
+                                                               data.view(n, rec)[:, hdr:])
     b_enc = n * (hdr + L + L + 12)  # read header + payload, write tag + payload
     b_dec = n * (hdr + L + 12 + L)
     res = {"packets": n, "header": hdr, "payload": L,
            "encrypt_GiBps": round(b_enc / (ms_e / 1e3) / 2**30, 2),
            "decrypt_GiBps": round(b_dec / (ms_d / 1e3) / 2**30, 2),
+           "decrypt_scratch_out_GiBps": round(b_dec / (ms_d1 / 1e3) / 2**30, 2),
+           "decrypt_scratch_out_hbm_frac": round(b_dec / (ms_d1 / 1e3) / 8e12, 4),
            "encrypt_hashed_GBps": round(n * (hdr + L) / (ms_e / 1e3) / 1e9, 1),
            "encrypt_hbm_frac": round(b_enc / (ms_e / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
            "encrypt_us": round(ms_e * 1e3, 1), "decrypt_us": round(ms_d * 1e3, 1),
@@ -824,12 +851,14 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
            "chacha20poly1305": {
                "seal_GiBps": round(b_enc / (ms_cs / 1e3) / 2**30, 2),
                "open_GiBps": round(b_dec / (ms_co / 1e3) / 2**30, 2),
+               "open_scratch_out_GiBps": round(b_dec / (ms_co1 / 1e3) / 2**30, 2),
                "seal_payload_GBps": round(n * L / (ms_cs / 1e3) / 1e9, 1),
                "seal_us": round(ms_cs * 1e3, 1), "open_us": round(ms_co * 1e3, 1),
                "verified": verified_c},
            "aes128gcm": {
                "seal_GiBps": round(b_enc / (ms_gs / 1e3) / 2**30, 2),
                "open_GiBps": round(b_dec / (ms_go / 1e3) / 2**30, 2),
+               "open_scratch_out_GiBps": round(b_dec / (ms_go1 / 1e3) / 2**30, 2),
                "seal_payload_GBps": round(n * L / (ms_gs / 1e3) / 1e9, 1),
                "seal_us": round(ms_gs * 1e3, 1), "open_us": round(ms_go * 1e3, 1),
                "verified": verified_g}}

@@ -106,6 +106,19 @@ extern "C" {
                                context completes them first.  Ignored by other
                                calls.  (The event-loop form: launch the turn's
                                FEC work, serve sockets, complete it next turn.) */
+#define QFEC_SCRATCH_OUTPUT 32u /* decrypt / open calls (NULL, ChaCha20-Poly1305,
+                               AES-128-GCM-12; device pointers): the output of a
+                               packet whose tag fails may hold its unverified
+                               plaintext (ok[p] = 0 still), so the kernel reads
+                               the ciphertext once (hash and copy together)
+                               instead of twice.  QuicFramer::DecryptPayload
+                               decrypts into a scratch buffer, retries the
+                               alternative decrypter into the same buffer and
+                               drops the packet on failure
+                               (quic_framer.cc:1884-1930), so this is a drop-in
+                               for that caller; without the flag the output is
+                               untouched on failure, as NullDecrypter leaves it
+                               (crypto/null_decrypter.cc:57-62). */
 
 /* qfec_complete() with wait == 0: the QFEC_ASYNC work is still running. */
 #define QFEC_PENDING 1
@@ -246,8 +259,10 @@ size_t qfec_wire_fec_packet_body(uint64_t packet_number, uint64_t fec_group, int
  *   (crypto/null_decrypter.cc:38-64), called by QuicFramer::DecryptPayload
  *   (quic_framer.cc:1884): ok[p] = 1 and in_len[p] - 12 payload bytes at
  *   out + out_off[p] when the tag verifies; ok[p] = 0 and the output untouched
- *   when it does not (or in_len[p] < 12).  Output must not overlap the input.
- * flags: QFEC_PTR_DEVICE / QFEC_PTR_HOST as above. */
+ *   when it does not (or in_len[p] < 12; with QFEC_SCRATCH_OUTPUT a failed
+ *   packet's output holds its unverified plaintext).  Output must not overlap
+ *   the input.
+ * flags: QFEC_PTR_DEVICE / QFEC_PTR_HOST as above, QFEC_SCRATCH_OUTPUT. */
 int qfec_null_encrypt_batch(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* ad_off,
                             const uint16_t* ad_len, const uint64_t* in_off,
                             const uint16_t* in_len, uint64_t n_packets, uint8_t* out,

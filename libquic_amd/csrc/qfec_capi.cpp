@@ -1450,6 +1450,7 @@ int null_protect(qfec_ctx* ctx, bool decrypt, const uint8_t* bytes, const uint64
   a.out_off = out_off;
   a.ok = ok;
   a.n = n;
+  a.scratch_out = (flags & QFEC_SCRATCH_OUTPUT) ? 1u : 0u;
   QFEC_HIP(ctx, qfec::launch_null_protect(a, decrypt, ctx->stream));
   return QFEC_OK;
 }
@@ -1482,6 +1483,7 @@ int aead_protect(qfec_ctx* ctx, bool aes, bool decrypt, const uint8_t* keys, con
   a.io.out_off = out_off;
   a.io.ok = ok;
   a.io.n = n;
+  a.io.scratch_out = (decrypt && (flags & QFEC_SCRATCH_OUTPUT)) ? 1u : 0u;
   a.keys = keys;
   a.prefixes = prefixes;
   a.key_idx = key_idx;

@@ -87,6 +87,9 @@ struct ProtectArgs {
   const uint64_t* out_off;
   uint8_t* ok;  // decrypt: 1 = tag verified and payload written
   uint64_t n;
+  // decrypt with QFEC_SCRATCH_OUTPUT: one pass, the output of a packet whose
+  // tag fails holds its unverified plaintext (else untouched, two passes)
+  uint32_t scratch_out = 0;
 };
 
 hipError_t launch_null_protect(const ProtectArgs& a, bool decrypt, hipStream_t s);

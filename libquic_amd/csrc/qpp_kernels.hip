@@ -526,6 +526,57 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   }
 }
 
+// Decrypt in ONE pass (QFEC_SCRATCH_OUTPUT): hash and copy from the same
+// slab loads, as encrypt does, and the verdict afterwards — the output of a
+// packet whose tag fails then holds its unverified plaintext, which is what
+// BoringSSL's AEAD open leaves too and what QuicFramer::DecryptPayload
+// tolerates (it decrypts into a scratch buffer and drops such a packet,
+// quic_framer.cc:1884-1904).  The default two-pass kernel above keeps the
+// reference NullDecrypter's output-untouched contract; this one reads the
+// ciphertext once instead of twice.
+template <uint32_t SC, bool R3 = true>
+__global__ __launch_bounds__(kBlock) void null_decrypt_onepass_kernel(ProtectArgs a) {
+  __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
+  __shared__ StageMeta s_meta[kWaves][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t clen = p < a.n ? a.in_len[p] : 0u;
+  const bool valid = p < a.n && clen >= kTag;
+  if (p < a.n && !valid) a.ok[p] = 0;  // ReadHash fails (null_decrypter.cc:48-50)
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = nullptr;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  uint32_t tag[3] = {0u, 0u, 0u};
+  if (valid) {
+    ad = a.bytes + a.ad_off[p];
+    const uint8_t* ct = a.bytes + a.in_off[p];
+    pt = ct + kTag;
+    alen = a.ad_len[p];
+    plen = clen - kTag;
+    o = a.out + a.out_off[p];
+    __builtin_memcpy(tag, ct, kTag);
+  }
+  const DstSplit sp = dst_split(o, plen);
+  const StageMeta m = line_meta(pt + sp.hd, o + sp.hd, sp.nmid, o + sp.hd);
+  s_meta[wv][lane] = m;
+  const u32x4 head = valid ? load_head(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  Fnv128 h = fnv_init();
+  if (valid) {
+    fnv_span<R3>(h, ad, alen);
+    fnv_bytes(h, head, 0u, sp.hd);
+  }
+  // output never overlaps the input (qfec.h): no in-place ordering
+  stage_hash<true, SC, R3, false>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
+  if (!valid) return;
+  const uint32_t t0 = tail_pos(sp.hd + 16u * sp.nmid, plen);
+  fnv_bytes(h, tail, t0, sp.tl);
+  store_from_aligned_start(o + sp.hd + 16u * sp.nmid, tail, t0, sp.tl);
+  store_to_aligned_end(o, head, 0u, sp.hd);
+  a.ok[p] = (h.x0 == tag[0] && h.x1 == tag[1] && h.x2 == tag[2]) ? 1 : 0;
+}
+
 // ===========================================================================
 // ChaCha20-Poly1305 (RFC 7539 AEAD; QUIC: 12-byte tag)
 //   seal  AeadBaseEncrypter::EncryptPacket  crypto/aead_base_encrypter.cc:107-134
@@ -943,7 +994,11 @@ __global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
   __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
 }
 
-template <uint32_t SC>
+// ONEPASS (QFEC_SCRATCH_OUTPUT): MAC and decrypt from the same slab loads;
+// a packet whose tag fails keeps its unverified plaintext in the output, as
+// BoringSSL's open_impl leaves it (e_chacha20poly1305.c:142-176 decrypts
+// before it compares) — one read of the ciphertext instead of two.
+template <uint32_t SC, bool ONEPASS = false>
 __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -971,6 +1026,28 @@ __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
     poly_init(poly, k0);
     poly_span_padded(poly, ad, alen);
     tail = tail_bytes(load_tail(ct, plen), plen);
+  }
+  if constexpr (ONEPASS) {
+    uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta[wv][lane] = StageMeta{ct, o, plen >> 4};
+    aead_pass<SC, true, true, false>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
+    if (!valid) return;
+    const uint32_t rem = plen & 15u;
+    if (rem) {
+      poly_block(poly, tail);  // zero padded ciphertext tail
+      const uint32_t c = plen >> 4;
+      uint32_t ks[16];
+      chacha_block(key, 1u + c / 4u, ks);
+      const u32x4 pt = tail ^ ks_chunk_lane(ks, c & 3u);
+      uint8_t b[16];
+      __builtin_memcpy(b, &pt, 16);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * c + i] = b[i];
+    }
+    poly_lengths(poly, alen, plen);
+    uint32_t tag[3];
+    poly_finish(poly, tag);
+    a.io.ok[p] = ((tag[0] ^ want[0]) | (tag[1] ^ want[1]) | (tag[2] ^ want[2])) == 0u ? 1 : 0;
+    return;
   }
   // pass 1: MAC over the ciphertext (no output)
   s_meta[wv][lane] = StageMeta{ct, nullptr, plen >> 4};
@@ -1403,7 +1480,7 @@ constexpr int kGcmNB = 4;   // chunks per step of the payload passes
 // Everything after the key setup, for one packet per lane.  Instantiated
 // twice in the kernel when UNI: with the key-uniform wave's round keys as
 // wave-uniform values (SGPRs, 44 VGPRs freed) and with per-lane keys.
-template <uint32_t SC, bool OPEN, int NB>
+template <uint32_t SC, bool OPEN, int NB, bool ONEPASS = false>
 __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
                                            const uint32_t (&nonce)[3], Ghash& gh,
                                            const uint32_t* s_te, uint32_t copy, StageMeta* meta,
@@ -1440,6 +1517,29 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
     const u32x4 t = gf_to_block(gh.y) ^ ek0;
     const uint32_t tag[3] = {t.x, t.y, t.z};
     __builtin_memcpy(o + plen, tag, kTag);  // ct || tag
+  } else if constexpr (ONEPASS) {
+    // QFEC_SCRATCH_OUTPUT: GHASH over the ciphertext and CTR decryption from
+    // the same slab loads; a failed packet keeps its unverified plaintext
+    // (aead_aes_gcm_open decrypts before it compares, e_aes.c:1093-1140)
+    uint32_t want[3] = {0u, 0u, 0u};
+    if (valid) __builtin_memcpy(want, in + plen, kTag);
+    uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
+    s_meta_w[lane] = StageMeta{in, o, plen >> 4};
+    gcm_pass<SC, NB, true, true, false>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+                                    plen >> 4, true);
+    if (!valid) return;
+    if (rem) {
+      ghash_block(gh, tail);  // zero padded ciphertext tail
+      const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
+      uint8_t b[16];
+      __builtin_memcpy(b, &pt, 16);
+      for (uint32_t i = 0; i < rem; ++i) o[16u * ctail + i] = b[i];
+    }
+    ghash_lengths(gh, alen, plen);
+    const u32x4 ek0 = aes_encrypt(key, u32x4{nonce[0], nonce[1], nonce[2], 0x01000000u}, s_te,
+                                  copy);
+    const u32x4 t = gf_to_block(gh.y) ^ ek0;
+    a.io.ok[p] = ((t.x ^ want[0]) | (t.y ^ want[1]) | (t.z ^ want[2])) == 0u ? 1 : 0;
   } else {
     uint32_t want[3] = {0u, 0u, 0u};
     if (valid) __builtin_memcpy(want, in + plen, kTag);
@@ -1470,7 +1570,7 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
 }
 
 template <uint32_t SC, bool OPEN, int NB = kGcmNB, int BLOCK = kGcmBlock, int WPE = kGcmWPE,
-          bool UNI = true>
+          bool UNI = true, bool ONEPASS = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
 aes128gcm_kernel(AeadArgs a) {
   constexpr int kGcmWaves = BLOCK / 64;
@@ -1546,11 +1646,11 @@ aes128gcm_kernel(AeadArgs a) {
     AesKey ks;  // the wave's key as uniform values
 #pragma unroll
     for (int i = 0; i < 44; ++i) ks.rk[i] = (uint32_t)__builtin_amdgcn_readlane((int)key.rk[i], src);
-    gcm_packet<SC, OPEN, NB>(a, ks, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane, p, valid,
-                             ad, in, alen, plen);
+    gcm_packet<SC, OPEN, NB, ONEPASS>(a, ks, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+                                      p, valid, ad, in, alen, plen);
   } else {
-    gcm_packet<SC, OPEN, NB>(a, key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane, p,
-                             valid, ad, in, alen, plen);
+    gcm_packet<SC, OPEN, NB, ONEPASS>(a, key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
+                                      p, valid, ad, in, alen, plen);
   }
 }
 
@@ -1568,7 +1668,9 @@ hipError_t launch_null_protect(const ProtectArgs& a0, bool decrypt, hipStream_t 
     a.out_off += p;
     if (decrypt) a.ok += p;
     const uint32_t blocks = (uint32_t)((a.n + kBlock - 1) / kBlock);
-    if (decrypt)
+    if (decrypt && a.scratch_out)
+      hipLaunchKernelGGL(null_decrypt_onepass_kernel<kSlabChunks>, dim3(blocks), dim3(kBlock), 0, s, a);
+    else if (decrypt)
       hipLaunchKernelGGL(null_decrypt_staged_kernel<kSlabChunks>, dim3(blocks), dim3(kBlock), 0, s, a);
     else
       hipLaunchKernelGGL(null_encrypt_staged_kernel<kSlabChunks>, dim3(blocks), dim3(kBlock), 0, s, a);
@@ -1601,7 +1703,9 @@ hipError_t launch_chacha20poly1305(const AeadArgs& a0, bool decrypt, hipStream_t
     a.packet_number += p;
     if (a.path_id) a.path_id += p;
     const uint32_t blocks = (uint32_t)((a.io.n + kBlock - 1) / kBlock);
-    if (decrypt)
+    if (decrypt && a.io.scratch_out)
+      hipLaunchKernelGGL((c20p1305_open_kernel<SC, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else if (decrypt)
       hipLaunchKernelGGL(c20p1305_open_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
     else
       hipLaunchKernelGGL(c20p1305_seal_kernel<SC>, dim3(blocks), dim3(kBlock), 0, s, a);
@@ -1644,8 +1748,12 @@ hipError_t launch_gcm_shape(const AeadArgs& a0, hipStream_t s) {
     a.packet_number += p;
     if (a.path_id) a.path_id += p;
     const uint32_t blocks = (uint32_t)((a.io.n + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL((aes128gcm_kernel<SC, OPEN, kGcmNB, BLOCK, WPE>), dim3(blocks), dim3(BLOCK),
-                       0, s, a);
+    if (OPEN && a.io.scratch_out)
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, OPEN, kGcmNB, BLOCK, WPE, true, true>), dim3(blocks),
+                         dim3(BLOCK), 0, s, a);
+    else
+      hipLaunchKernelGGL((aes128gcm_kernel<SC, OPEN, kGcmNB, BLOCK, WPE>), dim3(blocks),
+                         dim3(BLOCK), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

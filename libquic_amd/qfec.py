@@ -27,6 +27,7 @@ QFEC_CACHED = 2
 QFEC_PTR_MAPPED = 4
 QFEC_ONE_PASS = 8
 QFEC_ASYNC = 16
+QFEC_SCRATCH_OUTPUT = 32
 QFEC_PENDING = 1
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
@@ -319,10 +320,13 @@ class Context:
             _ptr(out), _ptr(out_off), QFEC_PTR_HOST if host else 0))
 
     def null_decrypt(self, data, ad_off, ad_len, in_off, in_len, n, out, out_off, ok, *,
-                     host=False):
+                     host=False, scratch_out=False):
+        """scratch_out: QFEC_SCRATCH_OUTPUT (one pass; a failed packet's output
+        holds its unverified plaintext)."""
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_SCRATCH_OUTPUT if scratch_out else 0)
         return self._check(self.lib.qfec_null_decrypt_batch(
             self.ctx, _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
-            _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+            _ptr(out), _ptr(out_off), _ptr(ok), fl))
 
     def chacha20poly1305_seal(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
                               ad_len, in_off, in_len, n, out, out_off, *, host=False):
@@ -332,11 +336,13 @@ class Context:
             _ptr(out), _ptr(out_off), QFEC_PTR_HOST if host else 0))
 
     def chacha20poly1305_open(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
-                              ad_len, in_off, in_len, n, out, out_off, ok, *, host=False):
+                              ad_len, in_off, in_len, n, out, out_off, ok, *, host=False,
+                              scratch_out=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_SCRATCH_OUTPUT if scratch_out else 0)
         return self._check(self.lib.qfec_chacha20poly1305_open_batch(
             self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
             _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
-            _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+            _ptr(out), _ptr(out_off), _ptr(ok), fl))
 
     def aes128gcm_seal(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
                        ad_len, in_off, in_len, n, out, out_off, *, host=False):
@@ -346,11 +352,13 @@ class Context:
             _ptr(out), _ptr(out_off), QFEC_PTR_HOST if host else 0))
 
     def aes128gcm_open(self, keys, prefixes, key_idx, packet_number, path_id, data, ad_off,
-                       ad_len, in_off, in_len, n, out, out_off, ok, *, host=False):
+                       ad_len, in_off, in_len, n, out, out_off, ok, *, host=False,
+                       scratch_out=False):
+        fl = (QFEC_PTR_HOST if host else 0) | (QFEC_SCRATCH_OUTPUT if scratch_out else 0)
         return self._check(self.lib.qfec_aes128gcm_open_batch(
             self.ctx, _ptr(keys), _ptr(prefixes), _ptr(key_idx), _ptr(packet_number),
             _ptr(path_id), _ptr(data), _ptr(ad_off), _ptr(ad_len), _ptr(in_off), _ptr(in_len), n,
-            _ptr(out), _ptr(out_off), _ptr(ok), QFEC_PTR_HOST if host else 0))
+            _ptr(out), _ptr(out_off), _ptr(ok), fl))
 
     # -- packet-entropy bookkeeping --------------------------------------------
     def entropy_cumulative(self, entropy, conn_ptr, cum_base, n_conns, cum, *, n_packets=0,

@@ -50,7 +50,8 @@ def encrypt_dev(ctx, data, ad_off, ad_len, pt_off, pt_len, out_off, out_size, ho
     return out.cpu().numpy()
 
 
-def decrypt_dev(ctx, data, ad_off, ad_len, ct_off, ct_len, out_off, out_size, fill=0, host=False):
+def decrypt_dev(ctx, data, ad_off, ad_len, ct_off, ct_len, out_off, out_size, fill=0, host=False,
+                scratch_out=False):
     n = ct_len.size
     if host:
         out = np.full(out_size, fill, np.uint8)
@@ -60,7 +61,7 @@ def decrypt_dev(ctx, data, ad_off, ad_len, ct_off, ct_len, out_off, out_size, fi
     out = torch.full((out_size,), fill, dtype=torch.uint8, device=DEV)
     ok = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
     ctx.null_decrypt(dv(data), dv(ad_off), dv(ad_len), dv(ct_off), dv(ct_len), n, out,
-                     dv(out_off), ok)
+                     dv(out_off), ok, scratch_out=scratch_out)
     ctx.sync()
     torch.cuda.synchronize()
     return out.cpu().numpy(), ok.cpu().numpy()
@@ -215,3 +216,37 @@ def test_encrypt_in_place_random(ctx, seed):
         mask[int(o):int(o) + int(c)] = True
     assert np.array_equal(res[mask], want[mask])
     assert np.array_equal(res[~mask], data[~mask])  # headers and gaps untouched
+
+
+@pytest.mark.parametrize("lmax", [17, 1452])
+def test_decrypt_scratch_output_one_pass(ctx, lmax):
+    """QFEC_SCRATCH_OUTPUT: one pass over the ciphertext; ok[] as the oracle,
+    verified packets' plaintext exact, and a failed packet's output is its
+    unverified plaintext (the ciphertext after the tag), never anything else."""
+    n = 20_000
+    data, ad_off, ad_len, pt_off, pt_len = random_batch(n, 77 + lmax, lmax=lmax)
+    out_off = offsets(pt_len.astype(np.uint64) + TAG)
+    size = int(out_off[-1]) + int(pt_len[-1]) + TAG
+    ct = OC.null_encrypt_batch(data, ad_off, ad_len, pt_off, pt_len, out_off, size)
+    hdr = np.concatenate([data[int(o):int(o) + int(l)] for o, l in zip(ad_off, ad_len)])
+    h_off = offsets(ad_len.astype(np.uint64))
+    ct_len = (pt_len.astype(np.uint64) + TAG).astype(np.uint16)
+    flip = np.arange(0, n, 7)
+    pos = out_off[flip] + (np.arange(flip.size) % (ct_len[flip].astype(np.uint64)))
+    ct = ct.copy()
+    ct[pos.astype(np.int64)] ^= 0x10
+    buf = np.concatenate([hdr, ct])
+    ct_off = out_off + np.uint64(hdr.size)
+    dout_off = offsets(pt_len.astype(np.uint64)) + np.uint64(5)
+    dsize = int(pt_len.astype(np.int64).sum()) + 6
+    out, ok = decrypt_dev(ctx, buf, h_off, ad_len, ct_off, ct_len, dout_off, dsize, fill=0xA5,
+                          scratch_out=True)
+    want_out, want_ok = OC.null_decrypt_batch(buf, h_off, ad_len, ct_off, ct_len, dout_off, dsize)
+    assert np.array_equal(ok, want_ok)
+    assert want_ok[flip].sum() == 0 and want_ok.sum() == n - flip.size
+    for p in range(n):
+        o, l = int(dout_off[p]), int(pt_len[p])
+        c = int(ct_off[p]) + TAG
+        assert np.array_equal(out[o:o + l], buf[c:c + l]), p   # verified or not
+    good = np.repeat(ok.astype(bool), pt_len.astype(np.int64))
+    assert np.array_equal(out[5:5 + good.size][good], want_out[5:5 + good.size][good])
