@@ -29,7 +29,8 @@ class Result(C.Structure):
                  ("cpu_xor_us", C.c_double),
                  ("cpu_xor_groups", C.c_uint64), ("streams_ok", C.c_int32),
                  ("connected", C.c_int32), ("status", C.c_int32), ("detail", C.c_char * 256),
-                 ("fec_wait_us", C.c_double), ("fec_launch_us", C.c_double)])
+                 ("fec_wait_us", C.c_double), ("fec_launch_us", C.c_double),
+                 ("debug_revived", C.c_uint64)])
 
 
 _lib = None

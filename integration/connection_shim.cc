@@ -97,6 +97,7 @@ struct fec_conn_result {
   char detail[256];
   double fec_wait_us;           // of fec_host_us: blocked waiting for the device (Complete(true))
   double fec_launch_us;         // of fec_host_us: the batcher's Launch (tables + queueing)
+  uint64_t debug_revived;       // QuicConnectionDebugVisitor::OnRevivedPacket calls (servers)
 };
 }
 
@@ -272,6 +273,19 @@ class SimWriter : public QuicPacketWriter {
   bool client_;
   HeaderProbe probe_;
   std::string payload_;
+};
+
+// Where Chromium's QuicConnectionLogger would emit NetLog's
+// QUIC_SESSION_PACKET_HEADER_REVIVED (net_log_event_type_list.h:1834): the
+// debug visitor's OnRevivedPacket, which the patch restores.  libquic ships no
+// logger, so the harness counts the calls.
+class RevivalCounter : public QuicConnectionDebugVisitor {
+ public:
+  void OnRevivedPacket(const QuicPacketHeader& header, base::StringPiece payload) override {
+    ++count;
+    bytes += payload.size();
+  }
+  uint64_t count = 0, bytes = 0;
 };
 
 class Endpoint : public QuicConnectionVisitorInterface {
@@ -477,6 +491,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   std::vector<std::unique_ptr<Wire>> c2s(n), s2c(n);
   std::vector<std::unique_ptr<SimWriter>> cw(n), sw(n);
   std::vector<std::unique_ptr<Endpoint>> ce(n), se(n);
+  RevivalCounter revival_log;
   std::vector<std::unique_ptr<QuicConnection>> cc(n), sc(n);
   const IPEndPoint client_addr(IPAddress(10, 0, 0, 1), 4433);
   for (int i = 0; i < n; ++i) {
@@ -500,6 +515,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     }
     cc[i]->set_visitor(ce[i].get());
     sc[i]->set_visitor(se[i].get());
+    sc[i]->set_debug_visitor(&revival_log);
     ce[i]->conn = cc[i].get();
     se[i]->conn = sc[i].get();
     if (params->group_size > 0) cc[i]->EnableFecSending(params->group_size);
@@ -570,6 +586,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   }
   r->turns = turn;
   r->stream_bytes = params->stream_len;
+  r->debug_revived = revival_log.count;
   std::string first_close;
   for (int i = 0; i < n; ++i) {
     const QuicConnectionStats& cs = cc[i]->GetStats();

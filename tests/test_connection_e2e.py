@@ -100,6 +100,8 @@ def test_connection_fec_revives_every_single_loss(batched, group_size, drop_ever
     # at most one loss per group, never the FEC packet
     assert r["dropped"] == r["groups_one_loss"], r
     assert r["revived"] <= r["dropped"] <= r["revived"] + r["retransmitted"], r
+    # every revival reached the debug visitor (where a NetLog logger hooks in)
+    assert r["debug_revived"] == r["revived"], r
     if group_size <= 10:
         assert r["revived"] == r["dropped"], r
     if batched:
