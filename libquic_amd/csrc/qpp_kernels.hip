@@ -65,7 +65,7 @@ __device__ __forceinline__ void fnv_step(Fnv128& h, uint32_t b) {
   h.x3 = r3;
 }
 
-__device__ __forceinline__ void fnv_word(Fnv128& h, uint32_t w) {
+[[maybe_unused]] __device__ __forceinline__ void fnv_word(Fnv128& h, uint32_t w) {
   fnv_step(h, w & 0xFFu);
   fnv_step(h, (w >> 8) & 0xFFu);
   fnv_step(h, (w >> 16) & 0xFFu);
@@ -1473,7 +1473,6 @@ __device__ __forceinline__ void ghash_span_padded(Ghash& g, const uint8_t* d, ui
 // open +1.3% (profiles/round1/tune_gcm_g8.txt); smaller batches and open run
 // the 512-thread shape instead (launch_aes128gcm picks by batch size).
 constexpr int kGcmBlock = 768;
-constexpr int kGcmSC = 4;   // 16-B chunks per packet per slab
 constexpr int kGcmWPE = 3;  // waves per SIMD
 constexpr int kGcmNB = 4;   // chunks per step of the payload passes
 
