@@ -594,6 +594,13 @@ def main(argv=None):
         if not args.no_protect:
             line["protect"] = bench_protect(ctx, torch, dev, stream, G, k, L,
                                             cpu=not args.no_cpu_baseline)
+            if line.get("ceilings"):  # NULL encrypt is a copy + hash: its own roofline
+                cp = line["ceilings"]["copy_GBps"]
+                pr = line["protect"]
+                pr["encrypt_frac_of_copy_ceiling"] = round(
+                    pr["encrypt_hbm_frac"] * HBM_PEAK_GBS / cp, 4)
+                pr["decrypt_scratch_out_frac_of_copy_ceiling"] = round(
+                    pr["decrypt_scratch_out_hbm_frac"] * HBM_PEAK_GBS / cp, 4)
         _progress("protect done")
         if not args.no_entropy:
             line["entropy"] = bench_entropy(ctx, torch, dev, stream,
