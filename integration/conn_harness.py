@@ -16,7 +16,7 @@ class Params(C.Structure):
     _fields_ = [("version", C.c_int32), ("n_pairs", C.c_int32), ("group_size", C.c_int32),
                 ("drop_every", C.c_int32), ("stream_len", C.c_uint64), ("batched", C.c_int32),
                 ("max_turns", C.c_int32), ("fail_encode", C.c_int32),
-                ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("pad", C.c_int32)]
+                ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("reorder", C.c_int32)]
 
 
 _U64 = ("data_packets_sent fec_packets_sent dropped revived groups_one_loss fec_groups_skipped "
@@ -49,12 +49,12 @@ def lib():
 
 def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True,
         max_turns=20_000, fail_encode=False, require_gpu=False, version=31,
-        end_flush=True) -> dict:
+        end_flush=True, reorder=0) -> dict:
     """One simulated run; returns the result fields as a dict."""
     p = Params(version=version, n_pairs=n_pairs, group_size=group_size, drop_every=drop_every,
                stream_len=stream_len, batched=int(batched), max_turns=max_turns,
                fail_encode=int(fail_encode), require_gpu=int(require_gpu),
-               no_end_flush=int(not end_flush))
+               no_end_flush=int(not end_flush), reorder=reorder)
     r = Result()
     lib().fec_conn_run(C.byref(p), C.byref(r))
     out = {n: getattr(r, n) for n, _ in Result._fields_}

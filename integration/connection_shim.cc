@@ -71,7 +71,8 @@ struct fec_conn_params {
   int32_t fail_encode;  // 1: every FEC launch fails (GPU failure path)
   int32_t require_gpu;  // 1: fail (status 3) without a HIP device
   int32_t no_end_flush; // 1: no SendFecPacketNow at the end (partial groups: FEC alarm only)
-  int32_t pad;
+  int32_t reorder;       // R > 0: client->server packets reordered (adjacent pairs
+                         // swapped, about one in R held back a turn)
 };
 
 struct fec_conn_result {
@@ -368,6 +369,13 @@ void Endpoint::Pump() {
 }
 
 // About one group in drop_every loses the data packet at a per-group offset.
+uint64_t Mix(uint64_t z) {  // splitmix64 finaliser
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 bool DropPolicy(const fec_conn_params& p, QuicFecGroupNumber g, QuicPacketNumber pn) {
   if (p.drop_every <= 0) return false;
   const uint64_t h = (g + 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
@@ -422,6 +430,24 @@ WriteResult SimWriter::WritePacket(const char* buffer, size_t buf_len, const IPA
   }
   wire_->next.emplace_back(buffer, buf_len);
   return WriteResult(WRITE_STATUS_OK, static_cast<int>(buf_len));
+}
+
+// A reordering link (deterministic): adjacent packets of a turn swap places
+// with probability 1/2, and about one packet in R waits for the next turn
+// (it then arrives after packets sent after it, FEC packets included).
+void Reorder(std::vector<std::string>* now, std::vector<std::string>* later, int R, int turn,
+             int conn) {
+  std::vector<std::string> keep;
+  keep.reserve(now->size());
+  for (size_t j = 0; j < now->size(); ++j) {
+    const uint64_t h = Mix(((uint64_t)turn << 40) ^ ((uint64_t)conn << 20) ^ j);
+    if (h % (uint64_t)R == 0) later->push_back(std::move((*now)[j]));
+    else keep.push_back(std::move((*now)[j]));
+  }
+  for (size_t j = 0; j + 1 < keep.size(); j += 2)
+    if (Mix(((uint64_t)turn << 40) ^ ((uint64_t)conn << 20) ^ (j + 0x55555)) & 1)
+      std::swap(keep[j], keep[j + 1]);
+  now->swap(keep);
 }
 
 void crash_trace(int sig) {
@@ -535,6 +561,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     for (int i = 0; i < n; ++i) {
       c2s[i]->now.swap(c2s[i]->next);
       s2c[i]->now.swap(s2c[i]->next);
+      if (params->reorder > 0) Reorder(&c2s[i]->now, &c2s[i]->next, params->reorder, turn, i);
       for (const std::string& pk : c2s[i]->now)
         sc[i]->ProcessUdpPacket(server_self, client_addr,
                                 QuicReceivedPacket(pk.data(), pk.size(), clock.Now()));
