@@ -194,6 +194,19 @@ static void FullWidthGroup() {
   EXPECT(grp.UpdateFec(ENCRYPTION_NONE, fh, std::string(30, 'z')));
   EXPECT(grp.IsFinished() && !grp.CanRevive());
   EXPECT(grp.PayloadParity().empty() && !grp.detailed_error().empty());
+  // an entry outside the uint8 group-offset range: Flush refuses the whole
+  // batch before any launch (FecPacketBody could not serialise it)
+  for (QuicPacketNumber fec_pn : {QuicPacketNumber(1 + 256), QuicPacketNumber(0)}) {
+    QuicFecEncodeBatch bad;
+    QuicFecEncodeBatch::Entry e;
+    e.fec_group = 1;
+    e.fec_packet_number = fec_pn;
+    e.group.reset(new QuicFecGroup(1));
+    EXPECT(e.group->Update(ENCRYPTION_NONE, DataHeader(1, 1), Payload(9, 1, 20)));
+    bad.Add(std::move(e));
+    EXPECT(bad.Flush(nullptr) == QFEC_ERR_INVALID_FEC_DATA);
+    EXPECT(bad.entries().back().FecPacketBody().empty());
+  }
 }
 
 static void Simulation(qfec_ctx* ctx, int conns, int packets_per_conn, double loss,
