@@ -299,16 +299,24 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // payloads.  In-place safe for dst == src + 12: slab s is stored only after
 // slab s+1 has been loaded AND the loads have completed (waitcnt), so no store
 // overtakes a load of the 12 bytes it overwrites.
-template <bool COPY, uint32_t SC, bool R3 = true, bool INPLACE = true, bool NT = false>
+// NT: 0 default cache policy, 1 nontemporal slab loads and stores, 2 stores
+// only (the NULL kernels' default: the copy's destination is not read again;
+// nt stores measured +7% / +7% (encrypt / decrypt, 2^21 packets) on one box
+// and +3% / +8% on another, profiles/round3/null_align/tune_protect_nt_store*.txt;
+// nt LOADS cost -4% / -15%: the decrypt's copy pass re-reads the ciphertext
+// the hash pass loaded.  The AEAD kernels keep default stores: nt measured
+// -3% on ChaCha20-Poly1305 seal and -0.5% on AES-GCM seal, kAeadNTS)
+constexpr int kNullNT = 2;
+template <bool COPY, uint32_t SC, bool R3 = true, bool INPLACE = true, int NT = 0>
 __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32x4* rows,
                                            uint32_t lane, uint32_t my_nfull,
                                            uint32_t my_lo = 0u) {
   const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
   u32x4 cur[SC], nxt[SC];
-  if (nslab) stage_load<SC, true, NT>(meta, lane, 0, cur);
+  if (nslab) stage_load<SC, true, NT == 1>(meta, lane, 0, cur);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
     stage_to_lds<SC>(rows, lane, cur);
-    if (sl + 1u < nslab) stage_load<SC, true, NT>(meta, lane, sl + 1u, nxt);
+    if (sl + 1u < nslab) stage_load<SC, true, NT == 1>(meta, lane, sl + 1u, nxt);
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j)
       if (sl * SC + j >= my_lo && sl * SC + j < my_nfull)
@@ -317,7 +325,7 @@ __device__ __forceinline__ void stage_hash(Fnv128& h, const StageMeta* meta, u32
       // in place: vmcnt(0), the next slab's loads are done before this slab's
       // stores overwrite them; out of place the stores go out at once
       if constexpr (INPLACE) __builtin_amdgcn_s_waitcnt(0x0F70);
-      stage_store<SC, true, NT>(meta, lane, sl, cur);
+      stage_store<SC, true, NT != 0>(meta, lane, sl, cur);
     }
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
@@ -416,7 +424,7 @@ __device__ __forceinline__ StageMeta line_meta(const uint8_t* src, uint8_t* dst,
   return StageMeta{src - 16u * lo, dst ? dst - 16u * lo : nullptr, lo + nmid, lo};
 }
 
-template <uint32_t SC, bool R3 = true, bool NT = false>
+template <uint32_t SC, bool R3 = true, int NT = kNullNT>
 __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -460,7 +468,7 @@ __global__ __launch_bounds__(kBlock) void null_encrypt_staged_kernel(ProtectArgs
   __builtin_memcpy(o, tag, kTag);
 }
 
-template <uint32_t SC, bool R3 = true, bool NT = false>
+template <uint32_t SC, bool R3 = true, int NT = kNullNT>
 __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -512,10 +520,10 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_staged_kernel(ProtectArgs
   // every slab's round trip (SQ_WAIT_ANY 0.76 of the decrypt's wave cycles).
   const uint32_t nslab = (wave_max_u32(ok ? cm.nfull : 0u) + SC - 1) / SC;
   u32x4 cur[SC], nxt[SC];
-  if (nslab) stage_load<SC, true, NT>(s_meta[wv], lane, 0, cur);
+  if (nslab) stage_load<SC, true, NT == 1>(s_meta[wv], lane, 0, cur);
   for (uint32_t sl = 0; sl < nslab; ++sl) {
-    if (sl + 1u < nslab) stage_load<SC, true, NT>(s_meta[wv], lane, sl + 1u, nxt);
-    stage_store<SC, true, NT>(s_meta[wv], lane, sl, cur);
+    if (sl + 1u < nslab) stage_load<SC, true, NT == 1>(s_meta[wv], lane, sl + 1u, nxt);
+    stage_store<SC, true, NT != 0>(s_meta[wv], lane, sl, cur);
 #pragma unroll
     for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
   }
@@ -568,7 +576,7 @@ __global__ __launch_bounds__(kBlock) void null_decrypt_onepass_kernel(ProtectArg
     fnv_bytes(h, head, 0u, sp.hd);
   }
   // output never overlaps the input (qfec.h): no in-place ordering
-  stage_hash<true, SC, R3, false>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
+  stage_hash<true, SC, R3, false, kNullNT>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
   if (!valid) return;
   const uint32_t t0 = tail_pos(sp.hd + 16u * sp.nmid, plen);
   fnv_bytes(h, tail, t0, sp.tl);
@@ -893,7 +901,9 @@ __device__ __forceinline__ ChachaKey load_key(const AeadArgs& a, uint64_t p) {
 // MAC (MAC_IN: the MAC covers the input chunks; MAC_OUT: the output chunks)
 // every full chunk; the transformed chunks leave through LDS by coalesced
 // stores when meta[].dst is set.
-template <uint32_t SC, bool XOR, bool MAC_IN, bool MAC_OUT>
+// NTS: the ciphertext / plaintext leaves by nontemporal stores (kAeadNTS)
+constexpr bool kAeadNTS = false;
+template <uint32_t SC, bool XOR, bool MAC_IN, bool MAC_OUT, bool NTS = kAeadNTS>
 __device__ __forceinline__ void aead_pass(const ChachaKey& key, Poly1305& poly,
                                           const StageMeta* meta, u32x4* rows, uint32_t lane,
                                           uint32_t my_nfull, bool store) {
@@ -936,7 +946,7 @@ __device__ __forceinline__ void aead_pass(const ChachaKey& key, Poly1305& poly,
     if (store) {
       u32x4 out[SC];
       stage_from_lds<SC>(rows, lane, out);
-      stage_store<SC>(meta, lane, sl, out);
+      stage_store<SC, true, NTS>(meta, lane, sl, out);
     }
   }
 }
@@ -945,7 +955,7 @@ __device__ __forceinline__ void poly_lengths(Poly1305& p, uint32_t ad_len, uint3
   poly_block(p, u32x4{ad_len, 0u, ct_len, 0u});  // LE64(ad_len) || LE64(ct_len)
 }
 
-template <uint32_t SC>
+template <uint32_t SC, bool NTS = kAeadNTS>
 __global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
     tail = tail_bytes(load_tail(pt, plen), plen);  // before any store (in place)
   }
   s_meta[wv][lane] = StageMeta{pt, o, plen >> 4};
-  aead_pass<SC, true, false, true>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
+  aead_pass<SC, true, false, true, NTS>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
   if (!valid) return;
   const uint32_t rem = plen & 15u;
   if (rem) {
@@ -998,7 +1008,7 @@ __global__ __launch_bounds__(kBlock) void c20p1305_seal_kernel(AeadArgs a) {
 // a packet whose tag fails keeps its unverified plaintext in the output, as
 // BoringSSL's open_impl leaves it (e_chacha20poly1305.c:142-176 decrypts
 // before it compares) — one read of the ciphertext instead of two.
-template <uint32_t SC, bool ONEPASS = false>
+template <uint32_t SC, bool ONEPASS = false, bool NTS = kAeadNTS>
 __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
   __shared__ u32x4 s_rows[kWaves][64 * (SC + 1u)];
   __shared__ StageMeta s_meta[kWaves][64];
@@ -1030,7 +1040,7 @@ __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
   if constexpr (ONEPASS) {
     uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta[wv][lane] = StageMeta{ct, o, plen >> 4};
-    aead_pass<SC, true, true, false>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
+    aead_pass<SC, true, true, false, NTS>(key, poly, s_meta[wv], s_rows[wv], lane, plen >> 4, true);
     if (!valid) return;
     const uint32_t rem = plen & 15u;
     if (rem) {
@@ -1064,8 +1074,8 @@ __global__ __launch_bounds__(kBlock) void c20p1305_open_kernel(AeadArgs a) {
   // pass 2 (verified packets only): decrypt into the output
   uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
   s_meta[wv][lane] = StageMeta{ct, o, ok ? plen >> 4 : 0u};
-  aead_pass<SC, true, false, false>(key, poly, s_meta[wv], s_rows[wv], lane, ok ? plen >> 4 : 0u,
-                                    true);
+  aead_pass<SC, true, false, false, NTS>(key, poly, s_meta[wv], s_rows[wv], lane,
+                                         ok ? plen >> 4 : 0u, true);
   const uint32_t rem = plen & 15u;
   if (ok && rem) {
     const uint32_t c = plen >> 4;
@@ -1398,7 +1408,7 @@ __device__ __forceinline__ u32x4 gcm_ctr(const uint32_t (&n)[3], uint32_t c) {
 // Payload pass (as aead_pass for ChaCha20): XOR keystream / GHASH in or out,
 // NB chunks per step (NB independent AES blocks interleaved; GHASH with
 // aggregated reduction over the step).
-template <uint32_t SC, int NB, bool XOR, bool MAC_IN, bool MAC_OUT>
+template <uint32_t SC, int NB, bool XOR, bool MAC_IN, bool MAC_OUT, bool NTS = kAeadNTS>
 __device__ __forceinline__ void gcm_pass(const AesKey& key, const uint32_t (&nonce)[3],
                                          Ghash& gh, const uint32_t* te, uint32_t copy,
                                          const StageMeta* meta, u32x4* rows, uint32_t lane,
@@ -1435,7 +1445,7 @@ __device__ __forceinline__ void gcm_pass(const AesKey& key, const uint32_t (&non
     if (store) {
       u32x4 out[SC];
       stage_from_lds<SC>(rows, lane, out);
-      stage_store<SC>(meta, lane, sl, out);
+      stage_store<SC, true, NTS>(meta, lane, sl, out);
     }
   }
 }
@@ -1479,7 +1489,7 @@ constexpr int kGcmNB = 4;   // chunks per step of the payload passes
 // Everything after the key setup, for one packet per lane.  Instantiated
 // twice in the kernel when UNI: with the key-uniform wave's round keys as
 // wave-uniform values (SGPRs, 44 VGPRs freed) and with per-lane keys.
-template <uint32_t SC, bool OPEN, int NB, bool ONEPASS = false>
+template <uint32_t SC, bool OPEN, int NB, bool ONEPASS = false, bool NTS = kAeadNTS>
 __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
                                            const uint32_t (&nonce)[3], Ghash& gh,
                                            const uint32_t* s_te, uint32_t copy, StageMeta* meta,
@@ -1498,7 +1508,7 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
   if constexpr (!OPEN) {
     uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta_w[lane] = StageMeta{in, o, plen >> 4};
-    gcm_pass<SC, NB, true, false, true>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+    gcm_pass<SC, NB, true, false, true, NTS>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
                                     plen >> 4, true);
     if (!valid) return;
     if (rem) {
@@ -1524,7 +1534,7 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
     if (valid) __builtin_memcpy(want, in + plen, kTag);
     uint8_t* o = valid ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta_w[lane] = StageMeta{in, o, plen >> 4};
-    gcm_pass<SC, NB, true, true, false>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+    gcm_pass<SC, NB, true, true, false, NTS>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
                                     plen >> 4, true);
     if (!valid) return;
     if (rem) {
@@ -1557,7 +1567,7 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
     }
     uint8_t* o = ok ? a.io.out + a.io.out_off[p] : nullptr;
     s_meta_w[lane] = StageMeta{in, o, ok ? plen >> 4 : 0u};
-    gcm_pass<SC, NB, true, false, false>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
+    gcm_pass<SC, NB, true, false, false, NTS>(key, nonce, gh, s_te, copy, s_meta_w, s_rows_w, lane,
                                      ok ? plen >> 4 : 0u, true);
     if (ok && rem) {
       const u32x4 pt = tail ^ aes_encrypt(key, gcm_ctr(nonce, ctail), s_te, copy);
@@ -1569,7 +1579,7 @@ __device__ __forceinline__ void gcm_packet(const AeadArgs& a, const AesKey& key,
 }
 
 template <uint32_t SC, bool OPEN, int NB = kGcmNB, int BLOCK = kGcmBlock, int WPE = kGcmWPE,
-          bool UNI = true, bool ONEPASS = false>
+          bool UNI = true, bool ONEPASS = false, bool NTS = kAeadNTS>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
 aes128gcm_kernel(AeadArgs a) {
   constexpr int kGcmWaves = BLOCK / 64;
@@ -1645,11 +1655,11 @@ aes128gcm_kernel(AeadArgs a) {
     AesKey ks;  // the wave's key as uniform values
 #pragma unroll
     for (int i = 0; i < 44; ++i) ks.rk[i] = (uint32_t)__builtin_amdgcn_readlane((int)key.rk[i], src);
-    gcm_packet<SC, OPEN, NB, ONEPASS>(a, ks, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
-                                      p, valid, ad, in, alen, plen);
+    gcm_packet<SC, OPEN, NB, ONEPASS, NTS>(a, ks, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv],
+                                           lane, p, valid, ad, in, alen, plen);
   } else {
-    gcm_packet<SC, OPEN, NB, ONEPASS>(a, key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv], lane,
-                                      p, valid, ad, in, alen, plen);
+    gcm_packet<SC, OPEN, NB, ONEPASS, NTS>(a, key, nonce, gh, s_te, copy, s_meta[wv], s_rows[wv],
+                                           lane, p, valid, ad, in, alen, plen);
   }
 }
 

@@ -594,6 +594,21 @@ int main(int argc, char** argv) {
       {"null decrypt staged (product)", dec_b, hashed, [&] { CK(qfec::launch_null_protect(d, true, 0)); }},
       {"chacha20poly1305 seal (product)", enc_b, hashed, [&] { CK(qfec::launch_chacha20poly1305(as, false, 0)); }},
       {"chacha20poly1305 open (product)", dec_b, hashed, [&] { CK(qfec::launch_chacha20poly1305(ao, true, 0)); }},
+      {"chacha seal NT stores", enc_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::c20p1305_seal_kernel<16, true>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
+      {"chacha open NT stores", dec_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::c20p1305_open_kernel<16, false, true>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, ao); }},
+      {"chacha20poly1305 seal (product) again", enc_b, hashed, [&] { CK(qfec::launch_chacha20poly1305(as, false, 0)); }},
+      {"chacha seal NT stores again", enc_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::c20p1305_seal_kernel<16, true>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
+      {"aes128gcm seal (product)", enc_b, hashed, [&] { CK(qfec::launch_aes128gcm(as, false, 0)); }},
+      {"aes128gcm seal NT stores", enc_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::aes128gcm_kernel<8, false, qfec::kGcmNB, 512, 2, true, false, true>),
+                            dim3((uint32_t)((n + 511) / 512)), dim3(512), 0, 0, as); }},
+      {"aes128gcm seal (product) again", enc_b, hashed, [&] { CK(qfec::launch_aes128gcm(as, false, 0)); }},
+      {"aes128gcm seal NT stores again", enc_b, hashed, [&] {
+         hipLaunchKernelGGL((qfec::aes128gcm_kernel<8, false, qfec::kGcmNB, 512, 2, true, false, true>),
+                            dim3((uint32_t)((n + 511) / 512)), dim3(512), 0, 0, as); }},
       {"chacha20poly1305 seal SC=16", enc_b, hashed, [&] {
          hipLaunchKernelGGL(qfec::c20p1305_seal_kernel<16>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, as); }},
       {"chacha20poly1305 open SC=16", dec_b, hashed, [&] {
@@ -640,8 +655,10 @@ int main(int argc, char** argv) {
       {"ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
       {"ALIGNED glds SC=8 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
       {"ALIGNED glds SC=8 NB=3", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, ea); }},
-      {"nt staged enc SC=16", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, e); }},
-      {"nt staged dec SC=16", dec_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, true, true>), dim3(sblocks), dim3(256), 0, 0, d); }},
+      {"nt staged enc SC=16", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, true, 1>), dim3(sblocks), dim3(256), 0, 0, e); }},
+      {"default-store staged enc SC=16", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<16, true, 0>), dim3(sblocks), dim3(256), 0, 0, e); }},
+      {"nt staged dec SC=16", dec_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, true, 1>), dim3(sblocks), dim3(256), 0, 0, d); }},
+      {"default-store staged dec SC=16", dec_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_decrypt_staged_kernel<16, true, 0>), dim3(sblocks), dim3(256), 0, 0, d); }},
       {"SRC128-DST48 staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eC, false, 0)); }},
       {"SRC-ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(eA, false, 0)); }},
       {"SRC-ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eA); }},
