@@ -886,15 +886,25 @@ def bench_protect(ctx, torch, dev, stream, G, k, L, hdr=22, reps=5, cpu=True):
                "seal_payload_GBps": round(n * L / (ms_gs / 1e3) / 1e9, 1),
                "seal_us": round(ms_gs * 1e3, 1), "open_us": round(ms_go * 1e3, 1),
                "verified": verified_g}}
+    def targs(k):  # the kernel's template arguments
+        return [x.strip() for x in k.split("<", 1)[1].rsplit(">", 1)[0].split(",")] if "<" in k else []
+
+    def gcm(open_, onepass):
+        return lambda k: ("aes128gcm_kernel" in k and targs(k)[1] == ("true" if open_ else "false")
+                          and (len(targs(k)) > 6 and targs(k)[6] == "true") == onepass)
+
     res["issue_bound"] = {
-        "null_encrypt": _issue_bound(lambda k: "null_encrypt" in k, n, ms_e),
-        "null_decrypt": _issue_bound(lambda k: "null_decrypt" in k, n, ms_d),
+        "null_encrypt": _issue_bound(lambda k: "null_encrypt_staged" in k, n, ms_e),
+        "null_decrypt": _issue_bound(lambda k: "null_decrypt_staged" in k, n, ms_d),
+        "null_decrypt_scratch_out": _issue_bound(lambda k: "null_decrypt_onepass" in k, n, ms_d1),
         "chacha20poly1305_seal": _issue_bound(lambda k: "c20p1305_seal" in k, n, ms_cs),
-        "chacha20poly1305_open": _issue_bound(lambda k: "c20p1305_open" in k, n, ms_co),
-        "aes128gcm_seal": _issue_bound(lambda k: "aes128gcm_kernel" in k and ", false," in k, n,
-                                       ms_gs),
-        "aes128gcm_open": _issue_bound(lambda k: "aes128gcm_kernel" in k and ", true," in k, n,
-                                       ms_go),
+        "chacha20poly1305_open": _issue_bound(
+            lambda k: "c20p1305_open" in k and targs(k)[1:2] != ["true"], n, ms_co),
+        "chacha20poly1305_open_scratch_out": _issue_bound(
+            lambda k: "c20p1305_open" in k and targs(k)[1:2] == ["true"], n, ms_co1),
+        "aes128gcm_seal": _issue_bound(gcm(False, False), n, ms_gs),
+        "aes128gcm_open": _issue_bound(gcm(True, False), n, ms_go),
+        "aes128gcm_open_scratch_out": _issue_bound(gcm(True, True), n, ms_go1),
         "note": "fraction of kernel time the VALU / LDS / scalar units were busy (PMC)"}
     del cat, dout, data
     torch.cuda.empty_cache()
