@@ -427,6 +427,85 @@ __global__ __launch_bounds__(64) void null_encrypt_glds2_kernel(ProtectArgs a) {
   __builtin_memcpy(o, tag, kTag);
 }
 
+// Unpadded, XOR-swizzled staging rows (64 x SC x 16 B per wave instead of
+// 64 x (SC + 1) x 16 B): slot j of packet P's row at P*SC + (j ^ swz(P)),
+// conflict-free for the hashing lanes' ds_read_b128 (as the LDS-DMA kernel's
+// source swizzle).  With SC = 8 the block needs 38 KiB: 4 blocks per CU.
+template <uint32_t SC>
+__device__ __forceinline__ void stage_to_lds_swz(u32x4* rows, uint32_t lane, const u32x4 (&v)[SC]) {
+  const uint32_t i = lane / SC, m = lane % SC;
+  wave_lds_order();
+#pragma unroll
+  for (uint32_t I = 0; I < SC; ++I) {
+    const uint32_t P = (64u / SC) * I + i;
+    rows[P * SC + (m ^ glds_swz<SC>(P))] = v[I];
+  }
+  wave_lds_order();
+}
+
+template <uint32_t SC, int NT, bool INPLACE>
+__device__ __forceinline__ void stage_hash_swz(Fnv128& h, const StageMeta* meta, u32x4* rows,
+                                               uint32_t lane, uint32_t my_nfull, uint32_t my_lo) {
+  const uint32_t nslab = (wave_max_u32(my_nfull) + SC - 1) / SC;
+  const uint32_t sw = glds_swz<SC>(lane);
+  u32x4 cur[SC], nxt[SC];
+  if (nslab) stage_load<SC, true, NT == 1>(meta, lane, 0, cur);
+  for (uint32_t sl = 0; sl < nslab; ++sl) {
+    stage_to_lds_swz<SC>(rows, lane, cur);
+    if (sl + 1u < nslab) stage_load<SC, true, NT == 1>(meta, lane, sl + 1u, nxt);
+#pragma unroll
+    for (uint32_t j = 0; j < SC; ++j)
+      if (sl * SC + j >= my_lo && sl * SC + j < my_nfull)
+        fnv_chunk<true>(h, rows[lane * SC + (j ^ sw)]);
+    if constexpr (INPLACE) __builtin_amdgcn_s_waitcnt(0x0F70);
+    stage_store<SC, true, NT != 0>(meta, lane, sl, cur);
+#pragma unroll
+    for (uint32_t j = 0; j < SC; ++j) cur[j] = nxt[j];
+  }
+}
+
+template <uint32_t SC, int MINB>
+__global__ __launch_bounds__(kBlock, MINB) void null_encrypt_swz_kernel(ProtectArgs a) {
+  __shared__ u32x4 s_rows[kWaves][64 * SC];
+  __shared__ StageMeta s_meta[kWaves][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = p < a.n;
+  const uint8_t* ad = nullptr;
+  const uint8_t* pt = nullptr;
+  uint8_t* o = nullptr;
+  uint32_t alen = 0, plen = 0;
+  if (valid) {
+    ad = a.bytes + a.ad_off[p];
+    pt = a.bytes + a.in_off[p];
+    alen = a.ad_len[p];
+    plen = a.in_len[p];
+    o = a.out + a.out_off[p];
+  }
+  const DstSplit sp = dst_split(o + kTag, plen);
+  const StageMeta m = line_meta(pt + sp.hd, o + kTag + sp.hd, sp.nmid, o + kTag + sp.hd);
+  s_meta[wv][lane] = m;
+  const u32x4 head = valid ? load_head(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  const u32x4 tail = valid ? load_tail(pt, plen) : u32x4{0u, 0u, 0u, 0u};
+  Fnv128 h = fnv_init();
+  if (valid) {
+    fnv_span<true>(h, ad, alen);
+    fnv_bytes(h, head, 0u, sp.hd);
+  }
+  const bool overlap = valid && o + kTag < pt + plen && pt < o + kTag + plen;
+  if (wave_any_qpp(overlap))
+    stage_hash_swz<SC, kNullNT, true>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
+  else
+    stage_hash_swz<SC, kNullNT, false>(h, s_meta[wv], s_rows[wv], lane, m.nfull, m.lo);
+  if (!valid) return;
+  const uint32_t t0 = tail_pos(sp.hd + 16u * sp.nmid, plen);
+  fnv_bytes(h, tail, t0, sp.tl);
+  store_from_aligned_start(o + kTag + sp.hd + 16u * sp.nmid, tail, t0, sp.tl);
+  store_to_aligned_end(o + kTag, head, 0u, sp.hd);
+  const uint32_t tag[3] = {h.x0, h.x1, h.x2};
+  __builtin_memcpy(o, tag, kTag);
+}
+
 }  // namespace
 }  // namespace qfec
 
@@ -536,6 +615,9 @@ int main(int argc, char** argv) {
       {"glds2 SC=16 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
       {"glds2 SC=8 NB=2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<8, 2>), dim3(gblocks), dim3(64), 0, 0, eg); }},
       {"glds2 SC=8 NB=3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds2_kernel<8, 3>), dim3(gblocks), dim3(64), 0, 0, eg); }},
+      {"swz SC=8 x4", [&] { hipLaunchKernelGGL((qfec::null_encrypt_swz_kernel<8, 4>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, eg); }},
+      {"swz SC=8 x3", [&] { hipLaunchKernelGGL((qfec::null_encrypt_swz_kernel<8, 3>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, eg); }},
+      {"swz SC=16 x2", [&] { hipLaunchKernelGGL((qfec::null_encrypt_swz_kernel<16, 2>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, eg); }},
   };
   {
     std::vector<uint8_t> ref(n * (L + 12)), got(n * (L + 12));
@@ -650,6 +732,11 @@ int main(int argc, char** argv) {
       {"glds2 SC=16 NB=2", enc_b, hashed, glds[5].second},
       {"glds2 SC=8 NB=2", enc_b, hashed, glds[6].second},
       {"glds2 SC=8 NB=3", enc_b, hashed, glds[7].second},
+      {"swz SC=8 x4", enc_b, hashed, glds[8].second},
+      {"swz SC=8 x3", enc_b, hashed, glds[9].second},
+      {"swz SC=16 x2", enc_b, hashed, glds[10].second},
+      {"null encrypt (product) again", enc_b, hashed, [&] { CK(qfec::launch_null_protect(e, false, 0)); }},
+      {"swz SC=8 x4 again", enc_b, hashed, glds[8].second},
       {"ALIGNED staged (product)", enc_b, hashed, [&] { CK(qfec::launch_null_protect(ea, false, 0)); }},
       {"ALIGNED staged SC=8", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_staged_kernel<8>), dim3(sblocks), dim3(256), 0, 0, ea); }},
       {"ALIGNED glds SC=16 NB=2", enc_b, hashed, [&] { hipLaunchKernelGGL((qfec::null_encrypt_glds_kernel<16, 2>), dim3(gblocks), dim3(64), 0, 0, ea); }},
