@@ -579,10 +579,10 @@ def main(argv=None):
         if line["roofline"]:  # the encode kernel against this box's measured streaming read
             line["ceilings"]["encode_frac_of_read_ceiling"] = round(
                 line["roofline"]["achieved"] / line["ceilings"]["read_GBps"], 4)
-    # The CPU baseline: rank 0 only, after every rank's timed region (the other
-    # ranks wait at the final barrier), over rank 0's shard of the same workload.
+    # The CPU baseline: rank 0 at N=1 only, after the timed region, over the
+    # same workload (an N>1 line carries cpu_baseline null: the N=1 line has it).
     host_rows = None
-    if rank == 0 and not args.no_cpu_baseline and not args.profile_only:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
         host_rows = work.host_rows()
     if extras:
         work.release()
