@@ -92,6 +92,10 @@ int main(int argc, char** argv) {
   const uint32_t kmin = argc > 3 ? atoi(argv[3]) : 5, kspan = argc > 4 ? atoi(argv[4]) : 11;
   const uint32_t lmin = argc > 5 ? atoi(argv[5]) : 64, lspan = argc > 6 ? atoi(argv[6]) : 1287;
   const bool packed_out = argc > 7 && atoi(argv[7]) != 0;
+  // parity / revived slot stride when not packed (1452: kMaxPacketSize; 1472:
+  // an ALIGNAS(64) char[kMaxPacketSize] slot; 1536: 128-B lines)
+  const uint64_t slot = argc > 8 ? (uint64_t)atoi(argv[8]) : 1452u;
+  const uint64_t SB = 1536;  // buffer bytes per group (any slot <= 1536)
   uint64_t out_pos = 0;
   const uint64_t seed = 0x51554944;
   std::vector<uint32_t> ptr{0};
@@ -117,7 +121,7 @@ int main(int argc, char** argv) {
     enc_alg += s + mx;
     rec_alg += sm + 2.0 * mx;
     ptr.push_back((uint32_t)len.size());
-    poff[g] = packed_out ? out_pos : g * 1452;
+    poff[g] = packed_out ? out_pos : g * slot;
     out_pos += mx;
   }
   uint8_t* data;
@@ -131,14 +135,14 @@ int main(int argc, char** argv) {
   uint8_t *par, *out, *chk;
   uint16_t *plen, *plen2;
   uint32_t* err;
-  CK(hipMalloc(&par, G * 1452));
-  CK(hipMalloc(&out, G * 1452));
-  CK(hipMalloc(&chk, G * 1452));
+  CK(hipMalloc(&par, G * SB));
+  CK(hipMalloc(&out, G * SB));
+  CK(hipMalloc(&chk, G * SB));
   CK(hipMalloc(&plen, G * 2));
   CK(hipMalloc(&plen2, G * 2));
   CK(hipMalloc(&err, 4));
   CK(hipMemset(err, 0, 4));
-  CK(hipMemset(par, 0, G * 1452));
+  CK(hipMemset(par, 0, G * SB));
   CK(hipDeviceSynchronize());
 
   RaggedArgs e{};
@@ -168,6 +172,7 @@ int main(int argc, char** argv) {
     std::string name;
     bool rec;
     std::function<void(const RaggedArgs&)> run;
+    uint64_t stride = 0;  // != 0: output in slots of this stride (checked per group)
   };
   std::vector<V> vs;
   vs.push_back({"multi2 encode", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
@@ -180,6 +185,19 @@ int main(int argc, char** argv) {
                                      dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0,       \
                                      0xA5A5F00Du);                                             \
                 }})
+  if (getenv("TUNE_RW_SPLIT")) {  // round 3: where the store tail's cost goes
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_DIAG(false, 0, "diag0 product");
+      RG_DIAG(false, 1, "diag1 nostore (not exact)");
+      RG_DIAG(false, 11, "diag11 lds reads only (not exact)");
+      RG_DIAG(false, 12, "diag12 stores only (not exact)");
+      RG_DIAG(false, 2, "diag2 L2 store (not exact)");
+    }
+    RG_DIAG(true, 0, "diag0 product");
+    RG_DIAG(true, 1, "diag1 nostore (not exact)");
+    RG_DIAG(true, 11, "diag11 lds reads only (not exact)");
+    RG_DIAG(true, 12, "diag12 stores only (not exact)");
+  }
   if (getenv("TUNE_RW_DAL")) {  // round 3: destination-aligned stores, A/B twice each
     RG_DIAG(false, 0, "diag0 product");
     RG_DIAG(false, 10, "diag10 dst-aligned");
@@ -220,7 +238,82 @@ int main(int argc, char** argv) {
     RG_DIAG(true, 5, "diag5 xcd+wb");
   }
 #undef RG_DIAG
-  const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr || getenv("TUNE_RW_DAL") != nullptr;
+  // persistent waves over pairs (ragged_persist_kernel): a fresh zeroed
+  // counter word per launch
+  uint32_t* pctr;
+  const uint32_t n_pctr = 1u << 16;
+  CK(hipMalloc(&pctr, n_pctr * 4ull));
+  CK(hipMemset(pctr, 0, n_pctr * 4ull));
+  static uint32_t pctr_next = 0;
+  int ncu0 = 0;
+  CK(hipDeviceGetAttribute(&ncu0, hipDeviceAttributeMultiprocessorCount, 0));
+#define RG_PERSIST(REC, DYN, BPC, NAME)                                                         \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  if (pctr_next >= n_pctr) {                                                   \
+                    std::fprintf(stderr, "out of counter words\n");                           \
+                    std::exit(1);                                                              \
+                  }                                                                            \
+                  hipLaunchKernelGGL((qfec::ragged_persist_kernel<REC, DYN>),                  \
+                                     dim3((uint32_t)(ncu0 * BPC)), dim3(256), 0, 0, a0,        \
+                                     pctr + pctr_next++);                                      \
+                }})
+  if (getenv("TUNE_RW_PERSIST")) {
+    RG_PERSIST(false, false, 8, "persist static x8");
+    RG_PERSIST(false, true, 8, "persist dyn x8");
+    vs.push_back({"multi2 encode (again)", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+    RG_PERSIST(false, true, 8, "persist dyn x8 (again)");
+    RG_PERSIST(false, true, 7, "persist dyn x7");
+    vs.push_back({"multi2 recover", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_PERSIST(true, false, 8, "persist static x8");
+    RG_PERSIST(true, true, 8, "persist dyn x8");
+    vs.push_back({"multi2 recover (again)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_PERSIST(true, true, 8, "persist dyn x8 (again)");
+  }
+#undef RG_PERSIST
+  // parity / revived slot strides in ONE process (the placement of the
+  // buffers is per process): 1452, 1472 (ALIGNAS(64) char[kMaxPacketSize]),
+  // 1536 (128-B lines), each twice
+  if (getenv("TUNE_RW_SLOT")) {
+    const uint64_t strides[3] = {1452, 1472, 1536};
+    for (int rep = 0; rep < 2; ++rep)
+      for (int rec = 0; rec < 2; ++rec)
+        for (uint64_t st : strides) {
+          std::vector<uint64_t> ps(G);
+          for (uint64_t g = 0; g < G; ++g) ps[g] = g * st;
+          uint64_t* d_ps = up(ps);
+          uint8_t* par_s = nullptr;
+          if (rec) {  // the parity in this stride's slots
+            CK(hipMalloc(&par_s, G * SB));
+            RaggedArgs es = e;
+            es.out = par_s;
+            es.parity_off = d_ps;
+            es.parity_len_out = plen2;
+            launch_multi<false, 2>(es, G);
+            CK(hipDeviceSynchronize());
+          }
+          V v;
+          v.name = "slot " + std::to_string(st) + (rec ? " recover" : " encode") + (rep ? " (again)" : "");
+          v.rec = rec != 0;
+          v.stride = st;
+          v.run = [=](const RaggedArgs& a0) {
+            RaggedArgs a = a0;
+            a.parity_off = d_ps;
+            if (rec) {
+              a.parity = par_s;
+              a.out_off = d_ps;
+            }
+            if (rec)
+              launch_multi<true, 2>(a, G);
+            else
+              launch_multi<false, 2>(a, G);
+          };
+          vs.push_back(v);
+        }
+  }
+  const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr || getenv("TUNE_RW_DAL") != nullptr ||
+                         getenv("TUNE_RW_PERSIST") != nullptr || getenv("TUNE_RW_SLOT") != nullptr ||
+                         getenv("TUNE_RW_SPLIT") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
@@ -268,13 +361,13 @@ int main(int argc, char** argv) {
 #undef RG_PHASE
 
   // correctness: each variant's output (and parity lengths) == the product's
-  std::vector<uint8_t> want_e(G * 1452), want_r(G * 1452), got(G * 1452);
+  std::vector<uint8_t> want_e(G * SB), want_r(G * SB), got(G * SB);
   std::vector<uint16_t> want_pl(G), got_pl(G);
-  CK(hipMemcpy(want_e.data(), par, G * 1452, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(want_e.data(), par, G * SB, hipMemcpyDeviceToHost));
   CK(hipMemcpy(want_pl.data(), plen, G * 2, hipMemcpyDeviceToHost));
-  CK(hipMemset(out, 0, G * 1452));
+  CK(hipMemset(out, 0, G * SB));
   launch_multi<true, 2>(r, G);
-  CK(hipMemcpy(want_r.data(), out, G * 1452, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(want_r.data(), out, G * SB, hipMemcpyDeviceToHost));
   {  // the product against a host XOR on a sample
     std::vector<uint8_t> h(bytes);
     CK(hipMemcpy(h.data(), data, bytes, hipMemcpyDeviceToHost));
@@ -300,13 +393,20 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(hdat.data(), data, bytes, hipMemcpyDeviceToHost));
   bool all_ok = true;  // the d8 builds are KNOWN to differ: they do not fail the run
   for (auto& v : vs) {
-    CK(hipMemset(out, 0, G * 1452));
+    CK(hipMemset(out, 0, G * SB));
     CK(hipMemset(plen2, 0, G * 2));
     std::printf("check %s ...\n", v.name.c_str());
     v.run(v.rec ? r : e2);
     CK(hipDeviceSynchronize());
-    CK(hipMemcpy(got.data(), out, G * 1452, hipMemcpyDeviceToHost));
-    bool same = got == (v.rec ? want_r : want_e);
+    CK(hipMemcpy(got.data(), out, G * SB, hipMemcpyDeviceToHost));
+    bool same = true;
+    if (v.stride) {
+      const std::vector<uint8_t>& want = v.rec ? want_r : want_e;
+      for (uint64_t g = 0; g < G && same; ++g)
+        same = std::memcmp(&got[g * v.stride], &want[poff[g]], want_pl[g]) == 0;
+    } else {
+      same = got == (v.rec ? want_r : want_e);
+    }
     if (!v.rec) {
       CK(hipMemcpy(got_pl.data(), plen2, G * 2, hipMemcpyDeviceToHost));
       same = same && got_pl == want_pl;
@@ -314,17 +414,17 @@ int main(int argc, char** argv) {
     uint32_t he;
     CK(hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost));
     std::printf("%-24s == multi2: %s (err %u)\n", v.name.c_str(), same ? "yes" : "NO", he);
-    if (!same && v.name.find("not exact") == std::string::npos) {  // which groups, and where in them
+    if (!same && !v.stride && v.name.find("not exact") == std::string::npos) {  // which groups, and where in them
       const std::vector<uint8_t>& want = v.rec ? want_r : want_e;
       uint64_t nbad = 0;
       for (uint64_t g = 0; g < G; ++g) {
-        const uint8_t* x = &got[g * 1452];
-        const uint8_t* y = &want[g * 1452];
-        if (std::memcmp(x, y, 1452) == 0) continue;
+        const uint8_t* x = &got[poff[g]];
+        const uint8_t* y = &want[poff[g]];
+        if (std::memcmp(x, y, want_pl[g]) == 0) continue;
         if (nbad++ < 4) {
           uint32_t j0 = 0, j1 = 0, W = 0;
           while (x[j0] == y[j0]) ++j0;
-          j1 = 1451;
+          j1 = want_pl[g] - 1;
           while (x[j1] == y[j1]) --j1;
           for (uint32_t p = ptr[g]; p < ptr[g + 1]; ++p)
             if (!v.rec || p - ptr[g] != miss[g]) W += (len[p] + 15) / 16;
@@ -376,8 +476,9 @@ int main(int argc, char** argv) {
       res[i].push_back((vs[i].rec ? rec_alg : enc_alg) / (ms / reps * 1e-3) / 1e9);
     }
   }
-  std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packets\n", kmin, kmin + kspan - 1,
-              lmin, lmin + lspan - 1, (unsigned long long)G, bytes / 1e9);
+  std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packets, parity slots %s %llu\n", kmin,
+              kmin + kspan - 1, lmin, lmin + lspan - 1, (unsigned long long)G, bytes / 1e9,
+              packed_out ? "packed" : "stride", (unsigned long long)(packed_out ? 0 : slot));
   std::printf("%-24s %10s %10s %8s\n", "variant", "med GB/s", "max GB/s", "%8TB/s");
   for (size_t i = 0; i < vs.size(); ++i) {
     auto v = res[i];
