@@ -241,7 +241,7 @@ int main(int argc, char** argv) {
   // persistent waves over pairs (ragged_persist_kernel): a fresh zeroed
   // counter word per launch
   uint32_t* pctr;
-  const uint32_t n_pctr = 1u << 16;
+  const uint32_t n_pctr = 1u << 20;
   CK(hipMalloc(&pctr, n_pctr * 4ull));
   CK(hipMemset(pctr, 0, n_pctr * 4ull));
   static uint32_t pctr_next = 0;
@@ -270,6 +270,31 @@ int main(int argc, char** argv) {
     vs.push_back({"multi2 recover (again)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
     RG_PERSIST(true, true, 8, "persist dyn x8 (again)");
   }
+#define RG_PXCD(REC, C, BPC, NAME)                                                             \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  if (pctr_next + 512u > n_pctr) {                                             \
+                    std::fprintf(stderr, "out of counter words\n");                          \
+                    std::exit(1);                                                              \
+                  }                                                                            \
+                  hipLaunchKernelGGL((qfec::ragged_persist_xcd_kernel<REC, C>),                \
+                                     dim3((uint32_t)(ncu0 * BPC)), dim3(256), 0, 0, a0,        \
+                                     pctr + pctr_next);                                        \
+                  pctr_next += 512u;                                                           \
+                }})
+  if (getenv("TUNE_RW_PERSIST2")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 encode (ref)", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+      RG_PXCD(false, 1, 8, "pxcd C1 x8");
+      RG_PXCD(false, 2, 8, "pxcd C2 x8");
+      RG_PXCD(false, 4, 8, "pxcd C4 x8");
+      RG_PXCD(false, 2, 7, "pxcd C2 x7");
+    }
+    vs.push_back({"multi2 recover (ref)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_PXCD(true, 2, 8, "pxcd C2 x8");
+    RG_PXCD(true, 4, 8, "pxcd C4 x8");
+  }
+#undef RG_PXCD
 #undef RG_PERSIST
   // parity / revived slot strides in ONE process (the placement of the
   // buffers is per process): 1452, 1472 (ALIGNAS(64) char[kMaxPacketSize]),
@@ -313,7 +338,8 @@ int main(int argc, char** argv) {
   }
   const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr || getenv("TUNE_RW_DAL") != nullptr ||
                          getenv("TUNE_RW_PERSIST") != nullptr || getenv("TUNE_RW_SLOT") != nullptr ||
-                         getenv("TUNE_RW_SPLIT") != nullptr;
+                         getenv("TUNE_RW_SPLIT") != nullptr ||
+                         getenv("TUNE_RW_PERSIST2") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
