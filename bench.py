@@ -723,7 +723,7 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
             "recover_frac": round(b_rec / rec / 1e9 / HBM_PEAK_GBS, 4),
             "encode_us": round(enc * 1e6, 1), "recover_us": round(rec * 1e6, 1),
             "hbm_traffic_over_algorithmic": traffic, "verified": bool(ok),
-            "kernel": "ragged_multi_kernel<RECOVER, true, 2>"}
+            "kernel": "ragged_block_kernel<RECOVER, 4, 8> (4 waves x 8 groups per block, one flat window space)"}
 
 
 def _time_on(torch, stream, fn, reps):

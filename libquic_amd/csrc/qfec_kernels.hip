@@ -26,10 +26,12 @@
 //    phase_xor_kernel instead: the same lanes and loads in a persistent
 //    one-workgroup-per-CU grid that separates the row reads and the parity
 //    writes into grid-wide phases (0.80 of 8 TB/s on any buffer placement).
-//  * Ragged CSR batches: two groups per wave (ragged_multi_kernel; the
-//    one-group body below is its exact fallback), lanes own 16-byte windows of the
-//    parity; a packet shorter than the window is loaded as the 16 bytes that
-//    end at its last byte and shifted down (zero fill), so again no load leaves
+//  * Ragged CSR batches: eight groups per 4-wave block in one flat window
+//    space (ragged_block_kernel; the one-group body below is its exact
+//    fallback; ragged_multi_kernel, two groups per wave, is the round-2 form
+//    kept for the A/B record), lanes own 16-byte windows of the packets; a
+//    window shorter than 16 bytes is loaded as the 16 bytes that end at the
+//    packet's last byte and shifted down (zero fill), so again no load leaves
 //    the packet.
 #include "qfec_internal.h"
 
@@ -889,7 +891,8 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
   ragged_group<RECOVER, NT, U, ACC, BF>(a, g, lane, f, s_par[wv], s_head[wv], s_meta[wv]);
 }
 
-// Two groups per wave (the launch_ragged default): GPW consecutive groups in
+// Two groups per wave (launch_ragged's round-2 kernel, now ragged_block_kernel
+// below; kept as the A/B reference of tools/tune): GPW consecutive groups in
 // ONE flat window space — their received packets fill the 64-lane packet
 // table together — so the per-group load chain (group pointer -> packet table
 // -> packet bytes), which parks the one-group waves for 70% of their cycles
@@ -1128,6 +1131,234 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) 
                                                 pl, doff))
     ragged_pair_store<NT, GPW>(a, ng, lane, s_par[wv], pl, doff);
 }
+
+// Ragged CSR, large batches — the PRODUCT kernel (launch_ragged), round 3:
+// BLOCK-flat windows.  A short-lived block of WAVES waves owns GPB consecutive
+// groups and numbers the 16-B windows of ALL their received packets
+// consecutively (the flat-window mapping of ragged_group, widened from one
+// wave to the block); lane tid of iteration i takes window NT i + tid
+// (NT = 64 WAVES), so one block instruction reads NT/4 KiB of the batch, in
+// batch order.  Why: without its parity stores ragged_multi_kernel (each wave
+// its own pair of groups, the waves 14 KB apart) read its packets at
+// 5.56 TB/s, where 16 waves streaming one chunk (the chunk-phased experiment)
+// read at ~6.3 TB/s — fewer, wider streams.  4 waves x 8 groups measured
+// +2.5% encode / +4.5% recover over ragged_multi_kernel on three boxes;
+// 2 x 4, 2 x 6, 4 x 6, 4 x 10, 4 x 12 less, 8 x 16 and 16 x 32 slower (block
+// barriers), U = 1 / 3 no better (profiles/round3/ragged_block/, DESIGN.md
+// §4).  One pass of setup per block: the group scalars (wave 0), one
+// received packet per lane, a block scan for each packet's first window S, a
+// start bitmask and per 64-window block the number of packets starting
+// before it (a second block scan).  Blocks that do not fit (more than NT
+// received packets or CAPW windows, a packet below 16 B, any invalid field)
+// run the per-group body, one wave per group, so outputs and error bits are
+// exactly those of the per-group kernel.  Encode parity lengths come from an
+// LDS atomicMax.
+template <int WAVES>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, uint32_t wv,
+                                                    uint32_t* s_w, uint32_t& total) {
+  const uint32_t incl = wave_incl_scan(x, lane);
+  if (lane == 63u) s_w[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < WAVES; ++w) {
+    const uint32_t v = s_w[w];
+    base += (uint32_t)w < wv ? v : 0u;
+    tot += v;
+  }
+  total = tot;
+  __syncthreads();  // s_w free again
+  return base + incl - x;
+}
+
+// PF (recover): the parity windows are loaded into the accumulators before the
+// packet table, so their round trip overlaps the table's (measured equal to
+// loading them after the scan, profiles/round3/ragged_block/block3.txt).
+template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true>
+__global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
+  static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
+  constexpr uint32_t NT = 64u * WAVES;
+  constexpr uint32_t NBLK = NT;        // 64-window blocks: CAPW = 64 NT windows
+  constexpr uint32_t CAPW = 64u * NBLK;
+  // per-wave fallback scratch (ragged_group): accumulator, start mask, table
+  constexpr uint32_t kFbWords = 4u * kParWin + 2u * kParWin + 4u * 64u;
+  constexpr uint32_t kMainWords = GPB * kAccWords + 4u * NT;  // accumulators + packet table
+  constexpr uint32_t kRawWords = kMainWords > WAVES * kFbWords ? kMainWords : WAVES * kFbWords;
+  __shared__ uint32_t s_raw[kRawWords];
+  __shared__ uint64_t s_head[NBLK];
+  __shared__ uint32_t s_cnt[NBLK];
+  __shared__ uint32_t s_rb[GPB + 1], s_kb[GPB], s_m[GPB], s_pl[GPB], s_ob[GPB + 1];
+  __shared__ uint64_t s_doff[GPB], s_poff[GPB];
+  __shared__ uint32_t s_w[WAVES], s_fit;
+  uint32_t* acc = s_raw;
+  u32x4* pk = reinterpret_cast<u32x4*>(s_raw + GPB * kAccWords);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t g0 = (uint64_t)blockIdx.x * GPB;
+  if (g0 >= a.n_groups) return;  // block-uniform
+  const uint32_t ng = (uint32_t)min<uint64_t>((uint64_t)GPB, a.n_groups - g0);
+  s_head[tid] = 0ull;  // NBLK == NT
+  // ---- 1. group scalars (wave 0, lane j = group slot j)
+  if (wv == 0u) {
+    uint32_t k = 0, m = 0xFFFFFFFFu, pl = 0, r = 0, p0 = 0;
+    uint64_t d = 0, po = 0;
+    bool ok = true;
+    if (lane < ng) {
+      p0 = a.grp_ptr[g0 + lane];
+      k = a.grp_ptr[g0 + lane + 1] - p0;
+      if constexpr (RECOVER) {
+        m = a.missing[g0 + lane];
+        pl = a.parity_len[g0 + lane];
+        d = a.out_off[g0 + lane];
+        po = a.parity_off[g0 + lane];
+        ok = m < k && pl >= 16u && pl <= kMaxPacket;
+      } else {
+        d = a.parity_off[g0 + lane];
+      }
+      ok = ok && k >= 1u && k <= 255u;
+      r = ok ? (RECOVER ? k - 1u : k) : 0u;
+    }
+    const uint32_t incl = wave_incl_scan(r, lane);
+    const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (lane < (uint32_t)GPB) {
+      s_rb[lane] = incl - r;
+      s_kb[lane] = p0;
+      s_m[lane] = m;
+      s_pl[lane] = pl;
+      s_doff[lane] = d;
+      s_poff[lane] = po;
+    }
+    const bool all_ok = !wave_any(lane < ng && !ok);  // every lane of wave 0
+    if (lane == 0u) {
+      s_rb[GPB] = R;
+      s_fit = (all_ok && R <= NT) ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  const uint32_t R = s_rb[GPB];
+  bool fit = s_fit != 0u;
+  // ---- 2. one received packet per lane
+  if (RECOVER && PF && fit) {
+    for (uint32_t q = tid; q < GPB * (uint32_t)kParWin; q += NT) {
+      const uint32_t jq = q / (uint32_t)kParWin, t = q - jq * (uint32_t)kParWin;
+      u32x4 w = {0u, 0u, 0u, 0u};
+      if (jq < ng) w = parity_window_bf<true>(a.parity + s_poff[jq], s_pl[jq], t);
+      lds_put16<1>(acc + jq * kAccWords, t, w);
+    }
+  }
+  uint32_t len = 0, offlo = 0, offhi = 0, j = 0;
+  if (fit && tid < R) {
+#pragma unroll
+    for (int q = 1; q < GPB; ++q) j += tid >= s_rb[q] ? 1u : 0u;
+    const uint32_t i = tid - s_rb[j];
+    const uint32_t p = s_kb[j] + i + (RECOVER && i >= s_m[j] ? 1u : 0u);
+    len = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    offlo = (uint32_t)o;
+    offhi = (uint32_t)(o >> 32);
+    const uint32_t lim = RECOVER ? s_pl[j] : kMaxPacket;
+    if (len < 16u || len > lim) s_fit = 0u;  // benign race: every writer stores 0
+    if (!RECOVER) atomicMax(&s_pl[j], len);
+  }
+  const uint32_t n = (len + 15u) >> 4;
+  uint32_t W;
+  const uint32_t S = block_excl_scan<WAVES>(n, lane, wv, s_w, W);  // (barriers publish s_fit)
+  fit = fit && s_fit != 0u && W <= CAPW;
+  if (!fit) {
+    // per-group body, one wave per group (exact outputs and error bits)
+    uint32_t* fb = s_raw + wv * kFbWords;
+    for (uint32_t jj = wv; jj < ng; jj += WAVES) {
+      GroupPrefetch f;
+      group_scalars<RECOVER>(a, g0 + jj, f);
+      group_vectors<RECOVER, true>(a, g0 + jj, lane, f);
+      wave_lds_order();
+      ragged_group<RECOVER, true, 2, 1>(a, g0 + jj, lane, f, fb,
+                                        reinterpret_cast<uint64_t*>(fb + 4u * kParWin),
+                                        reinterpret_cast<u32x4*>(fb + 6u * kParWin));
+      wave_lds_order();
+    }
+    return;
+  }
+  if (tid < R) {
+    pk[tid] = u32x4{offlo, offhi, len | (j << 16), S};
+    __hip_atomic_fetch_or(&s_head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  // accumulators: the parity rows (recover) or zero (encode), windows of all groups
+  if (!(RECOVER && PF)) {
+    for (uint32_t q = tid; q < GPB * (uint32_t)kParWin; q += NT) {
+      const uint32_t jq = q / (uint32_t)kParWin, t = q - jq * (uint32_t)kParWin;
+      u32x4 w = {0u, 0u, 0u, 0u};
+      if constexpr (RECOVER) {
+        if (jq < ng) w = parity_window_bf<true>(a.parity + s_poff[jq], s_pl[jq], t);
+      }
+      lds_put16<1>(acc + jq * kAccWords, t, w);
+    }
+  }
+  __syncthreads();  // packet table, start mask, accumulators, parity lengths
+  const uint32_t nblk = (W + 63u) >> 6;
+  uint32_t tot;
+  const uint32_t c = block_excl_scan<WAVES>(tid < nblk ? (uint32_t)__popcll(s_head[tid]) : 0u,
+                                            lane, wv, s_w, tot);
+  s_cnt[tid] = c;
+  if (wv == 0u) {  // output windows per group (encode: the max lengths are final)
+    const uint32_t nw = lane < ng ? (s_pl[lane] + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(nw, lane);
+    if (lane < (uint32_t)GPB) s_ob[lane] = incl - nw;
+    if (lane == 0u) s_ob[GPB] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (!RECOVER && lane < ng) a.parity_len_out[g0 + lane] = (uint16_t)s_pl[lane];
+  }
+  __syncthreads();
+  // ---- 3. the flat windows, U iterations' loads in flight
+  const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+  const uint32_t nit = (W + NT - 1u) / NT;
+  for (uint32_t it = 0; it < nit; it += U) {
+    u32x4 md[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t f = (it + (uint32_t)u) * NT + tid;
+      const uint32_t b = min(f >> 6, nblk - 1u);
+      const uint64_t M = s_head[b];
+      const uint32_t pi = min(s_cnt[b] + (uint32_t)__popcll(M & below) - 1u, R - 1u);
+      md[u] = pk[pi];
+    }
+    u32x4 v[U];
+    uint32_t tt[U], sh[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t f = (it + (uint32_t)u) * NT + tid;
+      const uint32_t ln = md[u].z & 0xFFFFu;
+      const uint32_t win = 16u * (f - md[u].w);
+      const bool full = win + 16u <= ln;
+      v[u] = ld16t<true>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) + (full ? win : ln - 16u));
+      sh[u] = full ? 0u : min(win + 16u - ln, 15u);
+      tt[u] = f < W ? (md[u].z >> 16) * kAccWords + (f - md[u].w) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tt[u] != 0xFFFFFFFFu) lds_xor16<1>(acc, tt[u], shr_bytes_bf(v[u], sh[u]));
+  }
+  __syncthreads();  // every lane's XORs done
+  // ---- 4. stores, flattened over the groups' output windows
+  const uint32_t NW = s_ob[GPB];
+  for (uint32_t q = tid; q < NW; q += NT) {
+    uint32_t jq = 0;
+#pragma unroll
+    for (int i = 1; i < GPB; ++i) jq += q >= s_ob[i] ? 1u : 0u;
+    const uint32_t t = q - s_ob[jq];
+    const uint32_t plen = s_pl[jq];
+    uint8_t* dst = a.out + s_doff[jq];
+    const uint32_t* ac = acc + jq * kAccWords;
+    if (16u * t + 16u <= plen) {
+      st16t<true>(dst + 16u * t, lds_get16<1>(ac, t));
+    } else {
+      const uint32_t o = plen - 16u * t;  // 1..15
+      st16t<true>(dst + plen - 16u, bytes16_at(lds_get16<1>(ac, t - 1u), lds_get16<1>(ac, t), o));
+    }
+  }
+}
+
 
 // Ragged CSR, parity-window form — the SMALL-BATCH (latency) kernel: the
 // mapped host path runs a batch of <= kDirectGroups groups with it
@@ -1515,9 +1746,11 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   return hipSuccess;
 }
 
+constexpr int kRaggedBlockWaves = 4, kRaggedBlockGroups = 8;  // ragged_block_kernel shape
+
 hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
   if (a0.n_groups == 0) return hipSuccess;
-  const uint64_t gpb = (kBlock / 64) * kRaggedGPW;  // kRaggedGPW groups per wave
+  const uint64_t gpb = kRaggedBlockGroups;
   const uint64_t maxg = kMaxBlocks256 * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     RaggedArgs a = a0;
@@ -1534,11 +1767,11 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
     }
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
     if (recover)
-      hipLaunchKernelGGL((ragged_multi_kernel<true, true, kRaggedGPW>), dim3((uint32_t)blocks),
-                         dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((ragged_block_kernel<true, kRaggedBlockWaves, kRaggedBlockGroups>),
+                         dim3((uint32_t)blocks), dim3(64 * kRaggedBlockWaves), 0, s, a);
     else
-      hipLaunchKernelGGL((ragged_multi_kernel<false, true, kRaggedGPW>), dim3((uint32_t)blocks),
-                         dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((ragged_block_kernel<false, kRaggedBlockWaves, kRaggedBlockGroups>),
+                         dim3((uint32_t)blocks), dim3(64 * kRaggedBlockWaves), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

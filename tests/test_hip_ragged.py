@@ -210,9 +210,11 @@ def test_cpp_quic_fec_group():
 
 @pytest.mark.parametrize("host", [False, True, "mapped"])
 def test_ragged_pair_boundaries(ctx, host):
-    """launch_ragged runs two consecutive groups per wave (groups 2w, 2w+1) in
-    one flat window space when their received packets fit the 64-lane table,
-    all are >= 16 B and every field is valid; otherwise the per-group body.
+    """The round-2 product (ragged_multi_kernel) ran two consecutive groups
+    per wave in one flat window space when their received packets fit the
+    64-lane table, all are >= 16 B and every field is valid; otherwise the
+    per-group body.  Its switch points, kept as a shape test of the block
+    kernel (these 17 groups are blocks of 8 with mixed fits and fallbacks).
     Pairs straddling each switch: 63 / 64 / 65 received packets (encode: k;
     recover: k - 1), a packet below 16 B in one group, a redundancy shorter
     than 16 B, k = 1 next to k = 255, and an odd group count (the last wave
@@ -252,10 +254,57 @@ def test_ragged_pair_boundaries(ctx, host):
     assert np.array_equal(out, want_o)
 
 
+@pytest.mark.parametrize("host", [False, True, "mapped"])
+def test_ragged_block_boundaries(ctx, host):
+    """launch_ragged runs eight consecutive groups per 4-wave block in one
+    flat window space (ragged_block_kernel) when their received packets fit
+    the 256-lane packet table, their windows fit the 16,384-window start
+    mask, every packet is >= 16 B and every field is valid; otherwise the
+    per-group body.  Blocks straddling each switch: 256 / 257 received
+    packets (encode) and 248 / 249 / 256 (recover), 16,016 windows (fits) and
+    16,744 (falls back), k = 1 groups on the fast path (recover: no received
+    packet, the revived packet is the redundancy), a packet below 16 B, and a
+    partial last block.  Against the oracle, bit-exact."""
+    rng = np.random.default_rng(12)
+
+    def grp(k, lo=16, hi=1452):
+        return list(rng.integers(lo, hi + 1, k))
+    groups = ([grp(32) for _ in range(8)]                       # 256 / 248
+              + [grp(32) for _ in range(7)] + [grp(33)]        # 257 / 249
+              + [grp(33) for _ in range(8)]                    # 264 / 256
+              + [grp(22, 1452) for _ in range(8)]              # 16,016 windows
+              + [grp(23, 1452) for _ in range(8)]              # 16,744 / 16,016
+              + [grp(1), grp(1), grp(1), grp(1), grp(5), [16], grp(2), grp(3)]
+              + [grp(5) + [15], grp(6), grp(4), grp(9), grp(3), grp(2), grp(7), grp(1)]
+              + [grp(4), grp(11), grp(1)])                     # partial last block
+    ln = np.array([l for g in groups for l in g], np.uint16)
+    ptr = np.zeros(len(groups) + 1, np.uint32)
+    ptr[1:] = np.cumsum([len(g) for g in groups])
+    gap = rng.integers(0, 9, ln.size).astype(np.uint64)
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gap[:-1])
+    data = rng.integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    n = len(groups)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1460) + np.uint64(5)
+    miss = np.array([rng.integers(0, len(g)) for g in groups], np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1460 + 5)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1460 + 5)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged(ctx, z, host=host)
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
+
+
 def test_ragged_large_batch_odd_groups(ctx):
-    """A large device batch (~213K groups) with odd groups mixed in (> 64
-    received packets and packets < 16 B take the per-group body of
-    ragged_multi_kernel): parity, lengths and revived packets against the
+    """A large device batch (~213K groups) with odd groups mixed in (65-200
+    received packets: a block of 8 groups then holds up to ~270, some blocks
+    over the 256-lane packet table and some under it; packets < 16 B take the
+    per-group body of ragged_block_kernel): parity, lengths and revived
+    packets against the
     oracle on sampled groups, the odd ones among them."""
     n = 212_992 + 333
     gs = np.arange(n, dtype=np.uint64)

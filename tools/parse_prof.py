@@ -21,11 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def kind(name):
     """fixed_xor_kernel<K, RECOVER, NT, SM> / phase_xor_kernel<K, RECOVER, ...> (the
-    product's fixed-shape kernels: one-pass and phased) / ragged_multi_kernel<RECOVER, NT, ...>."""
+    product's fixed-shape kernels: one-pass and phased) / ragged_block_kernel<RECOVER, ...> (round 3; ragged_multi_kernel before)."""
     m = re.search(r"(?:fixed|phase)_xor_kernel<(-?\d+), (true|false)", name)
     if m:
         return "recover" if m.group(2) == "true" else "encode"
-    m = re.search(r"ragged_(?:multi|xor)_kernel<(true|false)", name)
+    m = re.search(r"ragged_(?:multi|xor|block)_kernel<(true|false)", name)
     if m:
         return "ragged_recover" if m.group(1) == "true" else "ragged_encode"
     return None

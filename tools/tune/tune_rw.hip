@@ -295,6 +295,61 @@ int main(int argc, char** argv) {
     RG_PXCD(true, 4, 8, "pxcd C4 x8");
   }
 #undef RG_PXCD
+#define RG_BLOCK(REC, WV, GPB, NAME) RG_BLOCKU(REC, WV, GPB, 2, NAME)
+#define RG_BLOCKU(REC, WV, GPB, UU, NAME) RG_BLOCKX(REC, WV, GPB, UU, true, NAME)
+#define RG_BLOCKX(REC, WV, GPB, UU, PF, NAME)                                                   \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, WV, GPB, UU, PF>),        \
+                                     dim3((uint32_t)((G + GPB - 1) / GPB)), dim3(64 * WV), 0, 0, \
+                                     a0);                                                      \
+                }})
+  if (getenv("TUNE_RW_BLOCK3")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 recover (ref)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+      RG_BLOCKX(true, 4, 8, 2, false, "block W4 G8 noPF");
+      RG_BLOCKX(true, 4, 8, 2, true, "block W4 G8 PF");
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 encode (ref)", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+      RG_BLOCKX(false, 4, 8, 2, true, "block W4 G8");
+    }
+  }
+  if (getenv("TUNE_RW_BLOCK2")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 encode (ref)", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+      RG_BLOCK(false, 4, 8, "block W4 G8");
+      RG_BLOCK(false, 2, 4, "block W2 G4");
+      RG_BLOCK(false, 2, 6, "block W2 G6");
+      RG_BLOCK(false, 4, 6, "block W4 G6");
+      RG_BLOCK(false, 4, 10, "block W4 G10");
+      RG_BLOCKU(false, 4, 8, 1, "block W4 G8 U1");
+      RG_BLOCKU(false, 4, 8, 3, "block W4 G8 U3");
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 recover (ref)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+      RG_BLOCK(true, 4, 8, "block W4 G8");
+      RG_BLOCK(true, 2, 4, "block W2 G4");
+      RG_BLOCK(true, 4, 6, "block W4 G6");
+      RG_BLOCKU(true, 4, 8, 3, "block W4 G8 U3");
+    }
+  }
+  if (getenv("TUNE_RW_BLOCK")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      vs.push_back({"multi2 encode (ref)", false, [=](const RaggedArgs& a) { launch_multi<false, 2>(a, G); }});
+      RG_BLOCK(false, 4, 8, "block W4 G8");
+      RG_BLOCK(false, 4, 12, "block W4 G12");
+      RG_BLOCK(false, 8, 16, "block W8 G16");
+      RG_BLOCK(false, 16, 32, "block W16 G32");
+    }
+    vs.push_back({"multi2 recover (ref)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
+    RG_BLOCK(true, 4, 8, "block W4 G8");
+    RG_BLOCK(true, 8, 16, "block W8 G16");
+    RG_BLOCK(true, 16, 32, "block W16 G32");
+  }
+#undef RG_BLOCK
+#undef RG_BLOCKU
+#undef RG_BLOCKX
 #undef RG_PERSIST
   // parity / revived slot strides in ONE process (the placement of the
   // buffers is per process): 1452, 1472 (ALIGNAS(64) char[kMaxPacketSize]),
@@ -339,7 +394,9 @@ int main(int argc, char** argv) {
   const bool diag_only = getenv("TUNE_RW_DIAG") != nullptr || getenv("TUNE_RW_DAL") != nullptr ||
                          getenv("TUNE_RW_PERSIST") != nullptr || getenv("TUNE_RW_SLOT") != nullptr ||
                          getenv("TUNE_RW_SPLIT") != nullptr ||
-                         getenv("TUNE_RW_PERSIST2") != nullptr;
+                         getenv("TUNE_RW_PERSIST2") != nullptr || getenv("TUNE_RW_BLOCK") != nullptr ||
+                         getenv("TUNE_RW_BLOCK2") != nullptr ||
+                         getenv("TUNE_RW_BLOCK3") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
