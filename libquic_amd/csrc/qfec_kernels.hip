@@ -902,8 +902,8 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_xor_kernel(RaggedArgs a) {
 // run the per-group body above with its exact error semantics.  Measured
 // +1.0-1.6% encode and recover over one group per wave in three interleaved
 // A/B runs (tune_multi_t2.txt, ragged_slots_p*.txt, tune_multi_sp.txt);
-// three groups per wave overflow the table too often (-10%).
-constexpr int kRaggedGPW = 2;
+// three groups per wave overflow the table too often (-10%).  tools/tune runs
+// it with GPW = 2.
 
 template <int N, typename T>
 __device__ __forceinline__ T sel_n(const T (&v)[N], uint32_t j) {
