@@ -590,6 +590,8 @@ def main(argv=None):
         _progress("fixed-shape timed steps done")
         if not args.no_ragged:
             line["ragged"] = bench_ragged(ctx, torch, dev, stream, steps=max(5, args.steps // 2))
+            line["ragged_packed"] = bench_ragged(ctx, torch, dev, stream,
+                                                 steps=max(5, args.steps // 2), align=1, slot=1452)
         _progress("ragged done")
         if not args.no_protect:
             line["protect"] = bench_protect(ctx, torch, dev, stream, G, k, L,
@@ -648,25 +650,39 @@ def ragged_alg_bytes(G=1 << 20):
     return lens_sum + pl_sum, (lens_sum - miss_len) + 2 * pl_sum
 
 
-def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
-    """configs[3]: ragged batch, k 5-15, len 64-1350, packed CSR (device-resident)."""
+RAGGED_ALIGN, RAGGED_SLOT = 16, 1536  # the default ragged line's layout
+
+
+def ragged_layout_tag(align=RAGGED_ALIGN, slot=RAGGED_SLOT):
+    return f"align{align}_slot{slot}"
+
+
+def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20, align=RAGGED_ALIGN,
+                 slot=RAGGED_SLOT):
+    """configs[3]: ragged batch, k 5-15, len 64-1350 (device-resident).
+
+    align=16 / slot=1536 (the default line): payloads on 16-B boundaries, as
+    the host side's payload arena lays them out (quic_fec_group.cc
+    PayloadArena::Alloc), parity / revived rows in 128-B-aligned slots.
+    align=1 / slot=1452: byte-packed payloads and kMaxPacketSize slots (the
+    `ragged_packed` line).  Same groups, lengths and algorithmic bytes."""
     from libquic_amd import synth
     gs = np.arange(G, dtype=np.uint64)
-    ks, ptr, ln, off = synth.ragged_layout(0, G, 5, 15, 64, 1350, SEED_RAGGED)
+    ks, ptr, ln, off = synth.ragged_layout(0, G, 5, 15, 64, 1350, SEED_RAGGED, align=align)
     total = int(off[-1]) + int(ln[-1])
     plen_max = np.maximum.reduceat(ln, ptr[:-1].astype(np.int64))
     miss = synth.drop_indices(SEED_DROP, gs, ks).astype(np.uint8)
     t_off = torch.from_numpy(off.view(np.int64)).to(dev)
     t_len = torch.from_numpy(ln.view(np.int16)).to(dev)
     t_ptr = torch.from_numpy(ptr.view(np.int32)).to(dev)
-    poff = np.arange(G, dtype=np.uint64) * np.uint64(1452)
+    poff = np.arange(G, dtype=np.uint64) * np.uint64(slot)
     t_poff = torch.from_numpy(poff.view(np.int64)).to(dev)
     t_miss = torch.from_numpy(miss).to(dev)
     data = torch.empty(total, dtype=torch.uint8, device=dev)
     ctx.synth_ragged(data, t_off, t_len, t_ptr, 0, G, SEED_RAGGED)
-    par = torch.empty(G * 1452, dtype=torch.uint8, device=dev)
+    par = torch.empty(G * slot, dtype=torch.uint8, device=dev)
     plen = torch.empty(G, dtype=torch.int16, device=dev)
-    out = torch.empty(G * 1452, dtype=torch.uint8, device=dev)
+    out = torch.empty(G * slot, dtype=torch.uint8, device=dev)
 
     def run(ev=None):
         if ev:
@@ -700,9 +716,9 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
         p = int(ptr[g]) + int(miss[g])
         o, l_ = int(off[p]), int(ln[p])
         pl = int(plen_max[g])
-        seg = out_h[g * 1452: g * 1452 + pl]
+        seg = out_h[g * slot: g * slot + pl]
         ok = ok and np.array_equal(seg[:l_], data_h[o:o + l_]) and not seg[l_:].any()
-        acc = par_h[g * 1452: g * 1452 + pl].copy()
+        acc = par_h[g * slot: g * slot + pl].copy()
         for q in range(int(ptr[g]), int(ptr[g + 1])):
             acc[:int(ln[q])] ^= data_h[int(off[q]):int(off[q]) + int(ln[q])]
         ok = ok and not acc.any()
@@ -712,18 +728,21 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20):
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("ragged_groups") == G:
+        if tj.get("ragged_groups") == G and tj.get("ragged_layout") == ragged_layout_tag(align, slot):
             traffic = {kd: tj.get(f"ragged_{kd}_traffic_over_algorithmic")
                        for kd in ("encode", "recover")}
             traffic["source"] = "profiles/traffic_latest.json (PMC FETCH_SIZE + WRITE_SIZE)"
-    return {"groups": G, "k": "5-15", "len": "64-1350", "layout": "packed CSR",
+    layout = ("packed CSR (byte offsets)" if align == 1 else
+              f"CSR, payloads on {align}-B boundaries (the payload arena's layout)")
+    return {"groups": G, "k": "5-15", "len": "64-1350", "layout": layout,
+            "parity_slot_bytes": slot,
             "encode_GiBps": round(b_enc / enc / 2**30, 2),
             "recover_GiBps": round(b_rec / rec / 2**30, 2),
             "encode_frac": round(b_enc / enc / 1e9 / HBM_PEAK_GBS, 4),
             "recover_frac": round(b_rec / rec / 1e9 / HBM_PEAK_GBS, 4),
             "encode_us": round(enc * 1e6, 1), "recover_us": round(rec * 1e6, 1),
             "hbm_traffic_over_algorithmic": traffic, "verified": bool(ok),
-            "kernel": "ragged_block_kernel<RECOVER, 4, 8> (4 waves x 8 groups per block, one flat window space)"}
+            "kernel": "ragged_block_kernel<RECOVER, 4, 8> (4 waves x 8 groups per block, one flat window space; aligned last windows loaded in place)"}
 
 
 def _time_on(torch, stream, fn, reps):

@@ -1174,7 +1174,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // PF (recover): the parity windows are loaded into the accumulators before the
 // packet table, so their round trip overlaps the table's (measured equal to
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
-template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true>
+template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true>
 __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
   constexpr uint32_t NT = 64u * WAVES;
@@ -1325,19 +1325,38 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
     }
     u32x4 v[U];
     uint32_t tt[U], sh[U];
+    bool inp[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t f = (it + (uint32_t)u) * NT + tid;
       const uint32_t ln = md[u].z & 0xFFFFu;
       const uint32_t win = 16u * (f - md[u].w);
       const bool full = win + 16u <= ln;
-      v[u] = ld16t<true>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) + (full ? win : ln - 16u));
+      const uint64_t at = (((uint64_t)md[u].y << 32) | md[u].x) + win;
+      // AL: a last window whose start is 16-B aligned (payloads on 16-B
+      // boundaries, the payload arena's layout) is loaded in place and its
+      // bytes past the packet masked: an aligned 16-B load holding one packet
+      // byte cannot leave that byte's page.  Otherwise the 16 bytes ending at
+      // the packet end, shifted down.
+      inp[u] = full || (AL && win < ln && (at & 15u) == 0u);
+      v[u] = ld16t<true>(a.bytes + (inp[u] ? at : at - win + ln - 16u));
       sh[u] = full ? 0u : min(win + 16u - ln, 15u);
       tt[u] = f < W ? (md[u].z >> 16) * kAccWords + (f - md[u].w) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (tt[u] != 0xFFFFFFFFu) lds_xor16<1>(acc, tt[u], shr_bytes_bf(v[u], sh[u]));
+      if (tt[u] != 0xFFFFFFFFu) {
+        u32x4 w;
+        if constexpr (AL) {
+          // in place: v & (ones >> sh); shifted: v >> sh (sh = 0 when full)
+          const u32x4 ones = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+          const u32x4 m = shr_bytes_bf(inp[u] ? ones : v[u], sh[u]);
+          w = inp[u] ? (m & v[u]) : m;
+        } else {
+          w = shr_bytes_bf(v[u], sh[u]);
+        }
+        lds_xor16<1>(acc, tt[u], w);
+      }
   }
   __syncthreads();  // every lane's XORs done
   // ---- 4. stores, flattened over the groups' output windows

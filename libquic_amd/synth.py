@@ -41,8 +41,12 @@ def drop_indices(seed, g, k):
     return (h % np.asarray(k, dtype=np.uint64)).astype(np.int64)
 
 
-def ragged_layout(g0, n, kmin=5, kmax=15, lmin=64, lmax=1350, seed=SEED_RAGGED):
-    """Packed CSR layout of n groups: (k, grp_ptr u32, pkt_len u16, pkt_off u64)."""
+def ragged_layout(g0, n, kmin=5, kmax=15, lmin=64, lmax=1350, seed=SEED_RAGGED, align=1):
+    """CSR layout of n groups: (k, grp_ptr u32, pkt_len u16, pkt_off u64).
+
+    align=1: byte-packed payloads.  align=16: each payload starts on a 16-B
+    boundary (≤ 15 B of gap after each), which is the layout the host side's
+    payload arena hands the kernels (quic_fec_group.cc PayloadArena::Alloc)."""
     gs = np.arange(g0, g0 + n, dtype=np.uint64)
     ks = group_sizes(seed, gs, kmin, kmax)
     ptr = np.zeros(n + 1, np.uint32)
@@ -52,7 +56,11 @@ def ragged_layout(g0, n, kmin=5, kmax=15, lmin=64, lmax=1350, seed=SEED_RAGGED):
     ln = packet_lengths(seed, gidx, iidx, lmin, lmax).astype(np.uint16)
     off = np.zeros(ln.size, np.uint64)
     if ln.size > 1:
-        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+        step = ln[:-1].astype(np.uint64)
+        if align > 1:
+            a = np.uint64(align)
+            step = (step + a - np.uint64(1)) // a * a
+        off[1:] = np.cumsum(step)
     return ks, ptr, ln, off
 
 

@@ -88,8 +88,9 @@ def test_golden_ragged(ctx, golden_ragged, tag, host):
     assert np.array_equal(out, z["recovered"])
 
 
-def synth_batch(n, kmin=5, kmax=15, lmin=64, lmax=1350, g0=0, seed=Q.SEED_RAGGED):
-    """CSR shapes from the seeded generators; bytes filled on the host by the oracle."""
+def synth_batch(n, kmin=5, kmax=15, lmin=64, lmax=1350, g0=0, seed=Q.SEED_RAGGED, align=1):
+    """CSR shapes from the seeded generators; bytes filled on the host by the oracle.
+    align=16: payloads on 16-B boundaries (the host payload arena's layout)."""
     gs = np.arange(g0, g0 + n, dtype=np.uint64)
     ks = Q.ragged_k(seed, gs, kmin, kmax)
     ptr = np.zeros(n + 1, np.uint32)
@@ -98,13 +99,17 @@ def synth_batch(n, kmin=5, kmax=15, lmin=64, lmax=1350, g0=0, seed=Q.SEED_RAGGED
     iidx = np.arange(ptr[-1]) - np.repeat(ptr[:-1].astype(np.int64), ks)
     ln = Q.ragged_len(seed, gidx, iidx, lmin, lmax).astype(np.uint16)
     off = np.zeros(ln.size, np.uint64)
-    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    off[1:] = np.cumsum((ln[:-1].astype(np.uint64) + np.uint64(align - 1))
+                        // np.uint64(align) * np.uint64(align))
     return ks, ptr, ln, off
 
 
-def test_ragged_synth_vs_oracle(ctx):
+@pytest.mark.parametrize("align,slot", [(1, 1452), (16, 1536)])
+def test_ragged_synth_vs_oracle(ctx, align, slot):
+    """Whole-batch parity: byte-packed payloads with kMaxPacketSize parity
+    slots, and bench.py's default line (16-B-aligned payloads, 1,536-B slots)."""
     n = 20_000
-    ks, ptr, ln, off = synth_batch(n, g0=77)
+    ks, ptr, ln, off = synth_batch(n, g0=77, align=align)
     total = int(off[-1] + ln[-1])
     data_d = torch.zeros(total, dtype=torch.uint8, device=DEV)
     ctx.synth_ragged(data_d, dview(off), dview(ln), dview(ptr), 77, n, Q.SEED_RAGGED)
@@ -117,11 +122,11 @@ def test_ragged_synth_vs_oracle(ctx):
         want = np.zeros(int(ln[p]), np.uint8)
         OC.lib().qo_synth_row(Q.SEED_RAGGED, 77 + g, i, int(ln[p]), OC._p(want))
         assert np.array_equal(data[int(off[p]):int(off[p]) + int(ln[p])], want)
-    poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(slot)
     miss = Q.drop_index(Q.SEED_DROP, np.arange(77, 77 + n), ks).astype(np.uint8)
-    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * slot)
     rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
-                                    n * 1452)
+                                    n * slot)
     assert rc == 0 and rc2 == 0
     z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
              out_off=poff, parity=want_p, recovered=want_o)

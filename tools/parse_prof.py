@@ -71,10 +71,11 @@ def main(run_dir, groups=1 << 20, k=10, L=1350):
     # in a --profile-only run)
     if "ragged_encode" in fetch and "ragged_encode" in write:
         sys.path.insert(0, ROOT)
-        from bench import ragged_alg_bytes
+        from bench import ragged_alg_bytes, ragged_layout_tag
         rg = 1 << 20
         alg_e, alg_r = ragged_alg_bytes(rg)
         out["ragged_groups"] = rg
+        out["ragged_layout"] = ragged_layout_tag()  # the --profile-only leg's layout
         for kd, alg in (("encode", alg_e), ("recover", alg_r)):
             f_, w_ = fetch.get(f"ragged_{kd}"), write.get(f"ragged_{kd}")
             if f_ and w_:

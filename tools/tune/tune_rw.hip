@@ -96,6 +96,8 @@ int main(int argc, char** argv) {
   // an ALIGNAS(64) char[kMaxPacketSize] slot; 1536: 128-B lines)
   const uint64_t slot = argc > 8 ? (uint64_t)atoi(argv[8]) : 1452u;
   const uint64_t SB = 1536;  // buffer bytes per group (any slot <= 1536)
+  // TUNE_RW_PALIGN=16: payloads on 16-B boundaries (the payload arena's layout)
+  const uint64_t palign = getenv("TUNE_RW_PALIGN") ? (uint64_t)atoi(getenv("TUNE_RW_PALIGN")) : 1u;
   uint64_t out_pos = 0;
   const uint64_t seed = 0x51554944;
   std::vector<uint32_t> ptr{0};
@@ -113,7 +115,7 @@ int main(int argc, char** argv) {
       const uint32_t ln = lmin + (uint32_t)(sm64(seed ^ (0x4Cull << 56) ^ (g * 256 + i)) % lspan);
       len.push_back((uint16_t)ln);
       off.push_back(bytes);
-      bytes += ln;
+      bytes += (ln + palign - 1) / palign * palign;
       s += ln;
       if (i != miss[g]) sm += ln;
       mx = std::max(mx, ln);
@@ -304,6 +306,22 @@ int main(int argc, char** argv) {
                                      dim3((uint32_t)((G + GPB - 1) / GPB)), dim3(64 * WV), 0, 0, \
                                      a0);                                                      \
                 }})
+#define RG_BLOCKA(REC, AL, NAME)                                                               \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, AL>),      \
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0);      \
+                }})
+  if (getenv("TUNE_RW_BLOCKAL")) {  // aligned in-place tail loads (AL) on and off
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKA(false, false, "block AL0");
+      RG_BLOCKA(false, true, "block AL1");
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKA(true, false, "block AL0");
+      RG_BLOCKA(true, true, "block AL1");
+    }
+  }
   if (getenv("TUNE_RW_BLOCK3")) {
     for (int rep = 0; rep < 2; ++rep) {
       vs.push_back({"multi2 recover (ref)", true, [=](const RaggedArgs& a) { launch_multi<true, 2>(a, G); }});
@@ -396,7 +414,7 @@ int main(int argc, char** argv) {
                          getenv("TUNE_RW_SPLIT") != nullptr ||
                          getenv("TUNE_RW_PERSIST2") != nullptr || getenv("TUNE_RW_BLOCK") != nullptr ||
                          getenv("TUNE_RW_BLOCK2") != nullptr ||
-                         getenv("TUNE_RW_BLOCK3") != nullptr;
+                         getenv("TUNE_RW_BLOCK3") != nullptr || getenv("TUNE_RW_BLOCKAL") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
@@ -559,9 +577,11 @@ int main(int argc, char** argv) {
       res[i].push_back((vs[i].rec ? rec_alg : enc_alg) / (ms / reps * 1e-3) / 1e9);
     }
   }
-  std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packets, parity slots %s %llu\n", kmin,
+  std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packet buffer (payloads on %llu-B "
+              "boundaries), parity slots %s %llu\n", kmin,
               kmin + kspan - 1, lmin, lmin + lspan - 1, (unsigned long long)G, bytes / 1e9,
-              packed_out ? "packed" : "stride", (unsigned long long)(packed_out ? 0 : slot));
+              (unsigned long long)palign, packed_out ? "packed" : "stride",
+              (unsigned long long)(packed_out ? 0 : slot));
   std::printf("%-24s %10s %10s %8s\n", "variant", "med GB/s", "max GB/s", "%8TB/s");
   for (size_t i = 0; i < vs.size(); ++i) {
     auto v = res[i];
