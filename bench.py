@@ -728,10 +728,11 @@ def bench_ragged(ctx, torch, dev, stream, steps=10, G=1 << 20, align=RAGGED_ALIG
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("ragged_groups") == G and tj.get("ragged_layout") == ragged_layout_tag(align, slot):
-            traffic = {kd: tj.get(f"ragged_{kd}_traffic_over_algorithmic")
-                       for kd in ("encode", "recover")}
-            traffic["source"] = "profiles/traffic_latest.json (PMC FETCH_SIZE + WRITE_SIZE)"
+        ent = tj.get("ragged_by_layout", {}).get(ragged_layout_tag(align, slot))
+        if tj.get("ragged_groups") == G and ent:
+            traffic = {kd: ent.get(kd) for kd in ("encode", "recover")}
+            traffic["source"] = ("profiles/traffic_latest.json (PMC FETCH_SIZE + WRITE_SIZE, run "
+                                 f"{ent.get('source')})")
     layout = ("packed CSR (byte offsets)" if align == 1 else
               f"CSR, payloads on {align}-B boundaries (the payload arena's layout)")
     return {"groups": G, "k": "5-15", "len": "64-1350", "layout": layout,

@@ -51,7 +51,7 @@ def pmc(run_dir, counter):
     return vals
 
 
-def main(run_dir, groups=1 << 20, k=10, L=1350):
+def main(run_dir, groups=1 << 20, k=10, L=1350, layout=None):
     fetch = pmc(run_dir, "FETCH_SIZE")
     write = pmc(run_dir, "WRITE_SIZE")
     out = {"groups": groups, "k": k, "L": L, "source": run_dir,
@@ -75,7 +75,8 @@ def main(run_dir, groups=1 << 20, k=10, L=1350):
         rg = 1 << 20
         alg_e, alg_r = ragged_alg_bytes(rg)
         out["ragged_groups"] = rg
-        out["ragged_layout"] = ragged_layout_tag()  # the --profile-only leg's layout
+        # the --profile-only leg's layout (bench.py's default unless given)
+        out["ragged_layout"] = layout or ragged_layout_tag()
         for kd, alg in (("encode", alg_e), ("recover", alg_r)):
             f_, w_ = fetch.get(f"ragged_{kd}"), write.get(f"ragged_{kd}")
             if f_ and w_:
@@ -87,10 +88,23 @@ def main(run_dir, groups=1 << 20, k=10, L=1350):
                 out[f"ragged_{kd}_traffic_over_algorithmic"] = (f + w) / alg
     out["kernels"] = {k: sorted(v) for k, v in KERNELS.items()}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w") as fh:
+    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    # per-layout ragged ratios: this run's layout replaces its own entry, the
+    # other layouts' entries (earlier runs) are kept with their source
+    by = {}
+    if os.path.exists(path):
+        with open(path) as fh:
+            by = json.load(fh).get("ragged_by_layout", {})
+    if "ragged_layout" in out:
+        by[out["ragged_layout"]] = {
+            "encode": out.get("ragged_encode_traffic_over_algorithmic"),
+            "recover": out.get("ragged_recover_traffic_over_algorithmic"),
+            "source": os.path.basename(os.path.normpath(run_dir))}
+    out["ragged_by_layout"] = by
+    with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], layout=sys.argv[2] if len(sys.argv) > 2 else None)
