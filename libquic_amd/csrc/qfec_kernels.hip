@@ -1174,7 +1174,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // PF (recover): the parity windows are loaded into the accumulators before the
 // packet table, so their round trip overlaps the table's (measured equal to
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
-template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true>
+// DIAG (tools/tune only, not exact): 1 = no parity stores.
+template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
 __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
   constexpr uint32_t NT = 64u * WAVES;
@@ -1369,6 +1370,7 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
     const uint32_t plen = s_pl[jq];
     uint8_t* dst = a.out + s_doff[jq];
     const uint32_t* ac = acc + jq * kAccWords;
+    if (DIAG == 1 && plen != 0xFFFFFu) continue;  // never a real length: no stores
     if (16u * t + 16u <= plen) {
       st16t<true>(dst + 16u * t, lds_get16<1>(ac, t));
     } else {

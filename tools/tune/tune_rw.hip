@@ -98,6 +98,8 @@ int main(int argc, char** argv) {
   const uint64_t SB = 1536;  // buffer bytes per group (any slot <= 1536)
   // TUNE_RW_PALIGN=16: payloads on 16-B boundaries (the payload arena's layout)
   const uint64_t palign = getenv("TUNE_RW_PALIGN") ? (uint64_t)atoi(getenv("TUNE_RW_PALIGN")) : 1u;
+  // TUNE_RW_OUT16 (with packed_out): output rows back to back on 16-B boundaries
+  const bool out16 = getenv("TUNE_RW_OUT16") != nullptr;
   uint64_t out_pos = 0;
   const uint64_t seed = 0x51554944;
   std::vector<uint32_t> ptr{0};
@@ -124,7 +126,7 @@ int main(int argc, char** argv) {
     rec_alg += sm + 2.0 * mx;
     ptr.push_back((uint32_t)len.size());
     poff[g] = packed_out ? out_pos : g * slot;
-    out_pos += mx;
+    out_pos += out16 ? (mx + 15u) / 16u * 16u : mx;
   }
   uint8_t* data;
   CK(hipMalloc(&data, bytes + 4096));
@@ -312,6 +314,22 @@ int main(int argc, char** argv) {
                   hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, AL>),      \
                                      dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0);      \
                 }})
+#define RG_BLOCKD(REC, DG, NAME)                                                               \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, DG>), \
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0);      \
+                }})
+  if (getenv("TUNE_RW_BLOCKD")) {  // the block kernel without its parity stores
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(false, 0, "block product");
+      RG_BLOCKD(false, 1, "block nostore (not exact)");
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(true, 0, "block product");
+      RG_BLOCKD(true, 1, "block nostore (not exact)");
+    }
+  }
   if (getenv("TUNE_RW_BLOCKAL")) {  // aligned in-place tail loads (AL) on and off
     for (int rep = 0; rep < 2; ++rep) {
       RG_BLOCKA(false, false, "block AL0");
@@ -414,7 +432,8 @@ int main(int argc, char** argv) {
                          getenv("TUNE_RW_SPLIT") != nullptr ||
                          getenv("TUNE_RW_PERSIST2") != nullptr || getenv("TUNE_RW_BLOCK") != nullptr ||
                          getenv("TUNE_RW_BLOCK2") != nullptr ||
-                         getenv("TUNE_RW_BLOCK3") != nullptr || getenv("TUNE_RW_BLOCKAL") != nullptr;
+                         getenv("TUNE_RW_BLOCK3") != nullptr || getenv("TUNE_RW_BLOCKAL") != nullptr ||
+                         getenv("TUNE_RW_BLOCKD") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
@@ -580,7 +599,7 @@ int main(int argc, char** argv) {
   std::printf("k %u..%u, len %u..%u, %llu groups, %.3f GB packet buffer (payloads on %llu-B "
               "boundaries), parity slots %s %llu\n", kmin,
               kmin + kspan - 1, lmin, lmin + lspan - 1, (unsigned long long)G, bytes / 1e9,
-              (unsigned long long)palign, packed_out ? "packed" : "stride",
+              (unsigned long long)palign, packed_out ? (out16 ? "packed16" : "packed") : "stride",
               (unsigned long long)(packed_out ? 0 : slot));
   std::printf("%-24s %10s %10s %8s\n", "variant", "med GB/s", "max GB/s", "%8TB/s");
   for (size_t i = 0; i < vs.size(); ++i) {
