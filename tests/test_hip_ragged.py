@@ -111,7 +111,9 @@ def test_ragged_synth_vs_oracle(ctx, align, slot):
     n = 20_000
     ks, ptr, ln, off = synth_batch(n, g0=77, align=align)
     total = int(off[-1] + ln[-1])
-    data_d = torch.zeros(total, dtype=torch.uint8, device=DEV)
+    # gaps between aligned payloads hold 0xA5: a last window loaded in place
+    # (ragged_block_kernel AL) must mask them, not rely on zeros
+    data_d = torch.full((total,), 0xA5, dtype=torch.uint8, device=DEV)
     ctx.synth_ragged(data_d, dview(off), dview(ln), dview(ptr), 77, n, Q.SEED_RAGGED)
     ctx.sync()
     data = data_d.cpu().numpy()

@@ -135,6 +135,7 @@ int main(int argc, char** argv) {
   uint32_t* d_ptr = up(ptr);
   uint64_t* d_poff = up(poff);
   uint8_t* d_miss = up(miss);
+  CK(hipMemset(data, 0, bytes + 4096));  // gaps between aligned payloads: zero (BLOCKZ)
   CK(qfec::launch_synth_ragged(data, d_off, d_len, d_ptr, 0, G, seed, 0));
   uint8_t *par, *out, *chk;
   uint16_t *plen, *plen2;
@@ -320,6 +321,37 @@ int main(int argc, char** argv) {
                   hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, DG>), \
                                      dim3((uint32_t)((G + 7) / 8)), dim3(256), 0, 0, a0);      \
                 }})
+  // the block kernel at BPC blocks per CU (dynamic LDS padding; static LDS
+  // ~19 KB allows 8)
+#define RG_BLOCKO(REC, BPC, NAME)                                                              \
+  vs.push_back({std::string(NAME) + (REC ? " recover" : " encode"), REC,                      \
+                [=](const RaggedArgs& a0) {                                                    \
+                  static size_t stat = 0;                                                      \
+                  if (!stat) {                                                                 \
+                    hipFuncAttributes fa;                                                      \
+                    CK(hipFuncGetAttributes(&fa, (const void*)qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, 0>)); \
+                    stat = fa.sharedSizeBytes;                                                 \
+                  }                                                                            \
+                  const size_t pad = (160u << 10) / BPC - stat - 256;                          \
+                  hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, 0>), \
+                                     dim3((uint32_t)((G + 7) / 8)), dim3(256), pad, 0, a0);    \
+                }})
+  // TUNE_RW_BLOCKZ (round 3, profiles/round3/ragged_align/blockz.txt) ran a
+  // DIAG 2 build of ragged_block_kernel (zero-padded 16-B payload slots, every
+  // window loaded whole, no tail shift / mask): -1%, removed.
+  if (getenv("TUNE_RW_BLOCKO")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(false, 0, "block product");
+      RG_BLOCKO(false, 7, "block 7/CU");
+      RG_BLOCKO(false, 6, "block 6/CU");
+      RG_BLOCKO(false, 5, "block 5/CU");
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(true, 0, "block product");
+      RG_BLOCKO(true, 7, "block 7/CU");
+      RG_BLOCKO(true, 6, "block 6/CU");
+    }
+  }
   if (getenv("TUNE_RW_BLOCKD")) {  // the block kernel without its parity stores
     for (int rep = 0; rep < 2; ++rep) {
       RG_BLOCKD(false, 0, "block product");
@@ -433,7 +465,7 @@ int main(int argc, char** argv) {
                          getenv("TUNE_RW_PERSIST2") != nullptr || getenv("TUNE_RW_BLOCK") != nullptr ||
                          getenv("TUNE_RW_BLOCK2") != nullptr ||
                          getenv("TUNE_RW_BLOCK3") != nullptr || getenv("TUNE_RW_BLOCKAL") != nullptr ||
-                         getenv("TUNE_RW_BLOCKD") != nullptr;
+                         getenv("TUNE_RW_BLOCKD") != nullptr || getenv("TUNE_RW_BLOCKO") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
