@@ -1,8 +1,3 @@
-mkdir -p gpurun_out/pal
-timeout -k 10 400 python -u bench.py --protect-only > gpurun_out/pal/bench_protect.json 2> gpurun_out/pal/bench_protect.err; rc=$?; python - <<'PY'
-import json
-d=json.loads(open('gpurun_out/pal/bench_protect.json').read().strip().splitlines()[-1])
-p=d.get('protect', d)
-print({k:v for k,v in p.items() if k.startswith('encrypt')})
-PY
-exit $rc
+mkdir -p gpurun_out/win
+export TUNE_RW_PALIGN=16
+TUNE_RW_WINAL=1 timeout -k 10 200 tools/tune/build/tune_rw 10 5 5 11 64 1287 0 1536 > gpurun_out/win/winal.txt 2>&1; rc=$?; tail -n 14 gpurun_out/win/winal.txt; exit $rc

@@ -339,6 +339,17 @@ int main(int argc, char** argv) {
   // TUNE_RW_BLOCKZ (round 3, profiles/round3/ragged_align/blockz.txt) ran a
   // DIAG 2 build of ragged_block_kernel (zero-padded 16-B payload slots, every
   // window loaded whole, no tail shift / mask): -1%, removed.
+  if (getenv("TUNE_RW_WINAL")) {  // parity-window form (one wave per group) vs block, aligned payloads
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(false, 0, "block product");
+      vs.push_back({"window PB16 encode", false, [=](const RaggedArgs& a) { launch_win<false, 16>(a, G); }});
+      vs.push_back({"window PB8 encode", false, [=](const RaggedArgs& a) { launch_win<false, 8>(a, G); }});
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      RG_BLOCKD(true, 0, "block product");
+      vs.push_back({"window PB16 recover", true, [=](const RaggedArgs& a) { launch_win<true, 16>(a, G); }});
+    }
+  }
   if (getenv("TUNE_RW_BLOCKO")) {
     for (int rep = 0; rep < 2; ++rep) {
       RG_BLOCKD(false, 0, "block product");
@@ -465,7 +476,8 @@ int main(int argc, char** argv) {
                          getenv("TUNE_RW_PERSIST2") != nullptr || getenv("TUNE_RW_BLOCK") != nullptr ||
                          getenv("TUNE_RW_BLOCK2") != nullptr ||
                          getenv("TUNE_RW_BLOCK3") != nullptr || getenv("TUNE_RW_BLOCKAL") != nullptr ||
-                         getenv("TUNE_RW_BLOCKD") != nullptr || getenv("TUNE_RW_BLOCKO") != nullptr;
+                         getenv("TUNE_RW_BLOCKD") != nullptr || getenv("TUNE_RW_BLOCKO") != nullptr ||
+                         getenv("TUNE_RW_WINAL") != nullptr;
   // phased (ragged_phase_kernel): waves per CU x slots per wave
   uint32_t* psync;
   CK(hipMalloc(&psync, 20 * 256));
