@@ -199,3 +199,29 @@ def test_cpu_multithread_equals_single():
     p2 = np.zeros_like(p1)
     assert OC.lib().qo_encode_fixed_mt(OC._p(rows), k, L, n, OC._p(p2), 4) == 0
     assert np.array_equal(p1, p2)
+
+
+def test_ragged_layout_alignment():
+    """bench.py's configs[3] layouts: the same groups and lengths, payloads
+    byte-packed (align=1) or on 16-B boundaries with gaps < 16 B (align=16,
+    the payload arena's rounding); parity over the aligned layout equals the
+    packed one (gap bytes are never read)."""
+    from libquic_amd import synth
+    n = 500
+    ks1, p1, l1, o1 = synth.ragged_layout(0, n, 5, 15, 64, 1350, synth.SEED_RAGGED, align=1)
+    ks2, p2, l2, o2 = synth.ragged_layout(0, n, 5, 15, 64, 1350, synth.SEED_RAGGED, align=16)
+    assert np.array_equal(ks1, ks2) and np.array_equal(p1, p2) and np.array_equal(l1, l2)
+    assert np.array_equal(o1[1:] - o1[:-1], l1[:-1].astype(np.uint64))
+    assert not (o2 % np.uint64(16)).any()
+    gap = (o2[1:] - o2[:-1]).astype(np.int64) - l2[:-1].astype(np.int64)
+    assert gap.min() >= 0 and gap.max() < 16
+    rng = np.random.default_rng(3)
+    d1 = rng.integers(0, 256, int(o1[-1]) + int(l1[-1]), dtype=np.uint8)
+    d2 = rng.integers(0, 256, int(o2[-1]) + int(l2[-1]), dtype=np.uint8)  # gaps: noise
+    for q in range(l1.size):
+        d2[int(o2[q]):int(o2[q]) + int(l2[q])] = d1[int(o1[q]):int(o1[q]) + int(l1[q])]
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1536)
+    rc1, par1, pl1 = OC.encode_ragged(d1, o1, l1, p1, poff, n * 1536)
+    rc2, par2, pl2 = OC.encode_ragged(d2, o2, l2, p2, poff, n * 1536)
+    assert rc1 == 0 and rc2 == 0
+    assert np.array_equal(pl1, pl2) and np.array_equal(par1, par2)
