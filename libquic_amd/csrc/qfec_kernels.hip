@@ -199,6 +199,12 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
 // raises an abandon flag and every workgroup stops waiting for the rest of the
 // launch; results are identical either way.
 constexpr int kPhSteps = 40;         // 40 x 256 lanes x 16 B = 160 KiB of LDS
+// k = 10 (the headline shape): 32 more steps per phase held in VGPRs (one
+// wave per SIMD has the register file to itself): 19 phases instead of 35 at
+// 2^20 groups, encode +1.6% / recover +0.6% (tools/tune/tune_phase.hip "40+32",
+// profiles/round3/phase/tune_phase_rs*.txt; 40 + 40 / 48 / 64 spill into
+// AGPRs and lose).
+constexpr int kPhRegSteps = 32;
 constexpr int kPhUDefault = 1;       // steps loaded together (k loads in flight per lane)
 constexpr uint64_t kPhTimeout = 20000;  // s_memrealtime ticks (100 MHz): 200 us
 
@@ -267,13 +273,20 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
 // with the lost row's lanes masked off: 17 loads and 22 exec branches per step
 // instead of 18 and 32) +2.5% recover, 0.780 vs 0.761 on six buffer pairs
 // (profiles/round2/phase/tune_phase_compact.txt).
+// RS (encode, tools/tune): RS more steps per phase held in registers after the
+// STEPS LDS ones (a longer phase, fewer meetings; one wave per SIMD leaves the
+// register file to spare).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
-          bool NTLD = true, bool EDGE = false, bool COMPACT = true>
+          bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
   static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
+  static_assert(RS == 0 || (KC > 0 && kPhU == 1 && !XCDW && RS <= 64 &&
+                            (!RECOVER || (PARFIRST && COMPACT))),
+                "register steps: templated k, one step at a time (recover: parity first, compact)");
+  constexpr int TS = STEPS + RS;  // steps per phase
   __shared__ u32x4 s_par[STEPS][NTHR];  // lane tid's parity of each step
   const uint32_t tid = threadIdx.x, gl = tid / C, t = tid - gl * C;
   const bool lane_on = gl < gpb;
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     // XCDW: the workgroups of one XCD (b, b+8, ...) take one contiguous share
     // of the window, so the lines two neighbouring groups share stay in one L2
     const uint64_t wb = XCDW ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t base = ((uint64_t)p * (STEPS / kPhU) * B + wb) * (gpb * kPhU) + gl;
+    const uint64_t base = ((uint64_t)p * (TS / kPhU) * B + wb) * (gpb * kPhU) + gl;
     // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
     // 32-bit shifts only, STEPS <= 64)
     uint32_t bad_lo = 0, bad_hi = 0;
@@ -296,6 +309,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     };
     // recover: the lost-slot indices of the next steps are loaded one
     // iteration ahead (every row address depends on them)
+    uint32_t m_reg[RS > 0 && RECOVER ? RS : 1];  // register steps' lost slots, loaded early
+    if constexpr (RS > 0 && RECOVER) {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const uint64_t g = gidx(STEPS + j);
+        m_reg[j] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
+      }
+    }
     uint32_t m_next[kPhU];
     if constexpr (RECOVER) {
 #pragma unroll
@@ -429,8 +450,57 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
       for (int u = 0; u < kPhU; ++u) s_par[i + u][tid] = acc[u];
     }
+    u32x4 racc[RS > 0 ? RS : 1];
+    uint32_t ron[2] = {0u, 0u};  // step j's lane is on: bit j % 32 of word j / 32
+    bool rbad = false;           // recover: a register step's lost slot out of range
+    if constexpr (RS > 0) {
+      // one live row address, advanced step by step (the compiler would
+      // otherwise keep every step's address live across the unrolled steps)
+      const uint64_t g0r = gidx(STEPS);
+      const uint8_t* q = a.rows + g0r * a.group_stride + off;
+      const uint64_t dq = B * gpb * a.group_stride;
+      const uint8_t* qp = RECOVER ? a.parity + g0r * a.parity_stride + off : nullptr;
+      const uint64_t dqp = RECOVER ? B * gpb * a.parity_stride : 0u;
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const uint64_t g = g0r + (uint64_t)j * B * gpb;
+        bool on = lane_on && g < a.n_groups;
+        u32x4 v[KC];
+        if constexpr (RECOVER) {
+          uint32_t mj = m_reg[j];
+          if (mj >= k) {  // out-of-range lost slot: the group is not stored
+            rbad = rbad || on;
+            on = false;
+            mj = 0u;
+          }
+          const uint8_t* qq = on ? q : a.rows + off;
+          // the parity row, then the k-1 received rows in order (compact)
+          v[0] = ld16t<NTLD>(on ? qp : a.parity + off);
+#pragma unroll
+          for (int r = 0; r + 1 < KC; ++r)
+            v[r + 1] = ld16t<NTLD>(qq + ((uint32_t)r + ((uint32_t)r >= mj ? 1u : 0u)) * a.row_stride);
+        } else {
+          const uint8_t* qq = on ? q : a.rows + off;
+#pragma unroll
+          for (int r = 0; r < KC; ++r) v[r] = ld16t<NTLD>(qq + r * a.row_stride);
+        }
+        ron[j / 32] |= on ? 1u << (j % 32) : 0u;
+        u32x4 x = v[0];
+#pragma unroll
+        for (int r = 1; r < KC; ++r) x ^= v[r];
+        racc[j] = x;
+        q += dq;
+        // the next step's address waits for this step's XOR: one step's k
+        // loads in flight, as in the LDS steps
+        asm volatile("" : "+v"(q) : "v"(x));
+        if constexpr (RECOVER) {
+          qp += dqp;
+          asm volatile("" : "+v"(qp) : "v"(x));
+        }
+      }
+    }
     if constexpr (RECOVER) {
-      if ((bad_lo | bad_hi) != 0u && t == 0u) atomicOr(a.err, kErrMissingIndex);
+      if (((bad_lo | bad_hi) != 0u || rbad) && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
     phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
 #pragma unroll 4
@@ -439,6 +509,13 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
       const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
       if (lane_on && g < a.n_groups && !skip)
         st16t<true>(a.out + g * a.out_stride + off, s_par[i][tid]);
+    }
+    if constexpr (RS > 0) {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const uint64_t g = gidx(STEPS + j);
+        if ((ron[j / 32] >> (j % 32)) & 1u) st16t<true>(a.out + g * a.out_stride + off, racc[j]);
+      }
     }
     if constexpr (MEET2) phase_meet(a.phase_sync, 2u * p + 2u);
   }
@@ -1669,9 +1746,13 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
     QFEC_K_CASE(4)
     QFEC_K_CASE(5)
     QFEC_K_CASE(8)
-    QFEC_K_CASE(10)
     QFEC_K_CASE(16)
 #undef QFEC_K_CASE
+    case 10:  // the headline shape: kPhRegSteps more steps per phase in registers
+      hipLaunchKernelGGL((phase_xor_kernel<10, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
+                                           false, true, true, false, true, kPhRegSteps>),
+                         dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
+      break;
     default:
       hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C,
                          gpb, nphase);
@@ -1695,11 +1776,14 @@ constexpr uint32_t kPhMinPhases = 6;
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
   if (a.ncu == 0) return false;
   const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
+  // the threshold counts phases of the LDS steps alone (the measured band);
+  // the launch's phases hold the register steps too (k = 10)
   const uint64_t per = (uint64_t)wg * kPhSteps * gpb;
   const uint64_t np = (a.n_groups + per - 1) / per;
   if (np < (a.phase_min ? a.phase_min : kPhMinPhases) || np > 0xFFFFFFFFull) return false;
+  const uint64_t per_l = (uint64_t)wg * (kPhSteps + (a.k == 10u ? kPhRegSteps : 0u)) * gpb;
   *grid = wg;
-  *nphase = (uint32_t)np;
+  *nphase = (uint32_t)((a.n_groups + per_l - 1) / per_l);
   return true;
 }
 

@@ -1,3 +1,3 @@
-mkdir -p gpurun_out/win
-export TUNE_RW_PALIGN=16
-TUNE_RW_WINAL=1 timeout -k 10 200 tools/tune/build/tune_rw 10 5 5 11 64 1287 0 1536 > gpurun_out/win/winal.txt 2>&1; rc=$?; tail -n 14 gpurun_out/win/winal.txt; exit $rc
+mkdir -p gpurun_out/rs2
+timeout -k 10 300 python -u -m pytest tests/test_hip_phase.py tests/test_hip_fixed.py -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/rs2/pytest.log 2>&1 && tail -3 gpurun_out/rs2/pytest.log &&
+timeout -k 10 300 tools/tune/build/tune_phase 5 3 > gpurun_out/rs2/tune_phase_rs2.txt 2>&1 && tail -n 22 gpurun_out/rs2/tune_phase_rs2.txt

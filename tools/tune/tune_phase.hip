@@ -294,6 +294,12 @@ int main(int argc, char** argv) {
       {"prod edge-dflt", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, true>},
       {"prod recover compact", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true>},
       {"prod recover masked", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, false>},
+      {"prod 256 x 40+32", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 32>},
+      {"prod recover 40+32", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32>},
+      {"prod recover 40+48", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 48>},
+      {"prod 256 x 40+40", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 40>},
+      {"prod 256 x 40+48", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 48>},
+      {"prod 256 x 40+64", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 64>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
@@ -331,6 +337,10 @@ int main(int argc, char** argv) {
     if (pks[w].first.find("256 x 32") != std::string::npos) st = 32;
     if (pks[w].first.find("128 x 80") != std::string::npos) nt = 128, st = 80;
     if (pks[w].first.find("192 x 53") != std::string::npos) nt = 192, st = 53;
+    if (pks[w].first.find("40+32") != std::string::npos) st = 72;
+    if (pks[w].first.find("40+40") != std::string::npos) st = 80;
+    if (pks[w].first.find("40+48") != std::string::npos) st = 88;
+    if (pks[w].first.find("40+64") != std::string::npos) st = 104;
     const uint32_t gpb = nt / 85u, grid = ncu * bpc;
     const uint64_t per = (uint64_t)grid * st * gpb;
     const uint32_t nph = (uint32_t)((G + per - 1) / per);
