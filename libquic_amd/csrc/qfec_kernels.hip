@@ -278,7 +278,7 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
 // register file to spare).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
-          bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0>
+          bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0, bool RPF = false>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
@@ -461,6 +461,16 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
       const uint64_t dq = B * gpb * a.group_stride;
       const uint8_t* qp = RECOVER ? a.parity + g0r * a.parity_stride + off : nullptr;
       const uint64_t dqp = RECOVER ? B * gpb * a.parity_stride : 0u;
+      if constexpr (RECOVER && RPF) {
+        // RPF: every register step's parity row first (one stream, as the
+        // LDS steps' PARFIRST), then the received rows step by step
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          const uint64_t g = g0r + (uint64_t)j * B * gpb;
+          const bool on = lane_on && g < a.n_groups;
+          racc[j] = ld16t<NTLD>(a.parity + (on ? g : 0) * a.parity_stride + off);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = g0r + (uint64_t)j * B * gpb;
@@ -475,7 +485,8 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
           }
           const uint8_t* qq = on ? q : a.rows + off;
           // the parity row, then the k-1 received rows in order (compact)
-          v[0] = ld16t<NTLD>(on ? qp : a.parity + off);
+          if constexpr (RPF) v[0] = racc[j];
+          else v[0] = ld16t<NTLD>(on ? qp : a.parity + off);
 #pragma unroll
           for (int r = 0; r + 1 < KC; ++r)
             v[r + 1] = ld16t<NTLD>(qq + ((uint32_t)r + ((uint32_t)r >= mj ? 1u : 0u)) * a.row_stride);

@@ -296,10 +296,9 @@ int main(int argc, char** argv) {
       {"prod recover masked", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, false>},
       {"prod 256 x 40+32", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 32>},
       {"prod recover 40+32", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32>},
-      {"prod recover 40+48", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 48>},
-      {"prod 256 x 40+40", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 40>},
+      {"prod recover 40+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
+      {"prod recover 40+24 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 24, true>},
       {"prod 256 x 40+48", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 48>},
-      {"prod 256 x 40+64", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 64>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
   uint8_t* d_miss;
@@ -338,6 +337,7 @@ int main(int argc, char** argv) {
     if (pks[w].first.find("128 x 80") != std::string::npos) nt = 128, st = 80;
     if (pks[w].first.find("192 x 53") != std::string::npos) nt = 192, st = 53;
     if (pks[w].first.find("40+32") != std::string::npos) st = 72;
+    if (pks[w].first.find("40+24") != std::string::npos) st = 64;
     if (pks[w].first.find("40+40") != std::string::npos) st = 80;
     if (pks[w].first.find("40+48") != std::string::npos) st = 88;
     if (pks[w].first.find("40+64") != std::string::npos) st = 104;
