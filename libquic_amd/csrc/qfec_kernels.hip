@@ -201,7 +201,8 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
 constexpr int kPhSteps = 40;         // 40 x 256 lanes x 16 B = 160 KiB of LDS
 // k = 10 (the headline shape): 32 more steps per phase held in VGPRs (one
 // wave per SIMD has the register file to itself): 19 phases instead of 35 at
-// 2^20 groups, encode +1.6% / recover +0.6% (tools/tune/tune_phase.hip "40+32",
+// 2^20 groups, encode +1.6%; recover +0.1-1.3%, +1.7% with the register
+// steps' parity rows loaded first (RPF) (tools/tune/tune_phase.hip "40+32",
 // profiles/round3/phase/tune_phase_rs*.txt; 40 + 40 / 48 / 64 spill into
 // AGPRs and lose).
 constexpr int kPhRegSteps = 32;
@@ -1761,7 +1762,7 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
 #undef QFEC_K_CASE
     case 10:  // the headline shape: kPhRegSteps more steps per phase in registers
       hipLaunchKernelGGL((phase_xor_kernel<10, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
-                                           false, true, true, false, true, kPhRegSteps>),
+                                           false, true, true, false, true, kPhRegSteps, true>),
                          dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
       break;
     default:
