@@ -47,6 +47,9 @@ struct FixedArgs {
   // minimum phase count for the phased kernel (0: kPhMinPhases, about 184K
   // headline groups); test hook qfec_debug_phase_min, for the band study
   uint32_t phase_min = 0;
+  // steps per phase of the launch (set by launch_fixed: the batch spread
+  // evenly over its phases); 0 = the kernel's full phase
+  uint32_t phase_steps = 0;
 };
 
 // True if launch_fixed(a, nontemporal, ...) runs the phased kernel.

@@ -287,7 +287,11 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
   static_assert(RS == 0 || (KC > 0 && kPhU == 1 && !XCDW && RS <= 64 &&
                             (!RECOVER || (PARFIRST && COMPACT))),
                 "register steps: templated k, one step at a time (recover: parity first, compact)");
-  constexpr int TS = STEPS + RS;  // steps per phase
+  constexpr int TS = STEPS + RS;  // steps per phase (at most)
+  // the launch's steps per phase (launch_fixed spreads the batch evenly over
+  // its phases, so the last phase is not a sliver); the LDS steps come first
+  const int SP = (kPhU == 1 && a.phase_steps != 0u) ? min((int)a.phase_steps, TS) : TS;
+  const int NL = min(STEPS, SP);  // LDS steps in use
   __shared__ u32x4 s_par[STEPS][NTHR];  // lane tid's parity of each step
   const uint32_t tid = threadIdx.x, gl = tid / C, t = tid - gl * C;
   const bool lane_on = gl < gpb;
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     // XCDW: the workgroups of one XCD (b, b+8, ...) take one contiguous share
     // of the window, so the lines two neighbouring groups share stay in one L2
     const uint64_t wb = XCDW ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t base = ((uint64_t)p * (TS / kPhU) * B + wb) * (gpb * kPhU) + gl;
+    const uint64_t base = ((uint64_t)p * (uint64_t)(SP / kPhU) * B + wb) * (gpb * kPhU) + gl;
     // recover: steps whose lost-slot index is out of range (bit i of lo/hi:
     // 32-bit shifts only, STEPS <= 64)
     uint32_t bad_lo = 0, bad_hi = 0;
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = gidx(STEPS + j);
-        m_reg[j] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
+        m_reg[j] = lane_on && g < a.n_groups && STEPS + j < SP ? a.missing[g] : 0u;
       }
     }
     uint32_t m_next[kPhU];
@@ -334,8 +338,8 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         u32x4 w[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const uint64_t g = gidx(i + j < STEPS ? i + j : 0);
-          const bool on = i + j < STEPS && lane_on && g < a.n_groups;
+          const uint64_t g = gidx(i + j < NL ? i + j : 0);
+          const bool on = i + j < NL && lane_on && g < a.n_groups;
           w[j] = ld16t<NTLD>(a.parity + (on ? g : 0) * a.parity_stride + off);
         }
 #pragma unroll
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
       }
     }
 #pragma unroll 1
-    for (int i = 0; i < STEPS; i += kPhU) {
+    for (int i = 0; i < NL; i += kPhU) {
       u32x4 acc[kPhU];
       uint32_t m[kPhU];
       const uint8_t* src[kPhU];
@@ -440,7 +444,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         }
       }
       if constexpr (RECOVER) {
-        if (i + kPhU < STEPS) {
+        if (i + kPhU < NL) {
 #pragma unroll
           for (int u = 0; u < kPhU; ++u) {
             const uint64_t g = gidx(i + kPhU + u);
@@ -468,14 +472,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
         for (int j = 0; j < RS; ++j) {
           const uint64_t g = g0r + (uint64_t)j * B * gpb;
-          const bool on = lane_on && g < a.n_groups;
+          const bool on = lane_on && g < a.n_groups && STEPS + j < SP;
           racc[j] = ld16t<NTLD>(a.parity + (on ? g : 0) * a.parity_stride + off);
         }
       }
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = g0r + (uint64_t)j * B * gpb;
-        bool on = lane_on && g < a.n_groups;
+        bool on = lane_on && g < a.n_groups && STEPS + j < SP;
         u32x4 v[KC];
         if constexpr (RECOVER) {
           uint32_t mj = m_reg[j];
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     for (int i = 0; i < STEPS; ++i) {
       const uint64_t g = gidx(i);
       const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
-      if (lane_on && g < a.n_groups && !skip)
+      if (lane_on && g < a.n_groups && !skip && i < NL)
         st16t<true>(a.out + g * a.out_stride + off, s_par[i][tid]);
     }
     if constexpr (RS > 0) {
@@ -1799,6 +1803,13 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   return true;
 }
 
+// Steps per phase that spread n_groups evenly over nphase phases (a 393K-group
+// batch: 8 phases of 64 steps instead of 7 of 72 and one of 7).
+uint32_t phase_steps_for(const FixedArgs& a, uint32_t gpb, uint32_t grid, uint32_t nphase) {
+  const uint64_t per_step = (uint64_t)grid * gpb * nphase;
+  return (uint32_t)((a.n_groups + per_step - 1) / per_step);
+}
+
 }  // namespace
 
 bool fixed_uses_phases(const FixedArgs& a, bool nontemporal) {
@@ -1834,9 +1845,12 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   const uint32_t C = (a0.L + 15u) / 16u;  // <= 91 for L <= 1452
   const uint32_t gpb = kBlock / C;         // whole groups per workgroup (>= 2)
   uint32_t grid = 0, nphase = 0;
-  if (a0.phase_sync && nontemporal && phase_plan(a0, gpb, &grid, &nphase))
-    return recover ? launch_phase_k<true>(a0, C, gpb, grid, nphase, s)
-                   : launch_phase_k<false>(a0, C, gpb, grid, nphase, s);
+  if (a0.phase_sync && nontemporal && phase_plan(a0, gpb, &grid, &nphase)) {
+    FixedArgs a = a0;
+    a.phase_steps = phase_steps_for(a0, gpb, grid, nphase);
+    return recover ? launch_phase_k<true>(a, C, gpb, grid, nphase, s)
+                   : launch_phase_k<false>(a, C, gpb, grid, nphase, s);
+  }
   const uint64_t maxg = kMaxBlocks256 * gpb;
   for (uint64_t g = 0; g < a0.n_groups; g += maxg) {
     FixedArgs a = a0;
