@@ -1,2 +1,2 @@
-mkdir -p gpurun_out/band2
-timeout -k 10 400 python -u tools/phase_band.py 10 > gpurun_out/band2/phase_band_r3q.txt 2>&1; rc=$?; grep -v "^{" gpurun_out/band2/phase_band_r3q.txt | tail -n 14; exit $rc
+mkdir -p gpurun_out/rs6
+timeout -k 10 300 tools/tune/build/tune_phase 5 3 > gpurun_out/rs6/tune_phase_rs6.txt 2>&1; rc=$?; tail -n 22 gpurun_out/rs6/tune_phase_rs6.txt; exit $rc

@@ -297,7 +297,8 @@ int main(int argc, char** argv) {
       {"prod 256 x 40+32", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 32>},
       {"prod recover 40+32", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32>},
       {"prod recover 40+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
-      {"prod recover 40+24 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 24, true>},
+      {"prod recover 40+48 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 48, true>},
+      {"prod 256 x 40+56", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 56>},
       {"prod 256 x 40+48", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 48>},
   };
   pks.push_back({"prod recover one-pass", nullptr});
@@ -337,7 +338,7 @@ int main(int argc, char** argv) {
     if (pks[w].first.find("128 x 80") != std::string::npos) nt = 128, st = 80;
     if (pks[w].first.find("192 x 53") != std::string::npos) nt = 192, st = 53;
     if (pks[w].first.find("40+32") != std::string::npos) st = 72;
-    if (pks[w].first.find("40+24") != std::string::npos) st = 64;
+    if (pks[w].first.find("40+56") != std::string::npos) st = 96;
     if (pks[w].first.find("40+40") != std::string::npos) st = 80;
     if (pks[w].first.find("40+48") != std::string::npos) st = 88;
     if (pks[w].first.find("40+64") != std::string::npos) st = 104;
@@ -345,6 +346,8 @@ int main(int argc, char** argv) {
     const uint64_t per = (uint64_t)grid * st * gpb;
     const uint32_t nph = (uint32_t)((G + per - 1) / per);
     (void)pnph;
+    // the product spreads the batch evenly over its phases (launch_fixed)
+    a.phase_steps = (uint32_t)((G + (uint64_t)grid * gpb * nph - 1) / ((uint64_t)grid * gpb * nph));
     if (pks[w].second)
       hipLaunchKernelGGL(pks[w].second, dim3(grid), dim3(nt), 0, 0, a, 85u, gpb, nph);
     else
