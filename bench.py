@@ -331,8 +331,9 @@ def phased_default(G, k, L, args):
 def fixed_kernel_name(k, phased):
     """The encode kernel the line's roofline is about (libquic_amd/csrc/qfec_kernels.hip)."""
     if phased:
+        steps = "40 LDS + 32 register steps" if k == 10 else "40 LDS steps"
         return (f"phase_xor_kernel<{k}, false> (encode, k={k}, nt; one workgroup per CU, "
-                f"reads and parity writes in separate grid-wide phases)")
+                f"reads and parity writes in separate grid-wide phases of {steps})")
     return f"fixed_xor_kernel<{k}, false, true, false, false> (encode, k={k}, nt, one pass)"
 
 
