@@ -316,16 +316,11 @@ def timed_steps(work, steps, warmup, barrier, reduce_max):
     return elapsed, events
 
 
-def phased_default(G, k, L, args):
-    """Whether the library runs the phased kernel for this batch (the rule of
-    phase_plan in qfec_kernels.hip: nt, L >= 16, at least 8 phases of
-    CUs x 40 steps x floor(256 / ceil(L/16)) groups)."""
-    if args.cached or args.one_pass or args.cpu_workload or L < 16:
-        return False
-    import torch
-    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    per = ncu * 40 * (256 // ((L + 15) // 16))
-    return -(-G // per) >= 8
+def phased_used(work, cpu):
+    """Whether the timed fixed-shape launches ran the phased kernel, as the
+    library reports it (qfec_last_fixed_phased: its size rule, kPhMinPhases in
+    qfec_kernels.hip, and its contention backoff), not a copy of that rule."""
+    return (not cpu) and work.ctx.last_fixed_phased() == 1
 
 
 def fixed_kernel_name(k, phased):
@@ -533,11 +528,12 @@ def main(argv=None):
         rec_s = max(r["rec_s"] for r in per_rank)
     if verified is not None:
         verified = all(r["verified"] for r in per_rank)
+    phased = phased_used(work, cpu)
     line = result_line(world, args.steps, args.warmup, elapsed, G, k, L, work.bytes_encode,
                        work.bytes_recover, enc_s, rec_s,
-                       measured_traffic(G, k, L, phased_default(G, k, L, args)), verified,
-                       kernel=fixed_kernel_name(k, phased_default(G, k, L, args)))
-    if line["roofline"] and not cpu and phased_default(G, k, L, args):
+                       measured_traffic(G, k, L, phased), verified,
+                       kernel=fixed_kernel_name(k, phased))
+    if line["roofline"] and phased:
         # phased launches that gave up their meetings (should be 0 on an idle GPU)
         line["roofline"]["phase_abandons"] = work.ctx.phase_abandons()
     if world > 1 and line["roofline"]:
@@ -561,7 +557,7 @@ def main(argv=None):
         # the ragged kernels' launches for the rocprofv3 runs (tools/pmc.sh)
         work.release()
         line["ragged"] = bench_ragged(work.ctx, torch, dev, work.stream, steps=3)
-    if extras and not args.one_pass and phased_default(G, k, L, args):
+    if extras and not args.one_pass and phased:
         # the same steps with the one-pass kernel (QFEC_ONE_PASS), same buffers
         work.one_pass = True
         _, ev1 = timed_steps(work, args.steps, 1, barrier, reduce_max)

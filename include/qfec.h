@@ -146,6 +146,15 @@ int qfec_sync(qfec_ctx* ctx);
  * running.  Returns the first error of the calls it finished (the same codes
  * the synchronous call would have returned), else QFEC_OK. */
 int qfec_complete(qfec_ctx* ctx, int wait);
+/* The ticket of the last ragged call on this context if it was queued
+ * asynchronously (QFEC_ASYNC honoured), else 0. */
+uint64_t qfec_async_ticket(const qfec_ctx* ctx);
+/* Finish ONE queued op: wait blocks, otherwise QFEC_PENDING while it runs.
+ * Returns that op's own code only (an op finished early by another call --
+ * its staging slot reused, a synchronous call -- keeps its code for this);
+ * QFEC_ERR_INTERNAL for an unknown or already completed ticket.
+ * qfec_complete still finishes every op and claims every kept code. */
+int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait);
 const char* qfec_strerror(int code);
 /* Pinned, device-mapped host memory for QFEC_PTR_MAPPED payloads (the
  * registered receive / send buffers of a QUIC server: the GPU reads packets
@@ -374,6 +383,11 @@ int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count);
  * context then uses the one-pass kernel for the next 16 such batches and
  * tries the phased one again).  -1 for a null context. */
 int qfec_phase_backoff(qfec_ctx* ctx);
+/* Which kernel the context's last device-pointer fixed-shape call ran: 1 the
+ * phased kernel, 0 the one-pass kernel, -1 none yet (or a null context).
+ * The measurement names its roofline kernel from this, not from a copy of
+ * the library's size rule. */
+int qfec_last_fixed_phased(const qfec_ctx* ctx);
 /* Test hook: launch `extra` workgroups beyond one per CU in phased launches
  * (0..64; they cannot all be resident, so the first meeting times out — the
  * abandon path; the backoff does not apply while extra > 0), and with

@@ -43,17 +43,21 @@ LIB = os.path.join(OUT, "libquic_fec_patched.so")
 PATCHED = ["quic_protocol.h", "quic_protocol.cc", "quic_framer.h", "quic_framer.cc",
            "quic_connection_stats.h", "quic_connection_stats.cc",
            "quic_packet_creator.h", "quic_packet_creator.cc", "quic_packet_generator.h",
-           "quic_connection.h", "quic_connection.cc"]
+           "quic_connection.h", "quic_connection.cc", "quic_received_packet_manager.h",
+           "quic_received_packet_manager.cc", "quic_sent_packet_manager.h",
+           "quic_sent_packet_manager.cc"]
 FEC_HOST = ["quic_fec_group.h", "quic_fec_group.cc", "quic_fec_wire.h", "quic_fec_wire.cc",
             "quic_fec_connection.h", "quic_fec_connection.cc"]
 # translation units syntax-checked against the reference headers
 SYNTAX_UNITS = ["quic_protocol.cc", "quic_framer.cc", "quic_packet_creator.cc",
-                "quic_connection.cc", "quic_fec_group.cc", "quic_fec_wire.cc",
+                "quic_connection.cc", "quic_received_packet_manager.cc",
+                "quic_sent_packet_manager.cc", "quic_fec_group.cc", "quic_fec_wire.cc",
                 "quic_fec_connection.cc"]
 # linked: the patched units + the FEC host code (from _build) and, unmodified
 # from the reference tree, what the framer and the packet creator reach
 LINK_PATCHED = ["quic_protocol.cc", "quic_framer.cc", "quic_packet_creator.cc",
                 "quic_connection.cc", "quic_connection_stats.cc",
+                "quic_received_packet_manager.cc", "quic_sent_packet_manager.cc",
                 "quic_fec_group.cc", "quic_fec_wire.cc", "quic_fec_connection.cc"]
 LINK_REF = [
     "net/quic/core/crypto/quic_decrypter.cc", "net/quic/core/crypto/quic_encrypter.cc",
@@ -85,8 +89,7 @@ LINK_REF = [
     # UMA histograms), found by linking with -z defs until nothing is missing
     "net/quic/core/quic_alarm.cc", "net/quic/core/quic_bandwidth.cc",
     "net/quic/core/quic_clock.cc", "net/quic/core/quic_types.cc",
-    "net/quic/core/quic_packet_generator.cc", "net/quic/core/quic_received_packet_manager.cc",
-    "net/quic/core/quic_sent_entropy_manager.cc", "net/quic/core/quic_sent_packet_manager.cc",
+    "net/quic/core/quic_packet_generator.cc", "net/quic/core/quic_sent_entropy_manager.cc",
     "net/quic/core/quic_multipath_sent_packet_manager.cc",
     "net/quic/core/quic_unacked_packet_map.cc", "net/quic/core/quic_time.cc",
     "net/quic/core/quic_sustained_bandwidth_recorder.cc", "net/quic/core/quic_config.cc",
@@ -159,9 +162,19 @@ def syntax_check() -> list:
         return list(ex.map(one, SYNTAX_UNITS))
 
 
+def _inputs_mtime():
+    """Newest of what every unit may include beyond its own source: the patch
+    (it changes reference headers, e.g. QuicAckFrame's layout) and the FEC
+    host headers."""
+    hs = [PATCH] + [os.path.join(ROOT, "libquic_amd", "csrc", f) for f in FEC_HOST
+                    if f.endswith(".h")] + [os.path.join(ROOT, "include", "qfec.h")]
+    return max(os.path.getmtime(h) for h in hs)
+
+
 def _obj(src, flags, name, always=False):
     o = os.path.join(OUT, "obj", name + ".o")
-    if always or not os.path.exists(o) or os.path.getmtime(o) < os.path.getmtime(src):
+    if (always or not os.path.exists(o) or
+            os.path.getmtime(o) < max(os.path.getmtime(src), _inputs_mtime())):
         os.makedirs(os.path.dirname(o), exist_ok=True)
         subprocess.run([*flags, "-c", src, "-o", o], check=True)
     return o
@@ -190,6 +203,27 @@ def build_lib() -> str:
     return LIB
 
 
+def regen_patch() -> str:
+    """Maintainer step: rewrite integration/libquic_fec.patch from the edited
+    copies under _build/src (after prepare() and edits there), one
+    `diff -u` per PATCHED file against /root/reference, in file name order."""
+    out = []
+    for f in sorted(PATCHED):
+        rel = f"src/net/quic/core/{f}"
+        r = subprocess.run(["diff", "-u", "--label", "a/" + rel, "--label", "b/" + rel,
+                            os.path.join(REF, rel), os.path.join(CORE, f)],
+                           capture_output=True, text=True)
+        if r.returncode == 0:
+            continue
+        if r.returncode != 1:
+            raise RuntimeError(r.stderr)
+        out.append(f"diff --git a/{rel} b/{rel}\n" + r.stdout)
+    text = "".join(out)
+    with open(PATCH, "w") as fh:
+        fh.write(text)
+    return PATCH
+
+
 def build() -> bool:
     """prepare + syntax check + link; False where the reference is absent."""
     if not available():
@@ -204,6 +238,9 @@ def build() -> bool:
 
 
 if __name__ == "__main__":
+    if "--regen-patch" in sys.argv:
+        print("rewrote", regen_patch())
+        sys.exit(0)
     ok = build()
     print("integration build:", "ok" if ok else "skipped (no /root/reference)")
     sys.exit(0)

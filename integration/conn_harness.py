@@ -16,7 +16,8 @@ class Params(C.Structure):
     _fields_ = [("version", C.c_int32), ("n_pairs", C.c_int32), ("group_size", C.c_int32),
                 ("drop_every", C.c_int32), ("stream_len", C.c_uint64), ("batched", C.c_int32),
                 ("max_turns", C.c_int32), ("fail_encode", C.c_int32),
-                ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("reorder", C.c_int32)]
+                ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("reorder", C.c_int32),
+                ("inject_unencrypted_fec", C.c_int32), ("close_mid_batch", C.c_int32)]
 
 
 _U64 = ("data_packets_sent fec_packets_sent dropped revived groups_one_loss fec_groups_skipped "
@@ -30,7 +31,12 @@ class Result(C.Structure):
                  ("cpu_xor_groups", C.c_uint64), ("streams_ok", C.c_int32),
                  ("connected", C.c_int32), ("status", C.c_int32), ("detail", C.c_char * 256),
                  ("fec_wait_us", C.c_double), ("fec_launch_us", C.c_double),
-                 ("debug_revived", C.c_uint64)])
+                 ("debug_revived", C.c_uint64)] +
+                [(n, C.c_uint64) for n in ("revived_reported acks_with_revived "
+                                           "retransmitted_after_report retransmitted_of_revived "
+                                           "protected_entropy_set").split()] +
+                [(n, C.c_int32) for n in ("server_close_error client_close_error "
+                                          "peer_saw_close closed_with_pending").split()])
 
 
 _lib = None
@@ -49,12 +55,14 @@ def lib():
 
 def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True,
         max_turns=20_000, fail_encode=False, require_gpu=False, version=31,
-        end_flush=True, reorder=0) -> dict:
+        end_flush=True, reorder=0, inject_unencrypted_fec=False, close_mid_batch=0) -> dict:
     """One simulated run; returns the result fields as a dict."""
     p = Params(version=version, n_pairs=n_pairs, group_size=group_size, drop_every=drop_every,
                stream_len=stream_len, batched=int(batched), max_turns=max_turns,
                fail_encode=int(fail_encode), require_gpu=int(require_gpu),
-               no_end_flush=int(not end_flush), reorder=reorder)
+               no_end_flush=int(not end_flush), reorder=reorder,
+               inject_unencrypted_fec=int(inject_unencrypted_fec),
+               close_mid_batch=close_mid_batch)
     r = Result()
     lib().fec_conn_run(C.byref(p), C.byref(r))
     out = {n: getattr(r, n) for n, _ in Result._fields_}

@@ -39,6 +39,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,9 @@ struct fec_conn_params {
   int32_t no_end_flush; // 1: no SendFecPacketNow at the end (partial groups: FEC alarm only)
   int32_t reorder;       // R > 0: client->server packets reordered (adjacent pairs
                          // swapped, about one in R held back a turn)
+  int32_t inject_unencrypted_fec;  // 1: client 0 also sends an FEC packet at ENCRYPTION_NONE
+  int32_t close_mid_batch;  // T > 0: from turn T, client 0 closes its connection while
+                            // one of its FEC packets is pending in the batcher
 };
 
 struct fec_conn_result {
@@ -99,6 +103,16 @@ struct fec_conn_result {
   double fec_wait_us;           // of fec_host_us: blocked waiting for the device (Complete(true))
   double fec_launch_us;         // of fec_host_us: the batcher's Launch (tables + queueing)
   uint64_t debug_revived;       // QuicConnectionDebugVisitor::OnRevivedPacket calls (servers)
+  // the v<=31 ack's revived-packets list and the packets' entropy bits
+  uint64_t revived_reported;    // distinct packets clients saw listed as revived in acks
+  uint64_t acks_with_revived;   // acks (clients received) listing any revived packet
+  uint64_t retransmitted_after_report;  // retransmissions of a packet already reported revived
+  uint64_t retransmitted_of_revived;    // retransmissions of packets the servers revived
+  uint64_t protected_entropy_set;       // FEC-protected data packets sent with entropy bit 1
+  int32_t server_close_error;   // first server's QuicErrorCode if it closed, else 0
+  int32_t client_close_error;   // first client's QuicErrorCode if it closed, else 0
+  int32_t peer_saw_close;       // server 0 closed by the peer (close_mid_batch)
+  int32_t closed_with_pending;  // client 0 had a pending FEC packet when it closed
 };
 }
 
@@ -285,8 +299,30 @@ class RevivalCounter : public QuicConnectionDebugVisitor {
   void OnRevivedPacket(const QuicPacketHeader& header, base::StringPiece payload) override {
     ++count;
     bytes += payload.size();
+    revived.insert(header.packet_number);
   }
   uint64_t count = 0, bytes = 0;
+  std::set<QuicPacketNumber> revived;  // this server's revived packet numbers
+};
+
+// The sender's view of the revived-packets list (one per client): every
+// revived packet an ack reported, and every retransmission it sent after
+// that report (MarkPacketNotRetransmittable should leave none).
+class AckWatch : public QuicConnectionDebugVisitor {
+ public:
+  void OnAckFrame(const QuicAckFrame& frame) override {
+    if (!frame.revived_packets.empty()) ++acks_with_revived;
+    reported.insert(frame.revived_packets.begin(), frame.revived_packets.end());
+  }
+  void OnPacketSent(const SerializedPacket&, QuicPathId, QuicPacketNumber original_packet_number,
+                    TransmissionType, QuicTime) override {
+    if (original_packet_number == 0) return;
+    retransmitted_originals.push_back(original_packet_number);
+    if (reported.count(original_packet_number)) ++after_report;
+  }
+  std::set<QuicPacketNumber> reported;
+  std::vector<QuicPacketNumber> retransmitted_originals;
+  uint64_t acks_with_revived = 0, after_report = 0;
 };
 
 class Endpoint : public QuicConnectionVisitorInterface {
@@ -315,10 +351,11 @@ class Endpoint : public QuicConnectionVisitorInterface {
   void OnRstStream(const QuicRstStreamFrame&) override {}
   void OnGoAway(const QuicGoAwayFrame&) override {}
   void OnConnectionClosed(QuicErrorCode error, const std::string& details,
-                          ConnectionCloseSource) override {
+                          ConnectionCloseSource source) override {
     closed = true;
     close_error = error;
     close_details = details;
+    close_from_peer = source == ConnectionCloseSource::FROM_PEER;
   }
   void OnWriteBlocked() override {}
   void OnSuccessfulVersionNegotiation(const QuicVersion&) override {}
@@ -337,7 +374,7 @@ class Endpoint : public QuicConnectionVisitorInterface {
   uint64_t sent = 0;  // client: stream bytes consumed
   std::string received;
   std::vector<uint8_t> have;
-  bool fin = false, bad_frame = false, closed = false;
+  bool fin = false, bad_frame = false, closed = false, close_from_peer = false;
   QuicErrorCode close_error = QUIC_NO_ERROR;
   std::string close_details;
 
@@ -407,6 +444,7 @@ WriteResult SimWriter::WritePacket(const char* buffer, size_t buf_len, const IPA
         }
       } else {
         ++run_->r->data_packets_sent;
+        if (h.entropy_flag) ++run_->r->protected_entropy_set;
         // the historical sender: XorBuffers of this packet's protected
         // plaintext into the group's accumulator, on the connection thread
         std::vector<uint64_t>& acc = xor_acc[h.fec_group];
@@ -517,7 +555,8 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   std::vector<std::unique_ptr<Wire>> c2s(n), s2c(n);
   std::vector<std::unique_ptr<SimWriter>> cw(n), sw(n);
   std::vector<std::unique_ptr<Endpoint>> ce(n), se(n);
-  RevivalCounter revival_log;
+  std::vector<std::unique_ptr<RevivalCounter>> slog(n);
+  std::vector<std::unique_ptr<AckWatch>> cwatch(n);
   std::vector<std::unique_ptr<QuicConnection>> cc(n), sc(n);
   const IPEndPoint client_addr(IPAddress(10, 0, 0, 1), 4433);
   for (int i = 0; i < n; ++i) {
@@ -536,15 +575,50 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     for (QuicConnection* c : {cc[i].get(), sc[i].get()}) {
       c->SetEncrypter(ENCRYPTION_FORWARD_SECURE, new NullEncrypter());
       c->SetDefaultEncryptionLevel(ENCRYPTION_FORWARD_SECURE);
-      c->SetDecrypter(ENCRYPTION_FORWARD_SECURE, new NullDecrypter());
+      // (inject_unencrypted_fec: server 0 keeps only the ENCRYPTION_NONE
+      // decrypter, so what it decrypts first is at ENCRYPTION_NONE -- NULL
+      // encryption is the same at every level)
+      if (!(params->inject_unencrypted_fec && i == 0 && c == sc[i].get()))
+        c->SetDecrypter(ENCRYPTION_FORWARD_SECURE, new NullDecrypter());
       if (batcher) c->set_fec_batcher(batcher.get());
     }
+    slog[i].reset(new RevivalCounter());
+    cwatch[i].reset(new AckWatch());
     cc[i]->set_visitor(ce[i].get());
     sc[i]->set_visitor(se[i].get());
-    sc[i]->set_debug_visitor(&revival_log);
+    sc[i]->set_debug_visitor(slog[i].get());
+    cc[i]->set_debug_visitor(cwatch[i].get());
     ce[i]->conn = cc[i].get();
     se[i]->conn = sc[i].get();
     if (params->group_size > 0) cc[i]->EnableFecSending(params->group_size);
+  }
+  if (params->inject_unencrypted_fec && n > 0) {
+    // an FEC packet for group 1 at ENCRYPTION_NONE, ahead of client 0's
+    // first packets: server 0 must close with QUIC_UNENCRYPTED_FEC_DATA
+    QuicFramer f(versions, clock.Now(), Perspective::IS_CLIENT);
+    f.set_version(run.version);
+    QuicPacketHeader h;
+    h.public_header.connection_id = 0x5100000000ull;
+    h.public_header.connection_id_length = PACKET_8BYTE_CONNECTION_ID;
+    h.public_header.version_flag = true;
+    h.public_header.versions = versions;
+    h.public_header.packet_number_length = PACKET_6BYTE_PACKET_NUMBER;
+    h.packet_number = 3;
+    h.fec_flag = true;
+    h.is_in_fec_group = IN_FEC_GROUP;
+    h.fec_group = 1;
+    const std::string redundancy(100, '\x5A');
+    char buf[kMaxPacketSize];
+    const size_t len = f.BuildFecPacket(h, redundancy, buf, sizeof(buf));
+    const size_t enc = len == 0 ? 0
+                                : f.EncryptInPlace(ENCRYPTION_NONE, kDefaultPathId, h.packet_number,
+                                                   GetStartOfEncryptedData(run.version, h), len,
+                                                   sizeof(buf), buf);
+    if (enc == 0) {
+      std::snprintf(r->detail, sizeof(r->detail), "could not build the unencrypted FEC packet");
+      return r->status = 5;
+    }
+    c2s[0]->next.emplace_back(buf, enc);
   }
   for (int i = 0; i < n; ++i) ce[i]->Pump();
 
@@ -577,6 +651,14 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
       const double t0 = now_us();
       batcher->Launch();  // the GPU works while the next turn starts
       r->fec_wall_us += now_us() - t0;
+    }
+    if (params->close_mid_batch > 0 && turn >= params->close_mid_batch && n > 0 &&
+        cc[0]->connected() && cc[0]->NumPendingFecPackets() > 0) {
+      // a batched group of client 0 is in flight: close now (the close frame
+      // must leave although packets after the pending FEC packet are held)
+      r->closed_with_pending = 1;
+      cc[0]->CloseConnection(QUIC_PEER_GOING_AWAY, "closed while FEC is pending",
+                             ConnectionCloseBehavior::SEND_CONNECTION_CLOSE_PACKET);
     }
     clock.Advance(QuicTime::Delta::FromMilliseconds(1));
     bool done = true;
@@ -613,7 +695,19 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   }
   r->turns = turn;
   r->stream_bytes = params->stream_len;
-  r->debug_revived = revival_log.count;
+  for (int i = 0; i < n; ++i) {
+    r->debug_revived += slog[i]->count;
+    r->revived_reported += cwatch[i]->reported.size();
+    r->acks_with_revived += cwatch[i]->acks_with_revived;
+    r->retransmitted_after_report += cwatch[i]->after_report;
+    for (QuicPacketNumber p : cwatch[i]->retransmitted_originals)
+      r->retransmitted_of_revived += slog[i]->revived.count(p);
+    if (!r->server_close_error && se[i]->closed) r->server_close_error = se[i]->close_error;
+    if (!r->client_close_error && ce[i]->closed) r->client_close_error = ce[i]->close_error;
+  }
+  if (n > 0)
+    r->peer_saw_close = se[0]->closed && se[0]->close_from_peer &&
+                        se[0]->close_error == QUIC_PEER_GOING_AWAY;
   std::string first_close;
   for (int i = 0; i < n; ++i) {
     const QuicConnectionStats& cs = cc[i]->GetStats();

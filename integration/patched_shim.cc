@@ -257,3 +257,108 @@ SHIM_API int fec_e2e_run(int version, int group_size, uint64_t stream_len, int d
   r->fec_header_ok = visitor.header_ok;
   return r->status;
 }
+
+// ---------------------------------------------------------------------------
+// The v<=31 ack's revived-packets list as the PATCHED framer writes and reads
+// it (quic_framer.cc AppendAckFrameAndTypeByte / ProcessAckFrame): the tests
+// parse what fec_ack_build writes with the UNPATCHED reference framer
+// (oracle/_ref), which reads the list's count and numbers and discards them.
+// ---------------------------------------------------------------------------
+namespace {
+
+QuicPacketHeader AckHeader(uint64_t pn) {
+  QuicPacketHeader h;
+  h.public_header.connection_id = 0x0102030405060708ull;  // as oracle/ref/ref_framer_shim.cc
+  h.public_header.connection_id_length = PACKET_8BYTE_CONNECTION_ID;
+  h.public_header.version_flag = false;
+  h.public_header.packet_number_length = PACKET_6BYTE_PACKET_NUMBER;
+  h.packet_number = pn;
+  return h;
+}
+
+class AckCollector : public QuicFramerVisitorInterface {
+ public:
+  void OnError(QuicFramer*) override {}
+  bool OnProtocolVersionMismatch(QuicVersion) override { return false; }
+  void OnPacket() override {}
+  void OnPublicResetPacket(const QuicPublicResetPacket&) override {}
+  void OnVersionNegotiationPacket(const QuicVersionNegotiationPacket&) override {}
+  bool OnUnauthenticatedPublicHeader(const QuicPacketPublicHeader&) override { return true; }
+  bool OnUnauthenticatedHeader(const QuicPacketHeader&) override { return true; }
+  void OnDecryptedPacket(EncryptionLevel) override {}
+  bool OnPacketHeader(const QuicPacketHeader&) override { return true; }
+  bool OnStreamFrame(const QuicStreamFrame&) override { return true; }
+  bool OnAckFrame(const QuicAckFrame& f) override {
+    ++acks;
+    ack = f;
+    return true;
+  }
+  bool OnStopWaitingFrame(const QuicStopWaitingFrame&) override { return true; }
+  bool OnPaddingFrame(const QuicPaddingFrame&) override { return true; }
+  bool OnPingFrame(const QuicPingFrame&) override {
+    ++pings;
+    return true;
+  }
+  bool OnRstStreamFrame(const QuicRstStreamFrame&) override { return true; }
+  bool OnConnectionCloseFrame(const QuicConnectionCloseFrame&) override { return true; }
+  bool OnGoAwayFrame(const QuicGoAwayFrame&) override { return true; }
+  bool OnWindowUpdateFrame(const QuicWindowUpdateFrame&) override { return true; }
+  bool OnBlockedFrame(const QuicBlockedFrame&) override { return true; }
+  bool OnPathCloseFrame(const QuicPathCloseFrame&) override { return true; }
+  void OnPacketComplete() override { complete = true; }
+  QuicAckFrame ack;
+  int acks = 0, pings = 0;
+  bool complete = false;
+};
+
+}  // namespace
+
+// A v<=31 packet (8-byte connection id, 6-byte packet number, no version)
+// carrying one ack -- largest_observed, missing ranges [lo, hi), the revived
+// list -- and, if with_ping, a PING after it; NULL-encrypted at ENCRYPTION_NONE.
+// Returns the packet length (0 on failure).
+SHIM_API size_t fec_ack_build(int version, uint64_t pn, uint64_t largest_observed,
+                              const uint64_t* miss_lo, const uint64_t* miss_hi, size_t n_miss,
+                              const uint64_t* revived, size_t n_revived, int with_ping,
+                              uint8_t* out, size_t cap) {
+  QuicFramer framer(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_CLIENT);
+  framer.set_version(static_cast<QuicVersion>(version));
+  const QuicPacketHeader header = AckHeader(pn);
+  QuicAckFrame ack;
+  ack.largest_observed = largest_observed;
+  ack.missing = true;
+  for (size_t i = 0; i < n_miss; ++i) ack.packets.Add(miss_lo[i], miss_hi[i]);
+  ack.revived_packets.insert(revived, revived + n_revived);
+  QuicFrames frames;
+  frames.push_back(QuicFrame(&ack));
+  if (with_ping) frames.push_back(QuicFrame(QuicPingFrame()));
+  char* buf = reinterpret_cast<char*>(out);
+  // room for the NULL encrypter's 12-byte hash (as the creator's
+  // max_plaintext_size_)
+  const size_t n =
+      framer.BuildDataPacket(header, frames, buf, framer.GetMaxPlaintextSize(cap));
+  if (n == 0) return 0;
+  return framer.EncryptInPlace(ENCRYPTION_NONE, kDefaultPathId, pn,
+                               GetStartOfEncryptedData(framer.version(), header), n, cap, buf);
+}
+
+// Parses a packet with the PATCHED framer: the ack's revived list into
+// revived[0 .. return) (at most cap), -1 if the packet was refused or held no
+// ack; *pings = PING frames seen after it, *largest = the ack's largest observed.
+SHIM_API int fec_ack_parse(int version, const uint8_t* buf, size_t len, uint64_t* revived,
+                           size_t cap, int* pings, uint64_t* largest) {
+  QuicFramer framer(AllSupportedVersions(), QuicTime::Zero(), Perspective::IS_SERVER);
+  framer.set_version(static_cast<QuicVersion>(version));
+  AckCollector v;
+  framer.set_visitor(&v);
+  QuicEncryptedPacket p(reinterpret_cast<const char*>(buf), len, false);
+  if (!framer.ProcessPacket(p) || v.acks != 1 || !v.complete) return -1;
+  size_t i = 0;
+  for (QuicPacketNumber r : v.ack.revived_packets) {
+    if (i == cap) break;
+    revived[i++] = r;
+  }
+  *pings = v.pings;
+  *largest = v.ack.largest_observed;
+  return static_cast<int>(i);
+}

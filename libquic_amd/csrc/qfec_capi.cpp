@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +28,14 @@ thread_local char g_tls_error[512] = "";
 constexpr int kSlots = 3;                         // host path pipeline depth
 constexpr size_t kStageBytes = 64ull << 20;       // per-slot input staging
 constexpr uint64_t kDirectGroups = 256;  // mapped batches up to this size: no staging copies
+// Device error words (kernel-latched error bits), one per kind of work so
+// that collecting one never reads or clears another's: the
+// context stream's device-pointer calls, each staging slot's QFEC_ASYNC op,
+// and the synchronous host-pointer paths.
+constexpr int kErrStream = 0;
+constexpr int kErrSlot0 = 1;  // + slot index
+constexpr int kErrHost = kErrSlot0 + kSlots;
+constexpr int kErrWords = kErrHost + 1;
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -51,8 +60,8 @@ struct qfec_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  uint32_t* d_err = nullptr;
-  uint32_t* h_err = nullptr;  // pinned
+  uint32_t* d_err = nullptr;  // kErrWords words
+  uint32_t* h_err = nullptr;  // pinned, kErrWords words
   char last_error[512] = "";
   Slot slots[kSlots];
   bool staging_ready = false;
@@ -77,6 +86,7 @@ struct qfec_ctx {
   uint32_t* h_phase_dev = nullptr;
   uint32_t phase_seen = 0;
   uint32_t phase_backoff = 0;
+  int last_fixed_phased = -1;  // the last device fixed-shape launch: 1 phased, 0 one-pass
   uint32_t ncu = 0;          // CU count, queried once
   uint32_t phase_extra = 0;  // test hook (qfec_debug_phase)
   uint32_t phase_min = 0;    // test hook (qfec_debug_phase_min)
@@ -93,10 +103,15 @@ struct qfec_ctx {
     uint32_t token = 0;
     uint64_t cnt = 0;
     uint16_t* parity_len_out = nullptr;  // encode: the caller's lengths, filled at completion
-    uint64_t seq = 0;
+    uint64_t seq = 0;                    // its ticket (qfec_async_ticket)
   } async_ops[kSlots];
   int async_next = 0;
   uint64_t async_seq = 0;
+  uint64_t last_ticket = 0;  // of the last ragged mapped call, 0 if it ran synchronously
+  // results of async ops finished by a call other than their owner's (a slot
+  // reused, a synchronous call draining the slots), kept for
+  // qfec_complete_ticket: each op's code reaches its own caller only
+  std::map<uint64_t, int> finished;
   // device scratch of the host-pointer xor / protection / entropy calls:
   // grow-only buffers kept for the context's life (no allocation per call)
   std::vector<void*> scratch_p;
@@ -182,7 +197,7 @@ int wait_flag(qfec_ctx* ctx, int si, uint32_t token) {
   }
 }
 
-int collect_error(qfec_ctx* ctx, hipStream_t stream);
+int collect_error(qfec_ctx* ctx, hipStream_t stream, int word = kErrStream);
 
 // Finish the QFEC_ASYNC op of slot `si`: QFEC_PENDING if it is still running
 // and !wait; otherwise its encode lengths are copied out and its error word
@@ -213,7 +228,23 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   }
   if (!op.recover && op.parity_len_out)
     std::memcpy(op.parity_len_out, s.h_out, op.cnt * sizeof(uint16_t));
-  return op.direct ? QFEC_OK : collect_error(ctx, s.stream);
+  return op.direct ? QFEC_OK : collect_error(ctx, s.stream, kErrSlot0 + si);
+}
+
+// Finish the op of slot `si` (if live) for a caller that does not own it: its
+// code is kept for its owner's qfec_complete_ticket.
+void retire_async_op(qfec_ctx* ctx, int si) {
+  qfec_ctx::AsyncOp& op = ctx->async_ops[si];
+  if (!op.live) return;
+  const uint64_t t = op.seq;
+  const int rc = complete_async_op(ctx, si, true);
+  if (ctx->finished.size() >= 4096) ctx->finished.erase(ctx->finished.begin());
+  ctx->finished[t] = rc;
+}
+
+// Every outstanding op retired (synchronous calls that use the slots).
+void drain_async(qfec_ctx* ctx) {
+  for (int i = 0; i < kSlots; ++i) retire_async_op(ctx, i);
 }
 
 // Complete every outstanding QFEC_ASYNC op in issue order; the first error
@@ -221,6 +252,10 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
 // one is still running: the ones before it are finished).
 int complete_async(qfec_ctx* ctx, bool wait) {
   int first = QFEC_OK;
+  // ops retired by other calls report here too (then they are claimed)
+  for (const auto& f : ctx->finished)
+    if (f.second && !first) first = f.second;
+  ctx->finished.clear();
   for (;;) {
     int si = -1;
     for (int i = 0; i < kSlots; ++i)
@@ -260,13 +295,13 @@ int latch_error(qfec_ctx* ctx, uint32_t bits) {
 }
 
 // Read and clear the device error word after `stream` has drained.
-int collect_error(qfec_ctx* ctx, hipStream_t stream) {
-  QFEC_HIP(ctx, hipMemcpyAsync(ctx->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                               stream));
+int collect_error(qfec_ctx* ctx, hipStream_t stream, int word) {
+  QFEC_HIP(ctx, hipMemcpyAsync(ctx->h_err + word, ctx->d_err + word, sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, stream));
   QFEC_HIP(ctx, hipStreamSynchronize(stream));
-  const uint32_t bits = *ctx->h_err;
+  const uint32_t bits = ctx->h_err[word];
   if (bits) {
-    QFEC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), stream));
+    QFEC_HIP(ctx, hipMemsetAsync(ctx->d_err + word, 0, sizeof(uint32_t), stream));
     QFEC_HIP(ctx, hipStreamSynchronize(stream));
   }
   return latch_error(ctx, bits);
@@ -282,7 +317,7 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
                uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
-  if ((rc = complete_async(ctx, true))) return rc;
+  drain_async(ctx);
   const bool recover = parity != nullptr;
   const bool rows_pinned = is_pinned_or_device(rows);
   const bool par_pinned = recover && is_pinned_or_device(parity);
@@ -377,7 +412,7 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
     a.n_groups = cnt;
     a.k = k;
     a.L = L;
-    a.err = ctx->d_err;
+    a.err = ctx->d_err + kErrHost;
     QFEC_HIP(ctx, qfec::launch_fixed(a, true, s.stream));
     if (out_pinned && out_stride == L) {
       QFEC_HIP(ctx, hipMemcpyAsync(out + g0 * L, s.d_out, cnt * L, hipMemcpyDeviceToHost,
@@ -395,7 +430,7 @@ int fixed_host(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, const 
   }
   for (int si = 0; si < kSlots; ++si)
     if ((rc = finish(si))) return rc;
-  return collect_error(ctx, ctx->slots[0].stream);
+  return collect_error(ctx, ctx->slots[0].stream, kErrHost);
 }
 
 // ---- QFEC_PTR_MAPPED: payloads in pinned host memory, read in place ---------
@@ -426,7 +461,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
                  uint64_t parity_stride, uint64_t n, uint8_t* out, uint64_t out_stride) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
-  if ((rc = complete_async(ctx, true))) return rc;
+  drain_async(ctx);
   const bool recover = parity != nullptr;
   if ((rc = check_mapped(ctx, rows, "rows")) || (rc = check_mapped(ctx, out, "out")) ||
       (recover && (rc = check_mapped(ctx, parity, "parity"))))
@@ -441,7 +476,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   a.out_stride = out_stride;
   a.k = k;
   a.L = L;
-  a.err = ctx->d_err;
+  a.err = ctx->d_err + kErrHost;
   // the lost-slot indices are the only staged input (kStageBytes / 8 per chunk);
   // a small batch (one chunk of <= kDirectGroups) is latency-bound: the kernel
   // reads them from the mapped slot buffer itself (no copy), and the error
@@ -477,7 +512,7 @@ int fixed_mapped(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity, cons
   for (int si = 0; si < kSlots; ++si)
     if (live[si]) QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
   (void)g0_of;
-  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream);
+  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream, kErrHost);
 }
 
 
@@ -514,10 +549,12 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
       QFEC_HIP(ctx, hipEventRecord(ctx->phase_done, ctx->stream));
       ctx->phase_stream = ctx->stream;
       ctx->phase_recorded = true;
+      ctx->last_fixed_phased = 1;
       return QFEC_OK;
     }
   }
   QFEC_HIP(ctx, qfec::launch_fixed(a, nt, ctx->stream));
+  ctx->last_fixed_phased = 0;
   return QFEC_OK;
 }
 
@@ -676,11 +713,12 @@ qfec_ctx* qfec_create(int device) {
   ctx->device = device;
   bool ok = hipSetDevice(device) == hipSuccess &&
             hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc(&ctx->d_err, sizeof(uint32_t)) == hipSuccess &&
-            hipMemset(ctx->d_err, 0, sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc(&ctx->d_err, kErrWords * sizeof(uint32_t)) == hipSuccess &&
+            hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t)) == hipSuccess &&
             hipMalloc(&ctx->d_phase, kPhaseSyncBytes) == hipSuccess &&
             hipMemset(ctx->d_phase, 0, kPhaseSyncBytes) == hipSuccess &&
-            hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&ctx->h_err, kErrWords * sizeof(uint32_t), hipHostMallocDefault) ==
+                hipSuccess &&
             hipHostMalloc(&ctx->h_phase, sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
             hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->h_phase_dev), ctx->h_phase,
@@ -747,6 +785,24 @@ int qfec_complete(qfec_ctx* ctx, int wait) {
   int rc = bind(ctx);
   if (rc) return rc;
   return complete_async(ctx, wait != 0);
+}
+
+uint64_t qfec_async_ticket(const qfec_ctx* ctx) { return ctx ? ctx->last_ticket : 0; }
+
+int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  auto f = ctx->finished.find(ticket);
+  if (f != ctx->finished.end()) {
+    rc = f->second;
+    ctx->finished.erase(f);
+    return rc;
+  }
+  for (int i = 0; i < kSlots; ++i)
+    if (ctx->async_ops[i].live && ctx->async_ops[i].seq == ticket)
+      return complete_async_op(ctx, i, wait != 0);
+  return fail(ctx, QFEC_ERR_INTERNAL, "unknown or already completed ticket %llu",
+              (unsigned long long)ticket);
 }
 
 int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
@@ -934,7 +990,7 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
                 uint8_t* out, const uint64_t* out_off) {
   int rc = ensure_staging(ctx);
   if (rc) return rc;
-  if ((rc = complete_async(ctx, true))) return rc;
+  drain_async(ctx);
   if ((rc = validate_ragged(ctx, recover, pkt_len, grp_ptr, n, parity_len, missing))) return rc;
 
   const uint64_t in_cap = kStageBytes, out_cap = kStageBytes / 4;
@@ -1038,7 +1094,7 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
     a.pkt_len = reinterpret_cast<const uint16_t*>(s.d_in + lay.len);
     a.grp_ptr = reinterpret_cast<const uint32_t*>(s.d_in + lay.ptr);
     a.n_groups = c.n;
-    a.err = ctx->d_err;
+    a.err = ctx->d_err + kErrHost;
     a.out = s.d_out;
     if (recover) {
       a.parity = s.d_in;  // parity_off is relative to the staging base
@@ -1060,7 +1116,7 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
   }
   for (int i = 0; i < kSlots; ++i)
     if ((rc = finish((slot + i) % kSlots))) return rc;
-  return collect_error(ctx, ctx->slots[0].stream);
+  return collect_error(ctx, ctx->slots[0].stream, kErrHost);
 }
 
 
@@ -1117,9 +1173,9 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   int slot = 0;
   if (async) {
     slot = ctx->async_next;
-    if ((rc = complete_async_op(ctx, slot, true))) return rc;
-  } else if ((rc = complete_async(ctx, true))) {
-    return rc;
+    retire_async_op(ctx, slot);
+  } else {
+    drain_async(ctx);
   }
   // A small batch (the connection thread's flush of a few groups) is
   // latency-bound: the kernel reads the tables from the mapped slot buffer and
@@ -1161,7 +1217,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     a.grp_ptr = reinterpret_cast<const uint32_t*>(tab + t.ptr);
     a.parity_off = reinterpret_cast<const uint64_t*>(tab + t.poff);
     a.n_groups = cnt;
-    a.err = ctx->d_err;
+    a.err = ctx->d_err + (async ? kErrSlot0 + slot : kErrHost);
     if (recover) {
       a.parity = parity;
       a.parity_len = reinterpret_cast<const uint16_t*>(tab + t.plen);
@@ -1195,6 +1251,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       op.cnt = cnt;
       op.parity_len_out = recover ? nullptr : parity_len_out;
       op.seq = ++ctx->async_seq;
+      ctx->last_ticket = op.seq;
       ctx->async_next = (slot + 1) % kSlots;
       return QFEC_OK;
     }
@@ -1206,7 +1263,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   }
   for (int i = 0; i < kSlots; ++i)
     if ((rc = finish((slot + i) % kSlots))) return rc;
-  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream);
+  return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream, kErrHost);
 }
 
 }  // namespace
@@ -1217,6 +1274,7 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
                        uint16_t* parity_len_out, uint32_t flags) {
   int rc = bind(ctx);
   if (rc) return rc;
+  ctx->last_ticket = 0;
   if (ctx->debug_fail)
     return fail(ctx, QFEC_ERR_INTERNAL, "launch failure injected (qfec_debug_fail_launches)");
   if (n_groups == 0) return QFEC_OK;
@@ -1253,6 +1311,7 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
                         const uint64_t* out_off, uint32_t flags) {
   int rc = bind(ctx);
   if (rc) return rc;
+  ctx->last_ticket = 0;
   if (ctx->debug_fail)
     return fail(ctx, QFEC_ERR_INTERNAL, "launch failure injected (qfec_debug_fail_launches)");
   if (n_groups == 0) return QFEC_OK;
@@ -1571,6 +1630,8 @@ int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count) {
 }
 
 int qfec_phase_backoff(qfec_ctx* ctx) { return ctx ? (int)ctx->phase_backoff : -1; }
+
+int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_phased : -1; }
 
 int qfec_debug_fail_launches(qfec_ctx* ctx, int on) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");

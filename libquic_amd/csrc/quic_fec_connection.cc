@@ -238,6 +238,7 @@ int QuicFecReviveBatch::Flush(qfec_ctx* ctx, std::vector<Revived>* revived) {
     Revived r;
     r.tag = g.first;
     if (g.second->ReviveInPlace(&r.header, &r.payload) == 0) continue;  // not for CanRevive() groups
+    r.level = g.second->EffectiveEncryptionLevel();
     if (revived) revived->push_back(r);
   }
   flushed_.swap(groups_);
@@ -297,7 +298,7 @@ int QuicFecBatcher::Launch() {
 
 int QuicFecBatcher::Complete(bool wait) {
   if (!InFlight()) return QFEC_OK;
-  // one qfec_complete finishes both launches (same context)
+  // each launch completes on its own ticket (its own code)
   const auto t0 = std::chrono::steady_clock::now();
   auto spent = [&] {
     stats_.complete_us += std::chrono::duration<double, std::micro>(
@@ -348,6 +349,7 @@ int QuicFecBatcher::Complete(bool wait) {
       QuicFecReviveBatch::Revived r;
       r.tag = v;
       if (rev[j].group->ReviveInPlace(&r.header, &r.payload) == 0) continue;
+      r.level = rev[j].group->EffectiveEncryptionLevel();
       out.push_back(r);
       ++stats_.groups_revived;
     }

@@ -189,6 +189,10 @@ class QuicFecReviveBatch {
     // redundancy length, zero padded (PADDING frames): a view of the group's
     // accumulator, valid until this batch's next Flush / Clear / destruction
     StringPiece payload;
+    // the lowest decryption level of the packets the payload was rebuilt
+    // from (QuicFecGroup::EffectiveEncryptionLevel): the revived packet is
+    // processed at this level, as the historical connection did
+    EncryptionLevel level = NUM_ENCRYPTION_LEVELS;
   };
 
   void Add(void* tag, std::unique_ptr<QuicFecGroup> group);

@@ -418,13 +418,14 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
                                 pkt_len.data(), grp_ptr.data(), launched.size(),
                                 reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
                                 pend->plen.data(), flags);
-  pend->live = pend->rc == QFEC_OK && (flags & QFEC_ASYNC);
+  pend->ticket = pend->rc == QFEC_OK ? qfec_async_ticket(ctx) : 0;
+  pend->live = pend->ticket != 0;  // else it completed synchronously
   return pend->rc;
 }
 
 int QuicFecGroup::Finish(Pending* pend, bool wait) {
   if (pend->live) {
-    const int rc = qfec_complete(pend->ctx, wait ? 1 : 0);
+    const int rc = qfec_complete_ticket(pend->ctx, pend->ticket, wait ? 1 : 0);
     if (rc == QFEC_PENDING) return QFEC_PENDING;
     pend->rc = rc;
     pend->live = false;

@@ -142,7 +142,8 @@ class QuicFecGroup {
   // ComputeAll in two halves, for an event loop that overlaps the GPU work
   // with its other work: Launch queues the ONE ragged launch (QFEC_ASYNC when
   // every payload sits in mapped arena memory, else it completes at once) and
-  // Finish completes it (qfec_complete) and sets every group's parity.  The
+  // Finish completes THAT launch (qfec_complete_ticket: its own code, not
+  // another op's of the same context) and sets every group's parity.  The
   // groups must stay alive and take no packets in between.
   struct Pending {
     qfec_ctx* ctx = nullptr;
@@ -150,6 +151,7 @@ class QuicFecGroup {
     std::vector<uint16_t> plen;  // parity_len_out, filled at completion
     int rc = QFEC_OK;            // a synchronous failure at launch
     bool live = false;
+    uint64_t ticket = 0;         // the queued launch (qfec_async_ticket)
   };
   static int Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* p,
                     bool async);

@@ -95,8 +95,11 @@ SIGNATURES = [
     ("qfec_phase_backoff", C.c_int, [_vp]),
     ("qfec_debug_phase", C.c_int, [_vp, C.c_uint32, C.c_int]),
     ("qfec_debug_phase_min", C.c_int, [_vp, C.c_uint32]),
+    ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
+    ("qfec_async_ticket", C.c_uint64, [_vp]),
+    ("qfec_complete_ticket", C.c_int, [_vp, C.c_uint64, C.c_int]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -383,6 +386,11 @@ class Context:
         """Large fixed batches left on the one-pass kernel (contention backoff)."""
         return self.lib.qfec_phase_backoff(self.ctx)
 
+    def last_fixed_phased(self):
+        """1 if the last device fixed-shape call ran the phased kernel, 0 the
+        one-pass kernel, -1 none yet."""
+        return self.lib.qfec_last_fixed_phased(self.ctx)
+
     def debug_phase(self, extra, reset_backoff=True):
         """Test hook: extra workgroups in phased launches (forces the abandon
         path); reset_backoff clears the contention backoff."""
@@ -392,6 +400,16 @@ class Context:
         """Test hook: phased kernel from `min_phases` phases on (0 default,
         1 always, 0xFFFFFFFF never)."""
         return self._check(self.lib.qfec_debug_phase_min(self.ctx, min_phases))
+
+    def async_ticket(self):
+        """Ticket of the last ragged call if it was queued (QFEC_ASYNC), else 0."""
+        return self.lib.qfec_async_ticket(self.ctx)
+
+    def complete_ticket(self, ticket, wait=True):
+        """Finish one queued op: 0 done, QFEC_PENDING (1) still running;
+        raises its own error only."""
+        rc = self.lib.qfec_complete_ticket(self.ctx, ticket, 1 if wait else 0)
+        return rc if rc == 1 else self._check(rc)
 
     def complete(self, wait=True):
         """Finish QFEC_ASYNC calls: 0 done, QFEC_PENDING (1) still running."""

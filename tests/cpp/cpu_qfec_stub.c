@@ -56,6 +56,20 @@ int qfec_complete(qfec_ctx* ctx, int wait) {
   return QFEC_OK;
 }
 
+/* Work completes inside the call: nothing is ever queued. */
+uint64_t qfec_async_ticket(const qfec_ctx* ctx) {
+  (void)ctx;
+  return 0;
+}
+
+int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait) {
+  (void)ctx;
+  (void)ticket;
+  (void)wait;
+  strcpy(g_err, "unknown or already completed ticket");
+  return QFEC_ERR_INTERNAL;
+}
+
 int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_off,
                        const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
                        uint8_t* parity_out, const uint64_t* parity_off,

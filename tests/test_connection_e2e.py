@@ -47,6 +47,22 @@ def _have_device():
     return bool(c)
 
 
+def _check_revived_channel(r):
+    """The reference's entropy bits on FEC-protected packets and the v<=31
+    ack's revived-packets list: protected packets carry the creator's random
+    entropy bit (about half are 1), every ack still validates (no connection
+    closed on "Invalid entropy": _check_common), every revived packet is
+    reported to its sender in an ack, and no packet is retransmitted after an
+    ack reported it revived (QuicSentPacketManager::MarkPacketNotRetransmittable)."""
+    if r["data_packets_sent"] >= 64:
+        frac = r["protected_entropy_set"] / r["data_packets_sent"]
+        assert 0.3 < frac < 0.7, r
+    assert r["retransmitted_after_report"] == 0, r
+    if r["revived"]:
+        assert r["acks_with_revived"] > 0, r
+        assert 0 < r["revived_reported"] <= r["revived"], r
+
+
 def _check_common(r, n):
     assert r["status"] == 0, r["detail"]
     assert r["connected"] == n, r["detail"]
@@ -86,6 +102,21 @@ def test_fec_without_device_skips_groups(batched):
     assert r["dropped"] > 0 and r["retransmitted"] >= r["dropped"]
 
 
+def test_unencrypted_fec_data_closes_the_connection():
+    """An FEC packet that arrives at ENCRYPTION_NONE closes the connection with
+    QUIC_UNENCRYPTED_FEC_DATA (quic_protocol.h:549-550; the rule OnStreamFrame
+    applies to stream data), before its redundancy reaches any group; the
+    sender never FEC-protects a packet at ENCRYPTION_NONE.  No GPU work is
+    reached, so this runs on the CPU."""
+    h = _harness()
+    r = h.run(n_pairs=1, group_size=0, drop_every=0, stream_len=20_000,
+              inject_unencrypted_fec=True)
+    assert r["status"] == 0, r["detail"]
+    assert r["server_close_error"] == 77, r  # QUIC_UNENCRYPTED_FEC_DATA
+    assert r["connected"] == 0 and r["streams_ok"] == 0, r
+    assert r["revived"] == 0, r
+
+
 # ---- GPU ---------------------------------------------------------------------
 
 @pytest.mark.gpu
@@ -117,8 +148,11 @@ def test_connection_fec_revives_every_single_loss(batched, group_size, drop_ever
         assert r["launches"] > 0
         assert r["groups_encoded"] == r["fec_packets_sent"], r
         assert r["groups_revived"] == r["revived"], r
+    _check_revived_channel(r)
     print({k: r[k] for k in ("turns", "data_packets_sent", "fec_packets_sent", "dropped",
-                             "revived", "retransmitted", "launches")})
+                             "revived", "retransmitted", "launches", "revived_reported",
+                             "acks_with_revived", "retransmitted_of_revived",
+                             "protected_entropy_set")})
 
 
 @pytest.mark.gpu
@@ -139,8 +173,10 @@ def test_connection_fec_over_a_reordering_link(reorder):
     assert r["dropped"] > 0 and r["revived"] > 0, r
     assert r["dropped"] <= r["revived"] + r["retransmitted"], r
     assert r["debug_revived"] == r["revived"], r
+    _check_revived_channel(r)
     print({k: r[k] for k in ("turns", "data_packets_sent", "fec_packets_sent", "dropped",
-                             "revived", "retransmitted", "launches")})
+                             "revived", "retransmitted", "launches", "revived_reported",
+                             "retransmitted_of_revived")})
 
 
 @pytest.mark.gpu
@@ -183,3 +219,20 @@ def test_batcher_batches_across_connections():
     _check_common(r, n)
     assert r["dropped"] == r["revived"] > 0
     assert r["groups_encoded"] >= 4 * r["launches"], r
+    _check_revived_channel(r)
+
+
+@pytest.mark.gpu
+def test_close_while_fec_packet_pending():
+    """A batched connection closes while its group's FEC packet is still being
+    computed: packets numbered after a pending FEC packet are held back, but
+    the CONNECTION_CLOSE must leave at once (IsTerminationPacket) -- the peer
+    learns of the close, and the pending group goes without FEC."""
+    h = _harness()
+    r = h.run(n_pairs=2, group_size=10, drop_every=2, stream_len=150_000, batched=True,
+              require_gpu=True, close_mid_batch=3)
+    assert r["status"] == 0, r["detail"]
+    assert r["closed_with_pending"] == 1, r
+    assert r["peer_saw_close"] == 1, r
+    assert r["client_close_error"] == 16, r  # QUIC_PEER_GOING_AWAY
+    assert r["connected"] == 1 and r["streams_ok"] == 1, r  # the other pair is untouched

@@ -309,3 +309,53 @@ def test_ragged_mapped_async_error_at_completion(ctx):
     finally:
         data.close()
         par.close()
+
+
+@pytest.mark.parametrize("n", [3, 2000])
+def test_ragged_mapped_async_tickets(ctx, n):
+    """Each QFEC_ASYNC op completes on its own ticket (one
+    Pending's completion no longer finishes and reports another's): tickets
+    complete in any order, a synchronous call in between retires the queued
+    ops but keeps their codes for their tickets, a completed ticket is
+    unknown afterwards, and the outputs are the oracle's."""
+    z, want_l = _mapped_case(n, g0=7000 + n, kmin=2, kmax=30, lmin=1, lmax=1452)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(n * 1452)
+    par_in = qfec.HostBuffer(n * 1452)
+    par_in.array[:] = z["parity"]
+    out = qfec.HostBuffer(n * 1452)
+    plen = np.zeros(n, dtype=np.uint16)
+    try:
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        te = ctx.async_ticket()
+        ctx.recover_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n,
+                           par_in.array, z["parity_off"], want_l, z["missing"], out.array,
+                           z["out_off"], mapped=True, async_=True)
+        tr = ctx.async_ticket()
+        assert te and tr and te != tr
+        assert ctx.complete_ticket(tr) == 0   # the later op first
+        assert ctx.complete_ticket(te) == 0
+        assert np.array_equal(plen, want_l)
+        for g in range(n):
+            o, m = int(z["parity_off"][g]), int(want_l[g])
+            assert np.array_equal(par.array[o:o + m], z["parity"][o:o + m]), g
+            assert np.array_equal(out.array[o:o + m], z["recovered"][o:o + m]), g
+        with pytest.raises(qfec.QfecError, match="ticket"):
+            ctx.complete_ticket(te)
+        # queued, then retired by a synchronous call: the code stays claimable
+        plen[:] = 0
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        t3 = ctx.async_ticket()
+        plen2 = np.zeros(n, dtype=np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, out.array,
+                          z["parity_off"], plen2, mapped=True)
+        assert ctx.async_ticket() == 0  # the synchronous call queued nothing
+        assert np.array_equal(plen, want_l) and np.array_equal(plen2, want_l)
+        assert ctx.complete_ticket(t3) == 0
+        assert ctx.complete(wait=True) == 0
+    finally:
+        for b in (data, par, par_in, out):
+            b.close()

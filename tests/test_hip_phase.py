@@ -1,10 +1,12 @@
 """GPU parity tests of the phased fixed-shape kernel (phase_xor_kernel,
 libquic_amd/csrc/qfec_kernels.hip), through the C-ABI.
 
-Large nt batches (>= 8 phases of CUs x 40 steps x floor(256 / ceil(L/16))
-groups) run the phased kernel by default; QFEC_ONE_PASS forces the one-pass
-fixed kernel.  Every case here is sized just past that threshold with a
-ragged last phase, and checks the phased outputs byte-exact against the
+Large nt batches (>= kPhMinPhases = 6 phases of CUs x 40 steps x
+floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) run the phased
+kernel by default; QFEC_ONE_PASS forces the one-pass fixed kernel, and
+qfec_last_fixed_phased reports which one a call ran (every case here asserts
+it).  Every case is sized past that threshold (8 phases of 40 LDS steps) with
+a ragged last phase, and checks the phased outputs byte-exact against the
 one-pass kernel's on the same buffers, against the oracle on sampled groups,
 and through the round-trip properties (revived row == erased row, parity XOR
 every row == 0) on every group.
@@ -57,6 +59,8 @@ def run_both(ctx, rows, miss, k, L, n, ps=None, os_=None, **strides):
         if ps != L or os_ != L or strides:
             kw.update(out_stride=os_)
         ctx.recover(rows, par, miss, k, L, n, out, one_pass=one_pass, **kw)
+        # the library's own answer: phased unless QFEC_ONE_PASS (L >= 16 here)
+        assert ctx.last_fixed_phased() == (0 if one_pass or L < 16 else 1)
         ctx.sync()
         torch.cuda.synchronize()
         res[one_pass] = (par, out)

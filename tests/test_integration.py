@@ -43,7 +43,11 @@ def test_patch_names_only_the_hook_files():
         "quic_protocol.h", "quic_protocol.cc", "quic_framer.h", "quic_framer.cc",
         "quic_packet_creator.h", "quic_packet_creator.cc", "quic_packet_generator.h",
         "quic_connection.h", "quic_connection.cc", "quic_connection_stats.h",
-        "quic_connection_stats.cc"))
+        "quic_connection_stats.cc",
+        # the v<=31 ack's revived-packets list: receive side records revivals,
+        # send side stops retransmitting what the peer revived
+        "quic_received_packet_manager.h", "quic_received_packet_manager.cc",
+        "quic_sent_packet_manager.h", "quic_sent_packet_manager.cc"))
 
 
 def test_patch_applies_and_every_unit_compiles():

@@ -5,6 +5,7 @@
 // groups, nondeterministically (root cause not found; the product uses b32).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/debug/ragged_variants.hip -o tools/debug/build/ragged_variants
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
+#include "../tune/ragged_legacy.inc"
 
 
 #include <cstdio>

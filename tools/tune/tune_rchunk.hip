@@ -7,6 +7,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rchunk.hip -o tools/tune/build/tune_rchunk
 // run:   tune_rchunk [reps] [rounds]
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
+#include "ragged_legacy.inc"
 #include "ragged_chunk.inc"
 
 #include <algorithm>

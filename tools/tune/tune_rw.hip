@@ -8,6 +8,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rw.hip -o tools/tune/build/tune_rw
 // run:   tune_rw [reps] [rounds] [kmin] [kspan] [lmin] [lspan] [packed_out]
 #include "../../libquic_amd/csrc/qfec_kernels.hip"
+#include "ragged_legacy.inc"
 #include "ragged_exp.inc"
 
 #include <algorithm>
