@@ -399,6 +399,10 @@ int qfec_debug_phase(qfec_ctx* ctx, uint32_t extra, int reset_backoff);
  * phased kernel; 0 restores the default (6 phases, about 184K headline
  * groups).  1 forces it for any batch, 0xFFFFFFFF never. */
 int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases);
+/* Test hook: on == 0 runs phased launches without their register-held steps
+ * (40 LDS steps per phase only, more phases); 1 restores the default.  For
+ * the per-group-size A/B; results are identical. */
+int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on);
 /* Test hook: fail != 0 makes every ragged call on this context fail with
  * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
  * connection integration: groups go without FEC). */

@@ -90,6 +90,7 @@ struct qfec_ctx {
   uint32_t ncu = 0;          // CU count, queried once
   uint32_t phase_extra = 0;  // test hook (qfec_debug_phase)
   uint32_t phase_min = 0;    // test hook (qfec_debug_phase_min)
+  uint32_t no_regsteps = 0;  // test hook (qfec_debug_phase_regsteps)
   bool debug_fail = false;   // test hook (qfec_debug_fail_launches)
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
@@ -531,6 +532,7 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
   a.ncu = ctx->ncu;
   a.phase_extra = ctx->phase_extra;
   a.phase_min = ctx->phase_min;
+  a.no_regsteps = ctx->no_regsteps;
   a.phase_host = ctx->h_phase_dev;
   a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
   if (a.phase_sync && qfec::fixed_uses_phases(a, nt)) {
@@ -1655,6 +1657,13 @@ int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases) {
   int rc = bind(ctx);
   if (rc) return rc;
   ctx->phase_min = min_phases;
+  return QFEC_OK;
+}
+
+int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  ctx->no_regsteps = on ? 0u : 1u;
   return QFEC_OK;
 }
 

@@ -50,6 +50,9 @@ struct FixedArgs {
   // steps per phase of the launch (set by launch_fixed: the batch spread
   // evenly over its phases); 0 = the kernel's full phase
   uint32_t phase_steps = 0;
+  // test hook (qfec_debug_phase_regsteps): phased launches without the
+  // register-held steps (the A/B of DESIGN.md §4's per-k table)
+  uint32_t no_regsteps = 0;
 };
 
 // True if launch_fixed(a, nontemporal, ...) runs the phased kernel.

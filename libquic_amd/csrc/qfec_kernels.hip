@@ -1015,14 +1015,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // packet table, so their round trip overlaps the table's (measured equal to
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
 // DIAG (tools/tune only, not exact): 1 = no parity stores.
-// TL (round 4): the flat loop handles FULL windows only -- one load, four LDS
-// XORs, no shift or byte mask -- and each packet's partial last window is
-// XORed in by one lane per packet after the loop (the 16 bytes ending at the
-// packet end, shifted down).  The flat loop was VALU-bound (0.98 busy without
-// stores): the per-window shift / mask of the AL form was
-// about half of its VALU work, for the one window in ~45 that needs it.
-template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0,
-          bool TL = false>
+template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
 __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
   constexpr uint32_t NT = 64u * WAVES;
@@ -1128,13 +1121,6 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
     }
     return;
   }
-  // TL: the packet's partial last window is loaded now, so that its round
-  // trip overlaps the flat loop; XORed in after it
-  u32x4 tailv = {0u, 0u, 0u, 0u};
-  if constexpr (TL) {
-    if (tid < R && (len & 15u) != 0u)
-      tailv = ld16t<true>(a.bytes + ((((uint64_t)offhi << 32) | offlo) + len - 16u));
-  }
   if (tid < R) {
     pk[tid] = u32x4{offlo, offhi, len | (j << 16), S};
     __hip_atomic_fetch_or(&s_head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
@@ -1173,38 +1159,10 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t f = (it + (uint32_t)u) * NT + tid;
-      // f >> 6 = (it + u) WAVES + wv: the wave's 64-window block, wave-uniform
-      const uint32_t b = TL ? (uint32_t)__builtin_amdgcn_readfirstlane(
-                                  (int)min((it + (uint32_t)u) * (uint32_t)WAVES + wv, nblk - 1u))
-                            : min(f >> 6, nblk - 1u);
+      const uint32_t b = min(f >> 6, nblk - 1u);
       const uint64_t M = s_head[b];
       const uint32_t pi = min(s_cnt[b] + (uint32_t)__popcll(M & below) - 1u, R - 1u);
       md[u] = pk[pi];
-    }
-    if constexpr (TL) {
-      // full windows only; a partial last window's lane loads its packet's
-      // first window (in bounds, an L2 hit) and XORs nothing
-      u32x4 v[U];
-      uint32_t tt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t f = (it + (uint32_t)u) * NT + tid;
-        const uint32_t ln = md[u].z & 0xFFFFu;
-        const uint32_t win = 16u * (f - md[u].w);
-        const bool full = win + 16u <= ln;
-        const uint64_t at = (((uint64_t)md[u].y << 32) | md[u].x) + (full ? win : 0u);
-        v[u] = ld16t<true>(a.bytes + at);
-        tt[u] = f < W && full ? (md[u].z >> 16) * kAccWords + (f - md[u].w) : 0xFFFFFFFFu;
-      }
-      // every load issued before any is used: otherwise the compiler sinks
-      // the later loads into their lanes' conditional XOR, one load in flight
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (tt[u] != 0xFFFFFFFFu) lds_xor16<1, __HIP_MEMORY_SCOPE_WORKGROUP>(acc, tt[u], v[u]);
-      continue;
     }
     u32x4 v[U];
     uint32_t tt[U], sh[U];
@@ -1240,13 +1198,6 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
         }
         lds_xor16<1, __HIP_MEMORY_SCOPE_WORKGROUP>(acc, tt[u], w);
       }
-  }
-  if constexpr (TL) {
-    // each packet's partial last window: bytes [16t, len), from the 16 bytes
-    // ending at the packet end shifted down by 16 - len % 16 (len >= 16 here)
-    if (tid < R && (len & 15u) != 0u)
-      lds_xor16<1, __HIP_MEMORY_SCOPE_WORKGROUP>(acc, j * kAccWords + (len >> 4),
-                                                 shr_bytes_bf(tailv, 16u - (len & 15u)));
   }
   __syncthreads();  // every lane's XORs done
   // ---- 4. stores, flattened over the groups' output windows
@@ -1545,26 +1496,40 @@ hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t
   return hipGetLastError();
 }
 
+// Register-held steps per phase for a templated group size (0: none): every
+// templated k takes kPhRegSteps (round 4; round 3 had
+// them for k = 10 only).  Non-templated k run the LDS steps alone.
+__host__ __device__ constexpr uint32_t phase_reg_steps(uint32_t k) {
+  return (k == 2u || k == 4u || k == 5u || k == 8u || k == 10u || k == 16u) ? (uint32_t)kPhRegSteps
+                                                                            : 0u;
+}
+
 template <bool RECOVER>
 hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t grid,
                           uint32_t nphase, hipStream_t s) {
+  const bool rs = a.no_regsteps == 0u;
   switch (a.k) {
-#define QFEC_K_CASE(KV)                                                                     \
-  case KV:                                                                                   \
-    hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C, \
-                       gpb, nphase);                                                         \
+    // templated k: kPhRegSteps more steps per phase held in registers after
+    // the LDS steps (recover: their parity rows first, RPF), or without them
+    // (test hook)
+#define QFEC_K_CASE(KV)                                                                        \
+  case KV:                                                                                      \
+    if (rs)                                                                                     \
+      hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER, false, false, kPhUDefault, kPhSteps,    \
+                                           kBlock, false, true, true, false, true, kPhRegSteps, \
+                                           true>),                                              \
+                         dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);                    \
+    else                                                                                        \
+      hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C, \
+                         gpb, nphase);                                                          \
     break;
     QFEC_K_CASE(2)
     QFEC_K_CASE(4)
     QFEC_K_CASE(5)
     QFEC_K_CASE(8)
+    QFEC_K_CASE(10)
     QFEC_K_CASE(16)
 #undef QFEC_K_CASE
-    case 10:  // the headline shape: kPhRegSteps more steps per phase in registers
-      hipLaunchKernelGGL((phase_xor_kernel<10, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
-                                           false, true, true, false, true, kPhRegSteps, true>),
-                         dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
-      break;
     default:
       hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C,
                          gpb, nphase);
@@ -1593,7 +1558,8 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   const uint64_t per = (uint64_t)wg * kPhSteps * gpb;
   const uint64_t np = (a.n_groups + per - 1) / per;
   if (np < (a.phase_min ? a.phase_min : kPhMinPhases) || np > 0xFFFFFFFFull) return false;
-  const uint64_t per_l = (uint64_t)wg * (kPhSteps + (a.k == 10u ? kPhRegSteps : 0u)) * gpb;
+  const uint64_t per_l =
+      (uint64_t)wg * (kPhSteps + (a.no_regsteps ? 0u : phase_reg_steps(a.k))) * gpb;
   *grid = wg;
   *nphase = (uint32_t)((a.n_groups + per_l - 1) / per_l);
   return true;

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -342,8 +343,14 @@ int QuicFecGroup::ComputeAll(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& gr
   return Finish(&p, /*wait=*/true);
 }
 
+QuicFecGroup::LaunchProfile& QuicFecGroup::launch_profile() {
+  static thread_local LaunchProfile p;
+  return p;
+}
+
 int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* pend,
                          bool async) {
+  const auto t0 = std::chrono::steady_clock::now();
   *pend = Pending();
   std::vector<QuicFecGroup*> work;
   for (QuicFecGroup* g : groups)
@@ -414,10 +421,18 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
   }
   pend->plen.assign(launched.size(), 0);
   const uint32_t flags = mapped ? (QFEC_PTR_MAPPED | (async ? QFEC_ASYNC : 0u)) : QFEC_PTR_HOST;
+  const auto t1 = std::chrono::steady_clock::now();
   pend->rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
                                 pkt_len.data(), grp_ptr.data(), launched.size(),
                                 reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
                                 pend->plen.data(), flags);
+  LaunchProfile& prof = launch_profile();
+  const auto t2 = std::chrono::steady_clock::now();
+  prof.tables_us += std::chrono::duration<double, std::micro>(t1 - t0).count();
+  prof.call_us += std::chrono::duration<double, std::micro>(t2 - t1).count();
+  ++prof.launches;
+  prof.groups += launched.size();
+  prof.packets += npk;
   pend->ticket = pend->rc == QFEC_OK ? qfec_async_ticket(ctx) : 0;
   pend->live = pend->ticket != 0;  // else it completed synchronously
   return pend->rc;

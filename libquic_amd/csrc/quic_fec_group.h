@@ -159,6 +159,18 @@ class QuicFecGroup {
   // launch's qfec_* code (also in every launched group's detailed_error).
   static int Finish(Pending* p, bool wait);
 
+  // This thread's Launch time split (microseconds, accumulated): building the
+  // CSR tables over the payloads, and the qfec_*_ragged call that queues the
+  // launch (measurement: bench.py connection legs, tools/tune/host_cost.cc).
+  struct LaunchProfile {
+    double tables_us = 0;
+    double call_us = 0;
+    uint64_t launches = 0;
+    uint64_t groups = 0;
+    uint64_t packets = 0;
+  };
+  static LaunchProfile& launch_profile();
+
   // Detailed reason of the last failure (QuicFramer::detailed_error style).
   const std::string& detailed_error() const { return detailed_error_; }
 

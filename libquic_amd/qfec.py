@@ -95,6 +95,7 @@ SIGNATURES = [
     ("qfec_phase_backoff", C.c_int, [_vp]),
     ("qfec_debug_phase", C.c_int, [_vp, C.c_uint32, C.c_int]),
     ("qfec_debug_phase_min", C.c_int, [_vp, C.c_uint32]),
+    ("qfec_debug_phase_regsteps", C.c_int, [_vp, C.c_int]),
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
@@ -410,6 +411,10 @@ class Context:
         raises its own error only."""
         rc = self.lib.qfec_complete_ticket(self.ctx, ticket, 1 if wait else 0)
         return rc if rc == 1 else self._check(rc)
+
+    def debug_phase_regsteps(self, on):
+        """Test hook: phased launches with (True) or without their register-held steps."""
+        return self._check(self.lib.qfec_debug_phase_regsteps(self.ctx, 1 if on else 0))
 
     def complete(self, wait=True):
         """Finish QFEC_ASYNC calls: 0 done, QFEC_PENDING (1) still running."""

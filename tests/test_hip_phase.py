@@ -68,7 +68,7 @@ def run_both(ctx, rows, miss, k, L, n, ps=None, os_=None, **strides):
 
 
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
-                                 (5, 17), (2, 16)])
+                                 (5, 17), (2, 16), (4, 1350), (8, 1001)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
@@ -299,3 +299,33 @@ def test_phased_one_context_two_streams(ctx):
         assert torch.equal(o, want)
     assert ctx.phase_abandons() == a0
     assert ctx.phase_backoff() == 0
+
+
+@pytest.mark.parametrize("k,L", [(4, 1350), (16, 700)])
+def test_phased_register_steps_identical(ctx, k, L):
+    """Every templated k runs 32 register-held steps per phase after the 40
+    LDS steps (round 4; round 3: k = 10 only).  With the steps switched off
+    (qfec_debug_phase_regsteps) the same batch takes more, shorter phases:
+    the outputs must be byte-identical, and the round trip exact."""
+    n = 8 * phase_groups(L) + 333
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    miss = torch.from_numpy(Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)).to(DEV)
+    res = {}
+    try:
+        for on in (True, False):
+            ctx.debug_phase_regsteps(on)
+            par = torch.full((n * L,), 0xA5, dtype=torch.uint8, device=DEV)
+            out = torch.full((n * L,), 0x5A, dtype=torch.uint8, device=DEV)
+            ctx.encode(rows, k, L, n, par)
+            assert ctx.last_fixed_phased() == 1
+            ctx.recover(rows, par, miss, k, L, n, out)
+            ctx.sync()
+            torch.cuda.synchronize()
+            res[on] = (par, out)
+    finally:
+        ctx.debug_phase_regsteps(True)
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    r3 = rows.view(n, k, L)
+    assert torch.equal(r3[torch.arange(n, device=DEV), miss.long()], res[True][1].view(n, L))

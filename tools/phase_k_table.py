@@ -1,0 +1,97 @@
+"""Per-group-size table of the phased fixed-shape kernel (DESIGN.md §4,
+VERDICT r3 item 7): for every templated k, 2^20 groups x k x 1350 B,
+encode and recover with the register-held phase steps (the product since
+round 4) and without them (qfec_debug_phase_regsteps(0): 40 LDS steps per
+phase, round 3's kernel for k != 10), alternated round by round in one
+process on the same buffers.  The outputs of the two forms are compared
+byte for byte, and the round trip (revived row == lost row) is checked.
+GPU box; one JSON line per k, then a summary.
+
+  python tools/phase_k_table.py [rounds=3] [reps=8]
+
+The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from libquic_amd import qfec  # noqa: E402
+
+HBM = 8000.0  # GB/s, MI355X_MICROARCH.md
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    dev = torch.device("cuda:0")
+    G, L = 1 << 20, 1350
+    ctx = qfec.Context(0)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    out_rows = []
+    for k in (2, 4, 5, 8, 10, 16):
+        rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
+        ctx.synth_fixed(rows, k, L, 0, G, 0x5EED0000 + k)
+        miss = torch.from_numpy(
+            (np.random.default_rng(k).integers(0, k, G)).astype(np.uint8)).to(dev)
+        par = {m: torch.empty(G * L, dtype=torch.uint8, device=dev) for m in (0, 1)}
+        out = {m: torch.empty(G * L, dtype=torch.uint8, device=dev) for m in (0, 1)}
+        par[2], out[2] = par[0], out[0]  # one-pass writes where LDS-only did (compared below)
+        t = {(m, op): [] for m in (0, 1, 2) for op in ("enc", "rec")}
+        phased = {}
+        for r in range(rounds):
+            for m in (1, 0, 2):  # 1: register steps (product), 0: LDS steps only, 2: one-pass
+                ctx.debug_phase_regsteps(m == 1)
+                for op in ("enc", "rec"):
+                    def run():
+                        if op == "enc":
+                            ctx.encode(rows, k, L, G, par[m], one_pass=(m == 2))
+                        else:
+                            ctx.recover(rows, par[m], miss, k, L, G, out[m], one_pass=(m == 2))
+                    run()  # warm
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(reps):
+                        run()
+                    e1.record(stream)
+                    e1.synchronize()
+                    t[(m, op)].append(e0.elapsed_time(e1) / reps / 1e3)
+                    phased[(m, op)] = ctx.last_fixed_phased()
+        ctx.debug_phase_regsteps(True)
+        ctx.sync()
+        torch.cuda.synchronize()
+        same = torch.equal(par[0], par[1]) and torch.equal(out[0], out[1])  # one-pass wrote 0 last
+        r3 = rows.view(G, k, L)
+        trip = torch.equal(r3[torch.arange(G, device=dev), miss.long()], out[1].view(G, L))
+        b = G * (k + 1) * L  # encode: k rows read + parity written; recover: k-1 + parity + out
+        rec = {"k": k, "groups": G, "L": L, "identical": bool(same), "round_trip": bool(trip),
+               "phased": {f"{m}{op}": phased[(m, op)] for (m, op) in phased}}
+        for m, tag in ((1, "regsteps"), (0, "lds_only"), (2, "one_pass")):
+            for op in ("enc", "rec"):
+                s = float(np.median(t[(m, op)]))
+                rec[f"{tag}_{op}_us"] = round(s * 1e6, 1)
+                rec[f"{tag}_{op}_frac"] = round(b / s / 1e9 / HBM, 4)
+        print(json.dumps(rec), flush=True)
+        out_rows.append(rec)
+        del rows, par, out
+        torch.cuda.empty_cache()
+    print("\n| k | encode: register steps / LDS steps only / one-pass | "
+          "recover: register steps / LDS steps only / one-pass |")
+    print("|---|---|---|")
+    for r in out_rows:
+        print(f"| {r['k']} | {r['regsteps_enc_frac']:.3f} / {r['lds_only_enc_frac']:.3f} / "
+              f"{r['one_pass_enc_frac']:.3f} | {r['regsteps_rec_frac']:.3f} / "
+              f"{r['lds_only_rec_frac']:.3f} / {r['one_pass_rec_frac']:.3f} |")
+    ok = all(r["identical"] and r["round_trip"] for r in out_rows)
+    print("all identical and round trips exact:", ok)
+    return 0 if ok else 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

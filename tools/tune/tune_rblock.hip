@@ -52,9 +52,14 @@ struct V {
   std::function<void(const RaggedArgs&)> run;
 };
 
+// (round 4: a TL template flag -- full windows only in the flat loop, each
+// packet's partial last window by one lane after it -- measured exact and
+// 0.59-0.62 against the product's 0.69-0.71: profiles/round4/ragged_tl/,
+// commit ddd19fd; removed from the product)
 #define BLK(REC, U, TL)                                                                    \
   [=](const RaggedArgs& a) {                                                               \
-    hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, U, true, true, 0, TL>),      \
+    static_assert(!TL, "TL variant removed");                                              \
+    hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, U, true, true, 0>),          \
                        dim3((uint32_t)((a.n_groups + 7) / 8)), dim3(256), 0, 0, a);        \
   }
 
@@ -141,16 +146,10 @@ int main(int argc, char** argv) {
 
   std::vector<V> vs;
   vs.push_back({"product AL U2 encode", false, BLK(false, 2, false)});
-  vs.push_back({"TL U2 encode", false, BLK(false, 2, true)});
-  vs.push_back({"TL U1 encode", false, BLK(false, 1, true)});
-  vs.push_back({"TL U3 encode", false, BLK(false, 3, true)});
+  vs.push_back({"product AL U1 encode", false, BLK(false, 1, false)});
   vs.push_back({"product AL U2 encode (again)", false, BLK(false, 2, false)});
   vs.push_back({"product AL U2 recover", true, BLK(true, 2, false)});
-  vs.push_back({"TL U2 recover", true, BLK(true, 2, true)});
-  vs.push_back({"TL U1 recover", true, BLK(true, 1, true)});
-  vs.push_back({"TL U3 recover", true, BLK(true, 3, true)});
-  vs.push_back({"TL U4 encode", false, BLK(false, 4, true)});
-  vs.push_back({"TL U4 recover", true, BLK(true, 4, true)});
+  vs.push_back({"product AL U1 recover", true, BLK(true, 1, false)});
 
   std::vector<uint8_t> h_ref(OB), h_v(OB);
   std::vector<uint16_t> hp_ref(G), hp_v(G);
