@@ -622,6 +622,7 @@ def main(argv=None):
                                             args.cpu_threads)
         del host_rows
     line.setdefault("cpu_baseline", None)
+    line["summary"] = line_summary(line)  # last: the driver keeps the line's last 2 KB
     barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -630,6 +631,42 @@ def main(argv=None):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def line_summary(line):
+    """The legs' headline numbers, compact, as the LAST key of the line: the
+    driver keeps the last 2,000 characters of stdout, and the full legs
+    (connection_e2e, ceilings, protect, ...) are longer than that."""
+    def g(d, *path):
+        for p in path:
+            if not isinstance(d, dict) or p not in d:
+                return None
+            d = d[p]
+        return d
+    s = {"encode_frac": g(line, "roofline", "frac"),
+         "recover_frac": line.get("recover_roofline_frac"),
+         "traffic": g(line, "roofline", "traffic"),
+         "kernel_phased": (g(line, "roofline", "kernel") or "").startswith("phase_xor_kernel")}
+    for leg in ("one_pass", "ragged", "ragged_packed"):
+        if isinstance(line.get(leg), dict):
+            s[leg] = {kk: line[leg].get(kk) for kk in ("encode_frac", "recover_frac")}
+    if isinstance(line.get("ceilings"), dict):
+        s["encode_frac_of_read_ceiling"] = line["ceilings"].get("encode_frac_of_read_ceiling")
+    pr = line.get("protect")
+    if isinstance(pr, dict):
+        s["null_encrypt_hbm_frac"] = pr.get("encrypt_hbm_frac")
+        s["null_decrypt_scratch_out_hbm_frac"] = pr.get("decrypt_scratch_out_hbm_frac")
+    for leg, key in (("e2e_pinned_host", "encode_GiBps"), ("e2e_fec_gcm", "payload_GiBps")):
+        if isinstance(line.get(leg), dict):
+            s[f"{leg}_{key}"] = line[leg].get(key)
+    ce = line.get("connection_e2e")
+    if isinstance(ce, dict) and ce.get("runs"):
+        s["connection_e2e_host_us_per_group"] = {
+            str(r["connections"]): r.get("gpu_host_us_per_group") for r in ce["runs"]}
+    cb = line.get("cpu_baseline")
+    if isinstance(cb, dict):
+        s["cpu_baseline"] = {kk: cb.get(kk) for kk in ("value", "unit", "cores", "kind")}
+    return s
 
 
 def ragged_alg_bytes(G=1 << 20):
