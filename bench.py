@@ -1281,6 +1281,10 @@ def bench_connection_e2e():
             "gpu_host_us_per_group": round((r["fec_host_us"] - r["fec_wait_us"]) / max(1, groups), 3),
             "gpu_wait_us_per_launch": round(r["fec_wait_us"] / max(1, r["launches"]), 2),
             "launch_us_per_launch": round(r["fec_launch_us"] / max(1, r["launches"]), 2),
+            # of the launch: CSR tables / C-ABI calls per group; the slowest launch
+            "tables_us_per_group": round(r["fec_tables_us"] / max(1, groups), 3),
+            "capi_us_per_group": round(r["fec_call_us"] / max(1, groups), 3),
+            "launch_us_max": round(r["fec_launch_us_max"], 1),
             "cpu_1core_us_per_group": round(r["cpu_xor_us"] / enc, 3),
             "callbacks_incl_us_per_group": round(r["fec_wall_us"] / max(1, groups), 3),
             "run_s": round(wall, 2), "status": r["status"], "detail": r["detail"]})

@@ -36,7 +36,9 @@ class Result(C.Structure):
                                            "retransmitted_after_report retransmitted_of_revived "
                                            "protected_entropy_set").split()] +
                 [(n, C.c_int32) for n in ("server_close_error client_close_error "
-                                          "peer_saw_close closed_with_pending").split()])
+                                          "peer_saw_close closed_with_pending").split()] +
+                [(n, C.c_double) for n in ("fec_tables_us fec_call_us "
+                                           "fec_launch_us_max").split()])
 
 
 _lib = None

@@ -113,6 +113,9 @@ struct fec_conn_result {
   int32_t client_close_error;   // first client's QuicErrorCode if it closed, else 0
   int32_t peer_saw_close;       // server 0 closed by the peer (close_mid_batch)
   int32_t closed_with_pending;  // client 0 had a pending FEC packet when it closed
+  double fec_tables_us;         // of fec_launch_us: CSR tables
+  double fec_call_us;           // of fec_launch_us: the C-ABI calls queueing the launches
+  double fec_launch_us_max;     // the slowest single batcher Launch
 };
 }
 
@@ -692,6 +695,9 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     r->fec_host_us = batcher->stats().launch_us + batcher->stats().complete_us;
     r->fec_wait_us = batcher->stats().wait_us;
     r->fec_launch_us = batcher->stats().launch_us;
+    r->fec_tables_us = batcher->stats().tables_us;
+    r->fec_call_us = batcher->stats().call_us;
+    r->fec_launch_us_max = batcher->stats().launch_us_max;
   }
   r->turns = turn;
   r->stream_bytes = params->stream_len;

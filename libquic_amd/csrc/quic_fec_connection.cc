@@ -281,6 +281,7 @@ int QuicFecBatcher::Launch() {
   if (InFlight()) rc = Complete(true);
   if (enc_.empty() && rev_.empty()) return rc;
   const auto t0 = std::chrono::steady_clock::now();
+  const QuicFecGroup::LaunchProfile before = QuicFecGroup::launch_profile();
   enc_live_.swap(enc_);
   rev_live_.swap(rev_);
   std::vector<QuicFecGroup*> gs;
@@ -291,8 +292,13 @@ int QuicFecBatcher::Launch() {
   for (ReviveItem& e : rev_live_) gs.push_back(e.group.get());
   const int rrc = QuicFecGroup::Launch(ctx_, gs, &rev_pending_, /*async=*/true);
   ++stats_.launches;
-  stats_.launch_us += std::chrono::duration<double, std::micro>(
-                          std::chrono::steady_clock::now() - t0).count();
+  const double us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  stats_.launch_us += us;
+  stats_.launch_us_max = std::max(stats_.launch_us_max, us);
+  const QuicFecGroup::LaunchProfile& after = QuicFecGroup::launch_profile();
+  stats_.tables_us += after.tables_us - before.tables_us;
+  stats_.call_us += after.call_us - before.call_us;
   return erc ? erc : rrc;
 }
 

@@ -250,6 +250,12 @@ class QuicFecBatcher {
     // of complete_us: blocked in a waiting Complete(true) until the device
     // finished (a connection thread that polls with Complete(false) skips it)
     double wait_us = 0;
+    // of launch_us: the CSR tables over the payloads, and the C-ABI calls
+    // that queue the two launches (QuicFecGroup::launch_profile); the
+    // slowest single Launch
+    double tables_us = 0;
+    double call_us = 0;
+    double launch_us_max = 0;
   };
 
   explicit QuicFecBatcher(qfec_ctx* ctx = nullptr) : ctx_(ctx) {}

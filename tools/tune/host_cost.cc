@@ -1,8 +1,9 @@
 // host_cost.cc — where the connection thread's time goes in one batched FEC
 // launch (QuicFecBatcher::Launch at 4,096 connections
 // cost 0.44 us per group against 0.24 at 64).  N groups of 10 x 1350 B are
-// folded (QuicFecGroup::Update: the payloads copied into the pinned payload
-// arena, untimed), then per repetition:
+// folded round-robin over the groups (QuicFecGroup::Update: the payloads
+// copied into the pinned payload arena, untimed), the caches swept, then per
+// repetition:
 //   launch   QuicFecGroup::Launch(async): CSR tables over the arena
 //            payloads + qfec_encode_ragged(QFEC_PTR_MAPPED | QFEC_ASYNC)
 //   finish   QuicFecGroup::Finish(wait), of which `wait` is blocked on the GPU
@@ -48,6 +49,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   std::string pay(L, '\0');
+  std::vector<uint8_t> sweep(64u << 20);
   for (size_t i = 0; i < L; ++i) pay[i] = static_cast<char>(i * 131 + 7);
   for (size_t N : sizes) {
     const int reps = N >= 16384 ? 8 : 30;
@@ -58,16 +60,22 @@ int main(int argc, char** argv) {
       gs.reserve(N);
       for (size_t g = 0; g < N; ++g) {
         gs.emplace_back(new QuicFecGroup(1000 + 20 * g, ctx));
-        for (int i = 0; i < k; ++i) {
+        raw.push_back(gs.back().get());
+      }
+      // packets arrive round-robin over the connections (as in a server loop:
+      // every group's payloads interleaved with every other group's in the
+      // arena), then the thread does other work (a 64-MiB sweep evicts the
+      // groups from the caches) before the loop turn's launch
+      for (int i = 0; i < k; ++i)
+        for (size_t g = 0; g < N; ++g) {
           QuicPacketHeader h;
           h.packet_number = 1000 + 20 * g + i;
           h.is_in_fec_group = IN_FEC_GROUP;
           h.fec_group = 1000 + 20 * g;
           pay[0] = static_cast<char>(g + i);
-          gs.back()->Update(ENCRYPTION_FORWARD_SECURE, h, StringPiece(pay));
+          gs[g]->Update(ENCRYPTION_FORWARD_SECURE, h, StringPiece(pay));
         }
-        raw.push_back(gs.back().get());
-      }
+      for (size_t i = 0; i < sweep.size(); i += 64) sweep[i] += 1;
       QuicFecGroup::Pending p;
       const QuicFecGroup::LaunchProfile before = QuicFecGroup::launch_profile();
       const auto a0 = Clock::now();
