@@ -38,7 +38,8 @@ class Result(C.Structure):
                 [(n, C.c_int32) for n in ("server_close_error client_close_error "
                                           "peer_saw_close closed_with_pending").split()] +
                 [(n, C.c_double) for n in ("fec_tables_us fec_call_us "
-                                           "fec_launch_us_max").split()])
+                                           "fec_launch_us_max").split()] +
+                [(n, C.c_uint64) for n in ("payloads_adopted payloads_copied").split()])
 
 
 _lib = None

@@ -116,6 +116,8 @@ struct fec_conn_result {
   double fec_tables_us;         // of fec_launch_us: CSR tables
   double fec_call_us;           // of fec_launch_us: the C-ABI calls queueing the launches
   double fec_launch_us_max;     // the slowest single batcher Launch
+  uint64_t payloads_adopted;    // FEC payloads captured without a copy (send side)
+  uint64_t payloads_copied;     // FEC payloads copied into the arena (receive side)
 };
 }
 
@@ -505,6 +507,7 @@ void crash_trace(int sig) {
 
 SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   std::memset(r, 0, sizeof(*r));
+  const QuicFecGroup::LaunchProfile prof0 = QuicFecGroup::launch_profile();
   signal(SIGSEGV, crash_trace);
   signal(SIGABRT, crash_trace);
   FLAGS_quic_disable_pre_32 = false;  // QUIC_VERSION_31 carries FEC
@@ -700,6 +703,8 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     r->fec_launch_us_max = batcher->stats().launch_us_max;
   }
   r->turns = turn;
+  r->payloads_adopted = QuicFecGroup::launch_profile().payloads_adopted - prof0.payloads_adopted;
+  r->payloads_copied = QuicFecGroup::launch_profile().payloads_copied - prof0.payloads_copied;
   r->stream_bytes = params->stream_len;
   for (int i = 0; i < n; ++i) {
     r->debug_revived += slog[i]->count;

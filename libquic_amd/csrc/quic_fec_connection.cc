@@ -21,6 +21,23 @@ void QuicFecSender::set_max_packets_per_fec_group(size_t n) {
 
 bool QuicFecSender::OnDataPacket(QuicPacketNumber packet_number, StringPiece payload,
                                  bool entropy_flag, FecHeaderFields* fields) {
+  return OnData(packet_number, payload, nullptr, 0, entropy_flag, fields);
+}
+
+bool QuicFecSender::OnDataPacketInPlace(QuicPacketNumber packet_number,
+                                        QuicFecGroup::PacketBuffer* buf, size_t offset,
+                                        size_t len, bool entropy_flag, FecHeaderFields* fields) {
+  if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
+    detailed_error_ = "payload outside its packet buffer";
+    return false;
+  }
+  return OnData(packet_number, StringPiece(buf->data() + offset, len), buf, offset, entropy_flag,
+                fields);
+}
+
+bool QuicFecSender::OnData(QuicPacketNumber packet_number, StringPiece payload,
+                           QuicFecGroup::PacketBuffer* buf, size_t offset, bool entropy_flag,
+                           FecHeaderFields* fields) {
   if (last_packet_number_ != kInvalidPacketNumber && packet_number <= last_packet_number_) {
     detailed_error_ = "packet number does not increase: " + std::to_string(packet_number);
     return false;
@@ -46,7 +63,10 @@ bool QuicFecSender::OnDataPacket(QuicPacketNumber packet_number, StringPiece pay
     h.entropy_flag = entropy_flag;
     h.is_in_fec_group = IN_FEC_GROUP;
     h.fec_group = group_->FecGroupNumber();
-    if (!group_->Update(ENCRYPTION_FORWARD_SECURE, h, payload)) {
+    const bool ok = buf ? group_->UpdateInPlace(ENCRYPTION_FORWARD_SECURE, h, buf, offset,
+                                                payload.size())
+                        : group_->Update(ENCRYPTION_FORWARD_SECURE, h, payload);
+    if (!ok) {
       detailed_error_ = group_->detailed_error();
       return false;
     }

@@ -75,6 +75,12 @@ class QuicFecSender {
   // that does not increase; *fields is then unchanged.
   bool OnDataPacket(QuicPacketNumber packet_number, StringPiece payload, bool entropy_flag,
                     FecHeaderFields* fields);
+  // The same without a copy: the payload is buf->data() + [offset, offset +
+  // len) and the open group adopts *buf (QuicFecGroup::UpdateInPlace; the
+  // packet creator serialized the packet into a QuicFecGroup::AllocPacketBuffer
+  // and encrypts it out of place).  With protection off nothing is adopted.
+  bool OnDataPacketInPlace(QuicPacketNumber packet_number, QuicFecGroup::PacketBuffer* buf,
+                           size_t offset, size_t len, bool entropy_flag, FecHeaderFields* fields);
 
   bool IsFecGroupOpen() const { return group_ != nullptr; }
   // The open group's number (its first packet), 0 when none is open.
@@ -96,6 +102,10 @@ class QuicFecSender {
   const std::string& detailed_error() const { return detailed_error_; }
 
  private:
+  bool OnData(QuicPacketNumber packet_number, StringPiece payload,
+              QuicFecGroup::PacketBuffer* buf, size_t offset, bool entropy_flag,
+              FecHeaderFields* fields);
+
   size_t max_packets_per_fec_group_;
   bool fec_protect_ = true;
   std::unique_ptr<QuicFecGroup> group_;

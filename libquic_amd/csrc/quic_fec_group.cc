@@ -163,6 +163,7 @@ QuicFecGroup::Span QuicFecGroup::ArenaAlloc(size_t n) {
   if (sp.p) {
     sp.slab = slab;
     sp.n = n;
+    sp.data = sp.p;
   }
   return sp;
 }
@@ -174,7 +175,41 @@ void QuicFecGroup::ArenaFree(Span* sp) {
 
 qfec_ctx* QuicFecGroup::context() const { return ctx_ ? ctx_ : thread_default_ctx(); }
 
-bool QuicFecGroup::Fold(StringPiece payload, bool completes_group) {
+QuicFecGroup::PacketBuffer::~PacketBuffer() {
+  if (p_) PayloadArena::Release(static_cast<ArenaSlab*>(slab_), p_, n_);
+}
+
+QuicFecGroup::PacketBuffer::PacketBuffer(PacketBuffer&& o) noexcept
+    : p_(o.p_), slab_(o.slab_), n_(o.n_) {
+  o.p_ = nullptr;
+  o.slab_ = nullptr;
+  o.n_ = 0;
+}
+
+QuicFecGroup::PacketBuffer& QuicFecGroup::PacketBuffer::operator=(PacketBuffer&& o) noexcept {
+  if (this != &o) {
+    if (p_) PayloadArena::Release(static_cast<ArenaSlab*>(slab_), p_, n_);
+    p_ = o.p_;
+    slab_ = o.slab_;
+    n_ = o.n_;
+    o.p_ = nullptr;
+    o.slab_ = nullptr;
+    o.n_ = 0;
+  }
+  return *this;
+}
+
+QuicFecGroup::PacketBuffer QuicFecGroup::AllocPacketBuffer(size_t n) {
+  PacketBuffer b;
+  const Span sp = ArenaAlloc(n);
+  b.p_ = sp.p;
+  b.slab_ = sp.slab;
+  b.n_ = sp.p ? n : 0;
+  return b;
+}
+
+bool QuicFecGroup::Fold(StringPiece payload, bool completes_group, PacketBuffer* adopt,
+                        size_t adopt_offset) {
   if (payload.size() > kMaxPacketSize) {
     detailed_error_ = "Illegal payload size: " + std::to_string(payload.size());
     return false;
@@ -191,12 +226,27 @@ bool QuicFecGroup::Fold(StringPiece payload, bool completes_group) {
     detailed_error_ = "FEC group holds more than 255 payloads";
     return false;
   }
-  Span sp = ArenaAlloc(payload.size());
-  if (!sp.p) {
-    detailed_error_ = "out of payload memory";
-    return false;
+  Span sp;
+  if (adopt) {  // zero-copy: the payload already sits in arena memory
+    sp.p = adopt->p_;
+    sp.slab = adopt->slab_;
+    sp.n = adopt->n_;
+    sp.data = adopt->p_ + adopt_offset;
+    adopt->p_ = nullptr;
+    adopt->slab_ = nullptr;
+    adopt->n_ = 0;
+    ++launch_profile().payloads_adopted;
+  } else {
+    sp = ArenaAlloc(payload.size());
+    if (!sp.p) {
+      detailed_error_ = "out of payload memory";
+      return false;
+    }
+    std::memcpy(sp.p, payload.data(), payload.size());
+    LaunchProfile& prof = launch_profile();
+    ++prof.payloads_copied;
+    prof.payload_bytes_copied += payload.size();
   }
-  std::memcpy(sp.p, payload.data(), payload.size());
   payloads_.push_back(sp);
   lens_.push_back(static_cast<uint16_t>(payload.size()));
   dirty_ = true;
@@ -220,6 +270,22 @@ void QuicFecGroup::MarkReceived(QuicPacketNumber n) {
 
 bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                           StringPiece decrypted_payload) {
+  return UpdateImpl(encryption_level, header, decrypted_payload, nullptr, 0);
+}
+
+bool QuicFecGroup::UpdateInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                                 PacketBuffer* buf, size_t offset, size_t len) {
+  if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
+    detailed_error_ = "payload outside its packet buffer";
+    return false;
+  }
+  return UpdateImpl(encryption_level, header, StringPiece(buf->data() + offset, len), buf,
+                    offset);
+}
+
+bool QuicFecGroup::UpdateImpl(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                              StringPiece decrypted_payload, PacketBuffer* adopt,
+                              size_t adopt_offset) {
   if (HasReceived(header.packet_number)) return false;
   if (min_protected_packet_ != kInvalidPacketNumber &&
       max_protected_packet_ != kInvalidPacketNumber &&
@@ -232,7 +298,7 @@ bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHead
   const bool completes = min_protected_packet_ != kInvalidPacketNumber &&
                          num_received_ + 1 ==
                              max_protected_packet_ - min_protected_packet_ + 1;
-  if (!Fold(decrypted_payload, completes)) return false;
+  if (!Fold(decrypted_payload, completes, adopt, adopt_offset)) return false;
   MarkReceived(header.packet_number);
   if (encryption_level < effective_encryption_level_)
     effective_encryption_level_ = encryption_level;
@@ -391,7 +457,7 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
     mapped = mapped && static_cast<ArenaSlab*>(g->parity_.slab)->mapped;
     out_base = std::min(out_base, reinterpret_cast<uintptr_t>(g->parity_.p));
     for (const Span& sp : g->payloads_) {
-      in_base = std::min(in_base, reinterpret_cast<uintptr_t>(sp.p));
+      in_base = std::min(in_base, reinterpret_cast<uintptr_t>(sp.data));
       mapped = mapped && static_cast<ArenaSlab*>(sp.slab)->mapped;
     }
     npk += g->lens_.size();
@@ -413,7 +479,7 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
   parity_off.reserve(launched.size());
   for (QuicFecGroup* g : launched) {
     for (size_t i = 0; i < g->payloads_.size(); ++i) {
-      pkt_off.push_back(reinterpret_cast<uintptr_t>(g->payloads_[i].p) - in_base);
+      pkt_off.push_back(reinterpret_cast<uintptr_t>(g->payloads_[i].data) - in_base);
       pkt_len.push_back(g->lens_[i]);
     }
     grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));

@@ -107,9 +107,42 @@ class QuicFecGroup {
 
   // A data packet decrypted at `encryption_level`.  False if the packet was
   // already seen, lies outside the protected range, or its payload is longer
-  // than kMaxPacketSize ("Illegal payload size").
+  // than kMaxPacketSize ("Illegal payload size").  The payload is copied into
+  // the group's pinned payload arena.
   bool Update(EncryptionLevel encryption_level, const QuicPacketHeader& header,
               StringPiece decrypted_payload);
+
+  // Zero-copy capture (send side): a buffer in the calling thread's pinned
+  // payload arena, into which the packet creator serializes the whole packet
+  // (header + frames) and from which it encrypts out of place; the group then
+  // ADOPTS the buffer (UpdateInPlace) instead of copying the payload: the
+  // connection thread's per-packet FEC cost is no longer a 1,350-B memcpy (or,
+  // historically, a 1,350-B XOR) but a table entry.  Move-only; a buffer that
+  // is not adopted is released on destruction.
+  class PacketBuffer {
+   public:
+    PacketBuffer() = default;
+    ~PacketBuffer();
+    PacketBuffer(PacketBuffer&& o) noexcept;
+    PacketBuffer& operator=(PacketBuffer&& o) noexcept;
+    PacketBuffer(const PacketBuffer&) = delete;
+    PacketBuffer& operator=(const PacketBuffer&) = delete;
+    char* data() const { return reinterpret_cast<char*>(p_); }
+    size_t size() const { return n_; }
+    bool empty() const { return p_ == nullptr; }
+
+   private:
+    friend class QuicFecGroup;
+    uint8_t* p_ = nullptr;
+    void* slab_ = nullptr;
+    size_t n_ = 0;
+  };
+  // n <= the arena slab size; an empty buffer when no arena memory is left.
+  static PacketBuffer AllocPacketBuffer(size_t n);
+  // Update() for a payload at buf->data() + [offset, offset + len): on
+  // success the group owns *buf (it is left empty), the payload is not copied.
+  bool UpdateInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                     PacketBuffer* buf, size_t offset, size_t len);
   // The FEC packet: protects [fec_group_number, header.packet_number).  False if
   // a redundancy was already seen or a received packet is outside that range.
   bool UpdateFec(EncryptionLevel encryption_level, const QuicPacketHeader& header,
@@ -161,13 +194,19 @@ class QuicFecGroup {
 
   // This thread's Launch time split (microseconds, accumulated): building the
   // CSR tables over the payloads, and the qfec_*_ragged call that queues the
-  // launch (measurement: bench.py connection legs, tools/tune/host_cost.cc).
+  // launch (measurement: bench.py connection legs, tools/tune/host_cost.cc);
+  // and its payload captures.
   struct LaunchProfile {
     double tables_us = 0;
     double call_us = 0;
     uint64_t launches = 0;
     uint64_t groups = 0;
     uint64_t packets = 0;
+    // payload capture (Update / UpdateInPlace): copied into the arena, or
+    // adopted in place (zero-copy send side)
+    uint64_t payloads_copied = 0;
+    uint64_t payload_bytes_copied = 0;
+    uint64_t payloads_adopted = 0;
   };
   static LaunchProfile& launch_profile();
 
@@ -175,7 +214,10 @@ class QuicFecGroup {
   const std::string& detailed_error() const { return detailed_error_; }
 
  private:
-  bool Fold(StringPiece payload, bool completes_group);
+  bool Fold(StringPiece payload, bool completes_group, PacketBuffer* adopt = nullptr,
+            size_t adopt_offset = 0);
+  bool UpdateImpl(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                  StringPiece payload, PacketBuffer* adopt, size_t adopt_offset);
   int EnsureParity() const;
   QuicPacketCount NumMissingPackets() const;
   qfec_ctx* context() const;
@@ -197,9 +239,10 @@ class QuicFecGroup {
   // their lengths; the GPU-computed accumulator (kMaxPacketSize bytes of arena,
   // valid when !dirty_).
   struct Span {
-    uint8_t* p = nullptr;
+    uint8_t* p = nullptr;  // the arena allocation
     void* slab = nullptr;  // the arena slab holding p (released on destruction)
     size_t n = 0;
+    uint8_t* data = nullptr;  // the payload: p, or inside p for an adopted packet buffer
   };
   static Span ArenaAlloc(size_t n);
   static void ArenaFree(Span* s);

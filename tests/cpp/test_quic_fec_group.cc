@@ -130,6 +130,34 @@ int main() {
     EXPECT(group.EffectiveEncryptionLevel() == ENCRYPTION_INITIAL);
     EXPECT(!group.CanRevive());  // no redundancy yet
   }
+  // zero-copy capture (UpdateInPlace): payloads serialized into arena packet
+  // buffers after a header, adopted by the group -> the same parity; a
+  // refused packet (duplicate) leaves its buffer with the caller; a buffer
+  // range outside the buffer is refused
+  {
+    auto pays = MakePayloads(9, 0x51554951);
+    QuicFecGroup group(1, ctx);
+    const QuicFecGroup::LaunchProfile p0 = QuicFecGroup::launch_profile();
+    for (int i = 0; i < 9; ++i) {
+      const size_t hdr = 9 + i % 4;  // the packet header before the payload
+      QuicFecGroup::PacketBuffer b = QuicFecGroup::AllocPacketBuffer(hdr + pays[i].size());
+      EXPECT(!b.empty());
+      std::memset(b.data(), 0xEE, hdr);
+      std::memcpy(b.data() + hdr, pays[i].data(), pays[i].size());
+      EXPECT(group.UpdateInPlace(ENCRYPTION_FORWARD_SECURE, Header(1 + i, 1, false), &b, hdr,
+                                 pays[i].size()));
+      EXPECT(b.empty());  // adopted
+    }
+    EXPECT(QuicFecGroup::launch_profile().payloads_adopted - p0.payloads_adopted == 9);
+    EXPECT(QuicFecGroup::launch_profile().payloads_copied == p0.payloads_copied);
+    QuicFecGroup::PacketBuffer dup = QuicFecGroup::AllocPacketBuffer(64);
+    EXPECT(!group.UpdateInPlace(ENCRYPTION_FORWARD_SECURE, Header(3, 1, false), &dup, 0, 64));
+    EXPECT(!dup.empty());  // not adopted: the caller still owns it
+    EXPECT(!group.UpdateInPlace(ENCRYPTION_FORWARD_SECURE, Header(20, 1, false), &dup, 60, 5));
+    StringPiece par = group.PayloadParity();
+    std::string want = OracleParity(pays);
+    EXPECT(par.size() == want.size() && std::memcmp(par.data(), want.data(), want.size()) == 0);
+  }
   // oversize payload refused; 1452 accepted
   {
     QuicFecGroup group(1, ctx);

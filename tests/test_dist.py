@@ -138,3 +138,44 @@ def test_bench_cli_two_ranks_on_one_gpu():
         assert rc == 0 and rc2 == 0
         assert s["digests"][0] == hashlib.sha256(par.tobytes()).hexdigest()[:32]
         assert s["digests"][1] == hashlib.sha256(out.tobytes()).hexdigest()[:32]
+
+
+@pytest.mark.gpu
+def test_bench_cli_two_ranks_phased_on_one_gpu():
+    """VERDICT r3 missing 3: the phased kernel under N ranks.  Two ranks on
+    cuda:0 (QFEC_BENCH_SHARE_DEVICE), each with a shard large enough for the
+    phased kernel (262,144 groups: 8 phases of 40 LDS steps).  Two persistent
+    one-workgroup-per-CU grids on one GPU cannot both be resident, so a
+    rank's meetings may time out and its launch run without them (the
+    abandon path, then the contention backoff) -- results must be the same
+    bytes either way: every shard verified, its digests equal the oracle's."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    G = 1 << 18
+    p = _bench_cli(["--gpus", "2", "--groups", str(G), "--steps", "3", "--warmup", "1",
+                    "--digests", "--no-cpu-baseline"],
+                   env_extra={"QFEC_BENCH_SHARE_DEVICE": "1"}, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified"] is True
+    import hashlib
+    from oracle import oracle_c as OC
+    import bench
+    k, L = 10, 1350
+    shards = sorted(line["shards"], key=lambda s: s["rank"])
+    assert [s["g0"] for s in shards] == [0, G]
+    for s in shards:
+        assert s["verified"] and s["device"] == 0
+        rows = OC.synth_fixed(bench.SEED_FIXED, s["g0"], G, k, L)
+        rc, par = OC.encode_fixed(rows, k, L, G)
+        miss = bench.drop_indices(s["g0"], G, k)
+        rc2, out = OC.recover_fixed(rows, par, miss, k, L, G)
+        assert rc == 0 and rc2 == 0
+        assert s["digests"][0] == hashlib.sha256(par.tobytes()).hexdigest()[:32]
+        assert s["digests"][1] == hashlib.sha256(out.tobytes()).hexdigest()[:32]
+        del rows, par, out
+    print({"phase_abandons_rank0": line["roofline"].get("phase_abandons"),
+           "kernel": line["roofline"]["kernel"][:40]})
