@@ -116,8 +116,8 @@ struct fec_conn_result {
   double fec_tables_us;         // of fec_launch_us: CSR tables
   double fec_call_us;           // of fec_launch_us: the C-ABI calls queueing the launches
   double fec_launch_us_max;     // the slowest single batcher Launch
-  uint64_t payloads_adopted;    // FEC payloads captured without a copy (send side)
-  uint64_t payloads_copied;     // FEC payloads copied into the arena (receive side)
+  uint64_t payloads_adopted;    // FEC payloads captured without a copy (both sides)
+  uint64_t payloads_copied;     // FEC payloads copied into the arena
 };
 }
 

@@ -155,6 +155,7 @@ QuicFecGroup* QuicFecReceiver::GetFecGroup(QuicFecGroupNumber n) {
     // and is not recreated; otherwise the lowest group is dropped.
     if (n < group_map_.begin()->first) return nullptr;
     MarkClosed(group_map_.begin()->first);
+    Retire(std::move(group_map_.begin()->second));
     group_map_.erase(group_map_.begin());
   }
   QuicFecGroup* g = new QuicFecGroup(n);
@@ -164,6 +165,28 @@ QuicFecGroup* QuicFecReceiver::GetFecGroup(QuicFecGroupNumber n) {
 
 bool QuicFecReceiver::OnPacket(EncryptionLevel level, const QuicPacketHeader& header,
                                StringPiece payload) {
+  return OnPacketImpl(level, header, payload, nullptr, 0);
+}
+
+bool QuicFecReceiver::OnPacketInPlace(EncryptionLevel level, const QuicPacketHeader& header,
+                                      QuicFecGroup::PacketBuffer* buf, size_t offset, size_t len) {
+  if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
+    detailed_error_ = "payload outside its packet buffer";
+    return false;
+  }
+  return OnPacketImpl(level, header, StringPiece(buf->data() + offset, len), buf, offset);
+}
+
+void QuicFecReceiver::Retire(std::unique_ptr<QuicFecGroup> g) {
+  retired_.push_back(std::move(g));
+}
+
+bool QuicFecReceiver::OnPacketImpl(EncryptionLevel level, const QuicPacketHeader& header,
+                                   StringPiece payload, QuicFecGroup::PacketBuffer* buf,
+                                   size_t offset) {
+  // groups dropped while an earlier packet was processed: its frames have
+  // been parsed by now, so the payloads they adopted can go
+  retired_.clear();
   if (header.is_in_fec_group != IN_FEC_GROUP || header.fec_group == 0) {
     detailed_error_ = "packet is not in an FEC group";
     return false;
@@ -173,15 +196,22 @@ bool QuicFecReceiver::OnPacket(EncryptionLevel level, const QuicPacketHeader& he
     detailed_error_ = "FEC group already closed";
     return false;
   }
-  const bool ok = header.fec_flag ? g->UpdateFec(level, header, payload)
-                                  : g->Update(level, header, payload);
+  bool ok;
+  if (buf)
+    ok = header.fec_flag ? g->UpdateFecInPlace(level, header, buf, offset, payload.size())
+                         : g->UpdateInPlace(level, header, buf, offset, payload.size());
+  else
+    ok = header.fec_flag ? g->UpdateFec(level, header, payload)
+                         : g->Update(level, header, payload);
   if (!ok) {
     detailed_error_ = g->detailed_error();
     return false;
   }
   if (g->IsFinished()) {  // nothing lost: no revival needed, stop tracking
     MarkClosed(header.fec_group);
-    group_map_.erase(header.fec_group);
+    auto it = group_map_.find(header.fec_group);
+    Retire(std::move(it->second));
+    group_map_.erase(it);
   }
   return true;
 }
@@ -197,6 +227,7 @@ void QuicFecReceiver::CloseFecGroupsBefore(QuicPacketNumber packet_number) {
   for (auto it = group_map_.begin(); it != group_map_.end();) {
     if (it->second->IsWaitingForPacketBefore(packet_number)) {
       MarkClosed(it->first);
+      Retire(std::move(it->second));
       it = group_map_.erase(it);
     } else {
       ++it;

@@ -161,6 +161,11 @@ class QuicFecReceiver {
   // not taken: not in a group, its group was already evicted, or the group
   // refused it (duplicate, outside the protected range, oversize).
   bool OnPacket(EncryptionLevel level, const QuicPacketHeader& header, StringPiece payload);
+  // The same without a copy: the payload is buf->data() + [offset, offset +
+  // len) -- the framer decrypted the packet into this payload-arena buffer --
+  // and its group adopts *buf (left empty) when it takes the packet.
+  bool OnPacketInPlace(EncryptionLevel level, const QuicPacketHeader& header,
+                       QuicFecGroup::PacketBuffer* buf, size_t offset, size_t len);
 
   // Drop every group still waiting for a packet below `packet_number` (the
   // peer stopped waiting for them: STOP_WAITING / least unacked).
@@ -177,6 +182,12 @@ class QuicFecReceiver {
   const std::string& detailed_error() const { return detailed_error_; }
 
  private:
+  bool OnPacketImpl(EncryptionLevel level, const QuicPacketHeader& header, StringPiece payload,
+                    QuicFecGroup::PacketBuffer* buf, size_t offset);
+  // A dropped group is kept until the next packet: it may hold (adopted) the
+  // buffer the packet being processed was decrypted into, whose frames the
+  // framer is still parsing (a STOP_WAITING frame closes groups mid-packet).
+  void Retire(std::unique_ptr<QuicFecGroup> g);
   QuicFecGroup* GetFecGroup(QuicFecGroupNumber n);
   void MarkClosed(QuicFecGroupNumber n);
 
@@ -187,6 +198,7 @@ class QuicFecReceiver {
   size_t max_fec_groups_;
   std::map<QuicFecGroupNumber, std::unique_ptr<QuicFecGroup>> group_map_;
   std::set<QuicFecGroupNumber> closed_;
+  std::vector<std::unique_ptr<QuicFecGroup>> retired_;
   std::string detailed_error_;
 };
 

@@ -307,6 +307,23 @@ bool QuicFecGroup::UpdateImpl(EncryptionLevel encryption_level, const QuicPacket
 
 bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                              StringPiece redundancy) {
+  return UpdateFecImpl(encryption_level, header, redundancy, nullptr, 0);
+}
+
+bool QuicFecGroup::UpdateFecInPlace(EncryptionLevel encryption_level,
+                                    const QuicPacketHeader& header, PacketBuffer* buf,
+                                    size_t offset, size_t len) {
+  if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
+    detailed_error_ = "redundancy outside its packet buffer";
+    return false;
+  }
+  return UpdateFecImpl(encryption_level, header, StringPiece(buf->data() + offset, len), buf,
+                       offset);
+}
+
+bool QuicFecGroup::UpdateFecImpl(EncryptionLevel encryption_level,
+                                 const QuicPacketHeader& header, StringPiece redundancy,
+                                 PacketBuffer* adopt, size_t adopt_offset) {
   if (min_protected_packet_ != kInvalidPacketNumber) return false;  // redundancy already seen
   const QuicPacketNumber fec_packet_number = header.packet_number;
   if (fec_packet_number <= fec_group_number_ ||
@@ -328,7 +345,7 @@ bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketH
     return false;
   }
   const bool completes = num_received_ == span;
-  if (!Fold(redundancy, completes)) return false;
+  if (!Fold(redundancy, completes, adopt, adopt_offset)) return false;
   min_protected_packet_ = fec_group_number_;
   max_protected_packet_ = fec_packet_number - 1;
   if (encryption_level < effective_encryption_level_)

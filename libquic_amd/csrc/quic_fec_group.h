@@ -143,6 +143,10 @@ class QuicFecGroup {
   // success the group owns *buf (it is left empty), the payload is not copied.
   bool UpdateInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                      PacketBuffer* buf, size_t offset, size_t len);
+  // UpdateFec() for a redundancy at buf->data() + [offset, offset + len)
+  // (receive side: the framer decrypted the packet into the arena buffer).
+  bool UpdateFecInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                        PacketBuffer* buf, size_t offset, size_t len);
   // The FEC packet: protects [fec_group_number, header.packet_number).  False if
   // a redundancy was already seen or a received packet is outside that range.
   bool UpdateFec(EncryptionLevel encryption_level, const QuicPacketHeader& header,
@@ -218,6 +222,8 @@ class QuicFecGroup {
             size_t adopt_offset = 0);
   bool UpdateImpl(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                   StringPiece payload, PacketBuffer* adopt, size_t adopt_offset);
+  bool UpdateFecImpl(EncryptionLevel encryption_level, const QuicPacketHeader& header,
+                     StringPiece redundancy, PacketBuffer* adopt, size_t adopt_offset);
   int EnsureParity() const;
   QuicPacketCount NumMissingPackets() const;
   qfec_ctx* context() const;

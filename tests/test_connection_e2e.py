@@ -100,9 +100,11 @@ def test_fec_without_device_skips_groups(batched):
     assert r["fec_packets_sent"] == 0 and r["revived"] == 0
     assert r["fec_groups_skipped"] > 0
     assert r["dropped"] > 0 and r["retransmitted"] >= r["dropped"]
-    # zero-copy capture: every protected packet was serialized into an arena
-    # buffer its group adopted (heap arena without a device)
-    assert r["payloads_adopted"] == r["data_packets_sent"] > 0, r
+    # zero-copy capture: every protected packet was serialized (sender) and
+    # decrypted (receiver) into an arena buffer its group adopted -- heap
+    # arena without a device -- and no payload was copied
+    assert r["payloads_copied"] == 0, r
+    assert r["payloads_adopted"] >= r["data_packets_sent"] > 0, r
 
 
 def test_unencrypted_fec_data_closes_the_connection():
@@ -152,8 +154,8 @@ def test_connection_fec_revives_every_single_loss(batched, group_size, drop_ever
         assert r["groups_encoded"] == r["fec_packets_sent"], r
         assert r["groups_revived"] == r["revived"], r
     _check_revived_channel(r)
-    # zero-copy send-side capture: no protected payload copied on the sender
-    assert r["payloads_adopted"] == r["data_packets_sent"], r
+    # zero-copy capture on both sides: no protected payload copied
+    assert r["payloads_copied"] == 0 and r["payloads_adopted"] >= r["data_packets_sent"], r
     print({k: r[k] for k in ("turns", "data_packets_sent", "fec_packets_sent", "dropped",
                              "revived", "retransmitted", "launches", "revived_reported",
                              "acks_with_revived", "retransmitted_of_revived",
