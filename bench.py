@@ -1285,6 +1285,8 @@ def bench_connection_e2e():
             "tables_us_per_group": round(r["fec_tables_us"] / max(1, groups), 3),
             "capi_us_per_group": round(r["fec_call_us"] / max(1, groups), 3),
             "launch_us_max": round(r["fec_launch_us_max"], 1),
+            "arena_slabs_allocated": r["slabs_allocated"],
+            "payloads_copied": r["payloads_copied"], "payloads_adopted": r["payloads_adopted"],
             "cpu_1core_us_per_group": round(r["cpu_xor_us"] / enc, 3),
             "callbacks_incl_us_per_group": round(r["fec_wall_us"] / max(1, groups), 3),
             "run_s": round(wall, 2), "status": r["status"], "detail": r["detail"]})

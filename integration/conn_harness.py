@@ -39,7 +39,8 @@ class Result(C.Structure):
                                           "peer_saw_close closed_with_pending").split()] +
                 [(n, C.c_double) for n in ("fec_tables_us fec_call_us "
                                            "fec_launch_us_max").split()] +
-                [(n, C.c_uint64) for n in ("payloads_adopted payloads_copied").split()])
+                [(n, C.c_uint64) for n in ("payloads_adopted payloads_copied "
+                                           "slabs_allocated").split()])
 
 
 _lib = None

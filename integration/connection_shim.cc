@@ -118,6 +118,7 @@ struct fec_conn_result {
   double fec_launch_us_max;     // the slowest single batcher Launch
   uint64_t payloads_adopted;    // FEC payloads captured without a copy (both sides)
   uint64_t payloads_copied;     // FEC payloads copied into the arena
+  uint64_t slabs_allocated;     // payload-arena slabs allocated during the run
 };
 }
 
@@ -705,6 +706,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   r->turns = turn;
   r->payloads_adopted = QuicFecGroup::launch_profile().payloads_adopted - prof0.payloads_adopted;
   r->payloads_copied = QuicFecGroup::launch_profile().payloads_copied - prof0.payloads_copied;
+  r->slabs_allocated = QuicFecGroup::launch_profile().slabs_allocated - prof0.slabs_allocated;
   r->stream_bytes = params->stream_len;
   for (int i = 0; i < n; ++i) {
     r->debug_revived += slog[i]->count;

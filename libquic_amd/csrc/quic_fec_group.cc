@@ -113,6 +113,7 @@ class PayloadArena {
       return s;
     }
     ArenaSlab* s = new ArenaSlab();
+    ++QuicFecGroup::launch_profile().slabs_allocated;
     if (mapped_ok_) {
       s->base = static_cast<uint8_t*>(qfec_host_alloc(kSlabBytes));
       s->mapped = s->base != nullptr;

@@ -211,6 +211,9 @@ class QuicFecGroup {
     uint64_t payloads_copied = 0;
     uint64_t payload_bytes_copied = 0;
     uint64_t payloads_adopted = 0;
+    // 32-MiB payload-arena slabs this thread allocated (pinned: a
+    // hipHostMalloc each, milliseconds) -- growth inside a timed loop shows here
+    uint64_t slabs_allocated = 0;
   };
   static LaunchProfile& launch_profile();
 
