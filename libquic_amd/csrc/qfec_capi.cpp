@@ -202,7 +202,8 @@ int collect_error(qfec_ctx* ctx, hipStream_t stream, int word = kErrStream);
 
 // Finish the QFEC_ASYNC op of slot `si`: QFEC_PENDING if it is still running
 // and !wait; otherwise its encode lengths are copied out and its error word
-// collected (batches above kDirectGroups latch kernel-side errors).
+// collected (staged batches latch kernel-side errors; direct ones were
+// validated on the host).
 int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   qfec_ctx::AsyncOp& op = ctx->async_ops[si];
   if (!op.live) return QFEC_OK;
@@ -1179,12 +1180,18 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   } else {
     drain_async(ctx);
   }
-  // A small batch (the connection thread's flush of a few groups) is
-  // latency-bound: the kernel reads the tables from the mapped slot buffer and
-  // writes the encode lengths straight into the mapped output buffer — no
-  // copies, one launch and one synchronisation — and the error word is not
-  // fetched: validate_ragged checked every condition the kernel latches.
-  const bool direct = n <= std::min<uint64_t>(out_cap, kDirectGroups);
+  // A batch whose tables fit one slot (every batch a connection thread
+  // flushes) runs DIRECT: the kernel reads the tables from the mapped slot
+  // buffer and writes the encode lengths straight into the mapped output
+  // buffer, and its last workgroup stores a completion token into
+  // host-mapped memory -- no staging copies, no event, one launch -- and the
+  // error word is not fetched: validate_ragged checked every condition the
+  // kernel latches.  Up to kDirectGroups groups the small-batch kernel (one
+  // wave per group, every load of a group in flight at once: latency over
+  // PCIe), above that the block kernel.  (Round 3 staged the tables of
+  // batches above kDirectGroups to the device and waited on an event.)
+  const bool direct =
+      n <= out_cap && Tab(grp_ptr[n] - grp_ptr[0], n, recover).total <= kStageBytes;
   uint64_t g = 0;
   while (g < n) {
     const uint64_t g0 = g;
@@ -1236,7 +1243,10 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       a.done_count = ctx->d_done + slot;
       a.done_flag = ctx->h_flag_dev + slot;
       a.done_token = token;
-      QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
+      if (cnt <= kDirectGroups)
+        QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
+      else
+        QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
     } else {
       QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
     }

@@ -1016,7 +1016,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
 // DIAG (tools/tune only, not exact): 1 = no parity stores.
 template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
-__global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
+__device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
   constexpr uint32_t NT = 64u * WAVES;
   constexpr uint32_t NBLK = NT;        // 64-window blocks: CAPW = 64 NT windows
@@ -1221,6 +1221,37 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
 }
 
 
+// Completion signal for a host that spins on mapped memory instead of
+// waiting on an event (~6 us less per flush, tools/tune/tune_latency): every
+// thread's stores (outputs in mapped host memory) are made visible
+// system-wide, the block is counted, and the last block to finish resets the
+// counter and stores the token into the host-mapped flag.  Block-uniform
+// call, after the block's work.
+__device__ __forceinline__ void ragged_signal_done(const RaggedArgs& a) {
+  if (a.done_flag == nullptr) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.done_count, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(a.done_flag, a.done_token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// The block kernel; with done_flag set (mapped batches of any size, round 4)
+// it signals completion like the small-batch kernel, so the host neither
+// stages the tables nor waits on an event.
+template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
+__global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) {
+  ragged_block_body<RECOVER, WAVES, GPB, U, PF, AL, DIAG>(a);
+  ragged_signal_done(a);
+}
+
+
 // Ragged CSR, parity-window form — the SMALL-BATCH (latency) kernel: the
 // mapped host path runs a batch of <= kDirectGroups groups with it
 // (qfec_capi.cpp ragged_mapped), where the payloads are read over PCIe and a
@@ -1353,23 +1384,7 @@ __global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t g = (uint64_t)blockIdx.x * kFlatWaves + wv;
   if (g < a.n_groups) window_group<RECOVER, NT, PB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-  if (a.done_flag == nullptr) return;
-  // Completion signal for a host that spins on mapped memory instead of
-  // waiting on an event (~6 us less per small flush, tools/tune/tune_latency):
-  // every thread's stores (outputs in mapped host memory) are made visible
-  // system-wide, the block is counted, and the last block to finish resets
-  // the counter and stores the token into the host-mapped flag.
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(a.done_count, 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1u) {
-      __hip_atomic_store(a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      __hip_atomic_store(a.done_flag, a.done_token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  ragged_signal_done(a);
 }
 
 // ---------------------------------------------------------------------------

@@ -247,7 +247,8 @@ def test_registered_host_memory(ctx):
 def test_ragged_mapped_async(ctx, n):
     """QFEC_ASYNC (the event-loop form): an encode and a recover are queued on
     one context without waiting (n <= 256: the flag-completed latency path;
-    2000: the staged-table path), polled with qfec_complete(wait=0), then
+    2000: the block kernel, also reading its tables in place and signalling
+    through the flag since round 4), polled with qfec_complete(wait=0), then
     completed; the outputs — bytes and the encode lengths, which arrive only
     at completion — equal the oracle's, and equal a synchronous call's."""
     z, want_l = _mapped_case(n, g0=4000 + n, kmin=2, kmax=40, lmin=1, lmax=1452)
