@@ -136,3 +136,43 @@ def test_v32_ack_has_no_revived_list():
     r = R.parse(32, pkt)
     assert r["accepted"] == 1 and r["n_ping"] == 1, r
     assert parse_patched(L, 32, pkt)[0] == []
+
+
+def test_revived_list_property_vs_reference():
+    """Random acks (missing sets over up to 1,000 packets, random revived
+    subsets of them, 1- to 6-byte largest observed, packet capacities from
+    200 B): the unpatched reference framer accepts every ack the patched
+    writer produces, and the patched reader returns the NEWEST revived
+    packets at or below the largest observed the ack carries -- all of them
+    when they fit (at most 255)."""
+    from hypothesis import given, settings, strategies as st, HealthCheck
+    L, R = _libs()
+
+    @settings(max_examples=150, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(st.integers(2, 2**40), st.lists(st.integers(1, 1000), min_size=1, max_size=300),
+           st.data(), st.sampled_from([200, 400, 1452]), st.booleans())
+    def check(largest, back, data, cap, ping):
+        miss = sorted({largest - b for b in back if largest - b >= 1})
+        if not miss:
+            return
+        # as [lo, hi) ranges
+        ranges, lo = [], miss[0]
+        for a, b in zip(miss, miss[1:] + [None]):
+            if b != a + 1:
+                ranges.append((lo, a + 1))
+                lo = b
+        revived = sorted(set(data.draw(st.lists(st.sampled_from(miss), max_size=300))))
+        pkt = build(L, 31, largest + 1, largest, ranges, revived, ping=ping, cap=cap)
+        r = R.parse(31, pkt)
+        assert r["accepted"] == 1 and r["n_ack"] == 1, r
+        if ping and r["n_ping"] == 0:
+            # the ping did not fit after the ack (ack truncated to the packet)
+            pass
+        got, _, lo_written = parse_patched(L, 31, pkt)
+        assert lo_written == r["ack_largest_observed"]
+        want = sorted((x for x in revived if x <= lo_written), reverse=True)
+        assert got == sorted(want[:len(got)])
+        if len(pkt) + 8 < cap - 12:  # room was left: nothing was cut
+            assert len(got) == min(255, len(want))
+
+    check()
