@@ -39,6 +39,12 @@ SRC = os.path.join(OUT, "src")
 CORE = os.path.join(SRC, "net", "quic", "core")
 PATCH = os.path.join(HERE, "libquic_fec.patch")
 LIB = os.path.join(OUT, "libquic_fec_patched.so")
+# the same objects linked against tests/cpp/cpu_qfec_stub.c (a CPU restatement
+# of the qfec entry points the host code calls) instead of libqfec.so: TEST
+# INFRASTRUCTURE, so the connection path's FEC (groups, arena, zero-copy
+# capture, revival, acks) runs in the CPU suite; never loaded by the product
+LIB_CPU = os.path.join(OUT, "libquic_fec_patched_cpustub.so")
+STUB = os.path.join(ROOT, "tests", "cpp", "cpu_qfec_stub.c")
 
 PATCHED = ["quic_protocol.h", "quic_protocol.cc", "quic_framer.h", "quic_framer.cc",
            "quic_connection_stats.h", "quic_connection_stats.cc",
@@ -200,6 +206,11 @@ def build_lib() -> str:
                     "-Wl,-rpath,$ORIGIN/../../libquic_amd", "-Wl,-rpath-link,/opt/rocm/lib"],
                    check=True)
     os.replace(LIB + ".tmp", LIB)
+    stub = _obj(STUB, ["gcc", "-std=c11", "-O2", "-fPIC", "-fvisibility=hidden", "-I",
+                       os.path.join(ROOT, "include")], "cpu_qfec_stub")
+    subprocess.run(["g++", "-shared", "-pthread", "-Wl,--gc-sections", "-Wl,-z,defs", "-Wl,-Bsymbolic",
+                    "-o", LIB_CPU + ".tmp", *objs, stub], check=True)
+    os.replace(LIB_CPU + ".tmp", LIB_CPU)
     return LIB
 
 

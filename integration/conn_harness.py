@@ -10,6 +10,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "libquic_fec_patched.so")
+# the same build over tests/cpp/cpu_qfec_stub.c (CPU parity in place of the
+# GPU): lets the CPU suite run the connection path's FEC end to end
+LIB_CPU = os.path.join(HERE, "_build", "libquic_fec_patched_cpustub.so")
 
 
 class Params(C.Structure):
@@ -43,24 +46,26 @@ class Result(C.Structure):
                                            "slabs_allocated").split()])
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
-            raise RuntimeError(f"{LIB} missing: build it with python integration/build.py")
-        _lib = C.CDLL(LIB)
-        _lib.fec_conn_run.restype = C.c_int
-        _lib.fec_conn_run.argtypes = [C.POINTER(Params), C.POINTER(Result)]
-    return _lib
+def lib(cpu_stub=False):
+    path = LIB_CPU if cpu_stub else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: build it with python integration/build.py")
+        h = C.CDLL(path)
+        h.fec_conn_run.restype = C.c_int
+        h.fec_conn_run.argtypes = [C.POINTER(Params), C.POINTER(Result)]
+        _libs[path] = h
+    return _libs[path]
 
 
 def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True,
         max_turns=20_000, fail_encode=False, require_gpu=False, version=31,
-        end_flush=True, reorder=0, inject_unencrypted_fec=False, close_mid_batch=0) -> dict:
-    """One simulated run; returns the result fields as a dict."""
+        end_flush=True, reorder=0, inject_unencrypted_fec=False, close_mid_batch=0, cpu_stub=False) -> dict:
+    """One simulated run; returns the result fields as a dict.  cpu_stub: the
+    build whose qfec entry points are the CPU test stub (no GPU needed)."""
     p = Params(version=version, n_pairs=n_pairs, group_size=group_size, drop_every=drop_every,
                stream_len=stream_len, batched=int(batched), max_turns=max_turns,
                fail_encode=int(fail_encode), require_gpu=int(require_gpu),
@@ -68,7 +73,7 @@ def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True
                inject_unencrypted_fec=int(inject_unencrypted_fec),
                close_mid_batch=close_mid_batch)
     r = Result()
-    lib().fec_conn_run(C.byref(p), C.byref(r))
+    lib(cpu_stub).fec_conn_run(C.byref(p), C.byref(r))
     out = {n: getattr(r, n) for n, _ in Result._fields_}
     out["detail"] = r.detail.decode(errors="replace")
     return out

@@ -46,6 +46,10 @@ def _run(cmd, cwd=None):
 # of groups of 8 with lgkmcnt(0) — measured +8% AES-GCM, +5-14% NULL,
 # +3% ChaCha20-Poly1305 (profiles/round1/tune_gcm_g4.txt, tune_protect_g4.txt).
 FILE_FLAGS = {"qpp_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# the host C++: a local that shadows a parameter is an error (round 4: the
+# group offset shadowed the buffer offset in QuicFecSender::OnData)
+for _h in ("qfec_capi.cpp", "quic_fec_group.cc", "quic_fec_wire.cc", "quic_fec_connection.cc"):
+    FILE_FLAGS[_h] = ["-Wshadow", "-Werror=shadow"]
 
 
 def build_lib(force: bool = False, extra_flags=()) -> str:

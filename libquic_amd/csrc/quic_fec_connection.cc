@@ -50,11 +50,11 @@ bool QuicFecSender::OnData(QuicPacketNumber packet_number, StringPiece payload,
   f.entropy_flag = entropy_flag;
   if (fec_protect_) {
     if (!group_) group_.reset(new QuicFecGroup(packet_number));
-    const QuicPacketNumber offset = packet_number - group_->FecGroupNumber();
+    const QuicPacketNumber group_offset = packet_number - group_->FecGroupNumber();
     // uint8 first_fec_protected_packet_offset: the FEC packet needs an offset
     // above every data packet's, so data packets stop at offset 254.
-    if (offset >= 0xFF) {
-      detailed_error_ = "data packet at FEC group offset " + std::to_string(offset) +
+    if (group_offset >= 0xFF) {
+      detailed_error_ = "data packet at FEC group offset " + std::to_string(group_offset) +
                         ": no room left for the FEC packet (close the group first)";
       return false;
     }
@@ -71,7 +71,7 @@ bool QuicFecSender::OnData(QuicPacketNumber packet_number, StringPiece payload,
       return false;
     }
     f.in_fec_group = true;
-    f.fec_group_offset = static_cast<uint8_t>(offset);
+    f.fec_group_offset = static_cast<uint8_t>(group_offset);
   }
   last_packet_number_ = packet_number;
   if (fields) *fields = f;

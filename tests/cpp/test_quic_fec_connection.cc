@@ -172,6 +172,39 @@ static void ReceiverInPlace() {
   EXPECT(r.GetGroup(50) != nullptr && r.NumGroups() == 1);
 }
 
+// Zero-copy send (OnDataPacketInPlace): each packet serialized into an arena
+// buffer after a header of its own length; the group adopts the buffers and
+// its parity is the XOR of the payloads at their BUFFER offsets -- not at the
+// packets' FEC-group offsets (round 4: a local group offset shadowed the
+// buffer offset, and only the first packet of a group, at offset 0 both ways
+// when its header was empty, came out right).  The parity is compared where
+// the group can compute it (the CPU stub build, or a device).
+static void SenderInPlace() {
+  QuicFecSender s(4);
+  const size_t hdr[3] = {11, 9, 14};
+  std::string want(1200, '\0');
+  FecHeaderFields f;
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = Payload(5, 70 + i, 1000 + 100 * i);
+    QuicFecGroup::PacketBuffer b = QuicFecGroup::AllocPacketBuffer(kMaxPacketSize);
+    std::memset(b.data(), 0x5A, hdr[i]);  // the packet header: not protected
+    std::memcpy(b.data() + hdr[i], p.data(), p.size());
+    std::memset(b.data() + hdr[i] + p.size(), 0x77, 16);  // beyond the payload
+    EXPECT(s.OnDataPacketInPlace(70 + i, &b, hdr[i], p.size(), false, &f));
+    EXPECT(b.empty() && f.fec_group_offset == i);
+    for (size_t j = 0; j < p.size(); ++j) want[j] ^= p[j];
+  }
+  QuicFecGroup::PacketBuffer bad = QuicFecGroup::AllocPacketBuffer(100);
+  EXPECT(!s.OnDataPacketInPlace(80, &bad, 50, 60, false, &f));  // outside its buffer
+  QuicFecEncodeBatch batch;
+  EXPECT(s.CloseFecGroup(73, &batch, &s) && batch.size() == 1);
+  StringPiece par = batch.entries()[0].group->PayloadParity();
+  if (!par.empty()) {
+    EXPECT(par.size() == want.size());
+    EXPECT(par.size() == want.size() && std::memcmp(par.data(), want.data(), want.size()) == 0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // GPU: lossy multi-connection simulation
 // ---------------------------------------------------------------------------
@@ -400,6 +433,7 @@ int main(int argc, char** argv) {
   SenderBookkeeping();
   ReceiverBookkeeping();
   ReceiverInPlace();
+  SenderInPlace();
   FullWidthGroup();
   if (!cpu_only) {
     qfec_ctx* ctx = qfec_create(0);

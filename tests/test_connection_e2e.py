@@ -13,6 +13,14 @@ revived on the GPU.
 CPU (no device): the reference's own loss recovery alone (FEC off), and the
 FEC path when no GPU work can run — every group goes without FEC
 (fec_groups_skipped) and retransmission still delivers the stream.
+
+The FEC cases run twice: on the GPU (`gpu`, libqfec.so) and in the CPU suite
+(`cpustub`) over the same patched build linked against
+tests/cpp/cpu_qfec_stub.c, a CPU restatement of the qfec entry points the host
+code calls (test infrastructure) -- so the connection path's groups, payload
+arena, zero-copy capture, revival and ack channel are checked on every CPU run
+too (round 4: a send-side zero-copy bug reached the GPU box before any CPU
+test could see it).
 """
 import ctypes as C
 import os
@@ -22,10 +30,15 @@ import pytest
 from conftest import ROOT
 
 LIB = os.path.join(ROOT, "integration", "_build", "libquic_fec_patched.so")
+LIB_CPU = os.path.join(ROOT, "integration", "_build", "libquic_fec_patched_cpustub.so")
+
+# backend of the FEC cases: the GPU, or the CPU stub build
+BACKENDS = [pytest.param(False, marks=pytest.mark.gpu, id="gpu"),
+            pytest.param(True, id="cpustub")]
 
 
-def _harness():
-    if not os.path.exists(LIB):
+def _harness(cpu_stub=False):
+    if not os.path.exists(LIB_CPU if cpu_stub else LIB):
         if os.path.isdir("/root/reference/src/net/quic/core"):
             pytest.fail(f"{LIB} missing: python integration/build.py")
         pytest.skip("the patched reference library is built where /root/reference is")
@@ -122,21 +135,21 @@ def test_unencrypted_fec_data_closes_the_connection():
     assert r["revived"] == 0, r
 
 
-# ---- GPU ---------------------------------------------------------------------
+# ---- FEC on the GPU (gpu) and over the CPU stub (cpustub) --------------------
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("stub", BACKENDS)
 @pytest.mark.parametrize("batched", [False, True])
 @pytest.mark.parametrize("group_size,drop_every,n", [(10, 2, 4), (2, 3, 2), (255, 1, 2),
                                                      (10, 0, 2)])
-def test_connection_fec_revives_every_single_loss(batched, group_size, drop_every, n):
+def test_connection_fec_revives_every_single_loss(batched, group_size, drop_every, n, stub):
     """Every group that lost one packet is revived unless the sender's own
     loss recovery got there first (the peer's STOP_WAITING then closes the
     group: CloseFecGroupsBefore); with 10-packet groups the FEC packet always
     wins in this simulation (deterministic: simulated clock, one turn per
     millisecond), with 255-packet groups the retransmission may."""
-    h = _harness()
+    h = _harness(stub)
     r = h.run(n_pairs=n, group_size=group_size, drop_every=drop_every, stream_len=300_000,
-              batched=batched, require_gpu=True)
+              batched=batched, require_gpu=True, cpu_stub=stub)
     _check_common(r, n)
     assert r["fec_groups_skipped"] == 0, r
     assert r["fec_packets_sent"] > 0
@@ -162,9 +175,9 @@ def test_connection_fec_revives_every_single_loss(batched, group_size, drop_ever
                              "protected_entropy_set", "payloads_adopted", "payloads_copied")})
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("stub", BACKENDS)
 @pytest.mark.parametrize("reorder", [3, 7])
-def test_connection_fec_over_a_reordering_link(reorder):
+def test_connection_fec_over_a_reordering_link(reorder, stub):
     """Client->server packets reordered (adjacent pairs swapped, about one in
     `reorder` held back a turn, so FEC packets also arrive before the data
     they protect): streams still byte-identical, every drop repaired by a
@@ -172,9 +185,9 @@ def test_connection_fec_over_a_reordering_link(reorder):
     visitor.  A packet that is only LATE can be revived too — its group's FEC
     packet overtook it, as the historical receiver did — so revivals may
     exceed the drops here; the late original is then a duplicate."""
-    h = _harness()
+    h = _harness(stub)
     r = h.run(n_pairs=4, group_size=10, drop_every=2, stream_len=300_000, batched=True,
-              require_gpu=True, reorder=reorder)
+              require_gpu=True, reorder=reorder, cpu_stub=stub)
     _check_common(r, 4)
     assert r["fec_groups_skipped"] == 0 and r["fec_packets_sent"] > 0, r
     assert r["dropped"] > 0 and r["revived"] > 0, r
@@ -186,43 +199,43 @@ def test_connection_fec_over_a_reordering_link(reorder):
                              "retransmitted_of_revived")})
 
 
-@pytest.mark.gpu
-def test_fec_alarm_closes_a_partial_group():
+@pytest.mark.parametrize("stub", BACKENDS)
+def test_fec_alarm_closes_a_partial_group(stub):
     """A stream shorter than one group and no end-of-data close: only the FEC
     alarm (the group took no packet for max(1 ms, srtt/2)) can close the
     group and send its FEC packet.  The loss itself is repaired by whichever
     comes first, the revival or the sender's fast retransmit."""
-    h = _harness()
+    h = _harness(stub)
     r = h.run(n_pairs=1, group_size=200, drop_every=1, stream_len=20_000, batched=True,
-              require_gpu=True, end_flush=False)
+              require_gpu=True, end_flush=False, cpu_stub=stub)
     _check_common(r, 1)
     assert r["fec_packets_sent"] == 1 and r["fec_groups_skipped"] == 0, r
     assert r["dropped"] == 1 and r["revived"] + r["retransmitted"] >= 1, r
 
 
-@pytest.mark.gpu
-def test_gpu_failure_goes_without_fec():
+@pytest.mark.parametrize("stub", BACKENDS)
+def test_gpu_failure_goes_without_fec(stub):
     """Every FEC launch fails (qfec_debug_fail_launches): the groups go out
     without FEC packets (fec_groups_skipped), nothing is revived, and the
     reference's retransmission still delivers every stream — no connection
     is closed (it was OnUnrecoverableError in round 2)."""
-    h = _harness()
+    h = _harness(stub)
     r = h.run(n_pairs=3, group_size=10, drop_every=2, stream_len=150_000, batched=True,
-              fail_encode=True, require_gpu=True)
+              fail_encode=True, require_gpu=True, cpu_stub=stub)
     _check_common(r, 3)
     assert r["fec_packets_sent"] == 0 and r["revived"] == 0
     assert r["fec_groups_skipped"] > 0
     assert r["retransmitted"] >= r["dropped"] > 0
 
 
-@pytest.mark.gpu
-def test_batcher_batches_across_connections():
+@pytest.mark.parametrize("stub", BACKENDS)
+def test_batcher_batches_across_connections(stub):
     """64 connections on one batcher: each launch carries many connections'
     groups (one encode + one revive launch per loop turn)."""
-    h = _harness()
+    h = _harness(stub)
     n = 64
     r = h.run(n_pairs=n, group_size=10, drop_every=2, stream_len=60_000, batched=True,
-              require_gpu=True)
+              require_gpu=True, cpu_stub=stub)
     _check_common(r, n)
     assert r["dropped"] == r["revived"] > 0
     assert r["groups_encoded"] >= 4 * r["launches"], r
@@ -234,7 +247,8 @@ def test_close_while_fec_packet_pending():
     """A batched connection closes while its group's FEC packet is still being
     computed: packets numbered after a pending FEC packet are held back, but
     the CONNECTION_CLOSE must leave at once (IsTerminationPacket) -- the peer
-    learns of the close, and the pending group goes without FEC."""
+    learns of the close, and the pending group goes without FEC.  GPU only:
+    the CPU stub completes every launch inside the call (nothing pends)."""
     h = _harness()
     r = h.run(n_pairs=2, group_size=10, drop_every=2, stream_len=150_000, batched=True,
               require_gpu=True, close_mid_batch=3)
