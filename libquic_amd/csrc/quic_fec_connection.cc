@@ -335,8 +335,8 @@ int QuicFecBatcher::Launch() {
   const QuicFecGroup::LaunchProfile before = QuicFecGroup::launch_profile();
   enc_live_.swap(enc_);
   rev_live_.swap(rev_);
-  std::vector<QuicFecGroup*> gs;
-  gs.reserve(std::max(enc_live_.size(), rev_live_.size()));
+  std::vector<QuicFecGroup*>& gs = launch_groups_;  // keeps its capacity
+  gs.clear();
   for (EncodeItem& e : enc_live_) gs.push_back(e.group.get());
   const int erc = QuicFecGroup::Launch(ctx_, gs, &enc_pending_, /*async=*/true);
   gs.clear();

@@ -320,6 +320,7 @@ class QuicFecBatcher {
   std::vector<EncodeItem> enc_, enc_live_;
   std::vector<ReviveItem> rev_, rev_live_;
   QuicFecGroup::Pending enc_pending_, rev_pending_;
+  std::vector<QuicFecGroup*> launch_groups_;  // Launch's group list
   Stats stats_;
 };
 

@@ -250,6 +250,9 @@ bool QuicFecGroup::Fold(StringPiece payload, bool completes_group, PacketBuffer*
   }
   payloads_.push_back(sp);
   lens_.push_back(static_cast<uint16_t>(payload.size()));
+  addrs_.push_back(reinterpret_cast<uintptr_t>(sp.data));
+  min_data_ = std::min(min_data_, reinterpret_cast<uintptr_t>(sp.data));
+  payloads_mapped_ = payloads_mapped_ && static_cast<ArenaSlab*>(sp.slab)->mapped;
   dirty_ = true;
   return true;
 }
@@ -432,18 +435,95 @@ QuicFecGroup::LaunchProfile& QuicFecGroup::launch_profile() {
   return p;
 }
 
+void QuicFecGroup::LaunchTables::Clear() {
+  groups.clear();
+  pkt_off.clear();
+  pkt_len.clear();
+  grp_ptr.assign(1, 0);
+  parity_off.clear();
+  in_base = out_base = UINTPTR_MAX;
+  mapped = true;
+  rc = QFEC_OK;
+}
+
+bool QuicFecGroup::LaunchTables::Append(QuicFecGroup* g) {
+  if (!g || !g->dirty_) return true;
+  if (g->lens_.empty()) {  // only empty payloads folded: parity is empty
+    g->payload_parity_len_ = 0;
+    g->dirty_ = false;
+    return true;
+  }
+  if (!g->parity_.p) {
+    g->parity_ = ArenaAlloc(kMaxPacketSize);
+    if (!g->parity_.p) {
+      g->detailed_error_ = "out of payload memory";
+      rc = QFEC_ERR_INTERNAL;
+      return false;
+    }
+  }
+  mapped = mapped && g->payloads_mapped_ && static_cast<ArenaSlab*>(g->parity_.slab)->mapped;
+  in_base = std::min(in_base, g->min_data_);
+  const uintptr_t par = reinterpret_cast<uintptr_t>(g->parity_.p);
+  out_base = std::min(out_base, par);
+  pkt_off.insert(pkt_off.end(), g->addrs_.begin(), g->addrs_.end());
+  pkt_len.insert(pkt_len.end(), g->lens_.begin(), g->lens_.end());
+  grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));
+  parity_off.push_back(par);
+  groups.push_back(g);
+  return true;
+}
+
 int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* pend,
                          bool async) {
+  // the tables built here, in one pass over the groups (the batcher builds
+  // them as groups are queued instead)
+  static thread_local LaunchTables t;
+  t.Clear();
   const auto t0 = std::chrono::steady_clock::now();
-  *pend = Pending();
-  std::vector<QuicFecGroup*> work;
-  for (QuicFecGroup* g : groups)
-    if (g && g->dirty_) work.push_back(g);
-  if (work.empty()) return QFEC_OK;
+  for (size_t i = 0; i < groups.size(); ++i) {
+    // prefetch: the group object 8 ahead, its address / length arrays 4 ahead
+    if (i + 8 < groups.size() && groups[i + 8]) __builtin_prefetch(groups[i + 8]);
+    if (i + 4 < groups.size() && groups[i + 4]) {
+      const QuicFecGroup* nx = groups[i + 4];
+      const char* a4 = reinterpret_cast<const char*>(nx->addrs_.data());
+      for (size_t b = 0; b < nx->addrs_.size() * sizeof(uint64_t); b += 64)
+        __builtin_prefetch(a4 + b);
+      __builtin_prefetch(nx->lens_.data());
+    }
+    if (!t.Append(groups[i])) break;
+  }
+  launch_profile().tables_us +=
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  return Launch(ctx, &t, pend, async);
+}
+
+int QuicFecGroup::Launch(qfec_ctx* ctx, LaunchTables* t, Pending* pend, bool async) {
+  const auto t0 = std::chrono::steady_clock::now();
+  // reset, keeping the vectors' capacity (a batcher's Pending is reused every
+  // loop turn: no large block freed and reallocated per launch)
+  pend->ctx = nullptr;
+  pend->launched.clear();
+  pend->plen.clear();
+  pend->rc = QFEC_OK;
+  pend->live = false;
+  pend->ticket = 0;
   if (!ctx) ctx = thread_default_ctx();
   pend->ctx = ctx;
+  if (t->rc != QFEC_OK) {  // an accumulator could not be allocated
+    pend->rc = t->rc;
+    for (QuicFecGroup* g : t->groups) g->detailed_error_ = "out of payload memory";
+    pend->launched.assign(t->groups.begin(), t->groups.end());
+    t->Clear();
+    return pend->rc;
+  }
+  if (t->groups.empty()) {
+    t->Clear();
+    return QFEC_OK;
+  }
+  pend->launched.assign(t->groups.begin(), t->groups.end());
   if (!ctx) {
-    for (QuicFecGroup* g : work) g->detailed_error_ = qfec_last_error(nullptr);
+    for (QuicFecGroup* g : pend->launched) g->detailed_error_ = qfec_last_error(nullptr);
+    t->Clear();
     return pend->rc = QFEC_ERR_INTERNAL;
   }
   // Ragged CSR over every folded payload of every group, addressed IN PLACE:
@@ -453,72 +533,27 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
   // in a mapped arena slab the kernel reads and writes them where they are
   // (QFEC_PTR_MAPPED); otherwise the host path gathers them into the
   // context's pinned staging (QFEC_PTR_HOST).
-  size_t npk = 0;
-  std::vector<QuicFecGroup*>& launched = pend->launched;
-  launched.reserve(work.size());
-  uintptr_t in_base = UINTPTR_MAX, out_base = UINTPTR_MAX;
-  bool mapped = true;
-  for (QuicFecGroup* g : work) {
-    if (g->lens_.empty()) {  // only empty payloads folded: parity is empty
-      g->payload_parity_len_ = 0;
-      g->dirty_ = false;
-      continue;
-    }
-    if (!g->parity_.p) {
-      g->parity_ = ArenaAlloc(kMaxPacketSize);
-      if (!g->parity_.p) {
-        g->detailed_error_ = "out of payload memory";
-        launched.clear();
-        return pend->rc = QFEC_ERR_INTERNAL;
-      }
-    }
-    mapped = mapped && static_cast<ArenaSlab*>(g->parity_.slab)->mapped;
-    out_base = std::min(out_base, reinterpret_cast<uintptr_t>(g->parity_.p));
-    for (const Span& sp : g->payloads_) {
-      in_base = std::min(in_base, reinterpret_cast<uintptr_t>(sp.data));
-      mapped = mapped && static_cast<ArenaSlab*>(sp.slab)->mapped;
-    }
-    npk += g->lens_.size();
-    launched.push_back(g);
-  }
-  if (launched.empty()) return QFEC_OK;
-  // index tables: per-thread buffers that keep their capacity between flushes
-  // (the call stages them, so they are free again when it returns)
-  static thread_local std::vector<uint64_t> pkt_off, parity_off;
-  static thread_local std::vector<uint16_t> pkt_len;
-  static thread_local std::vector<uint32_t> grp_ptr;
-  pkt_off.clear();
-  pkt_off.reserve(npk);
-  pkt_len.clear();
-  pkt_len.reserve(npk);
-  grp_ptr.assign(1, 0);
-  grp_ptr.reserve(launched.size() + 1);
-  parity_off.clear();
-  parity_off.reserve(launched.size());
-  for (QuicFecGroup* g : launched) {
-    for (size_t i = 0; i < g->payloads_.size(); ++i) {
-      pkt_off.push_back(reinterpret_cast<uintptr_t>(g->payloads_[i].data) - in_base);
-      pkt_len.push_back(g->lens_[i]);
-    }
-    grp_ptr.push_back(static_cast<uint32_t>(pkt_len.size()));
-    parity_off.push_back(reinterpret_cast<uintptr_t>(g->parity_.p) - out_base);
-  }
-  pend->plen.assign(launched.size(), 0);
-  const uint32_t flags = mapped ? (QFEC_PTR_MAPPED | (async ? QFEC_ASYNC : 0u)) : QFEC_PTR_HOST;
+  for (uint64_t& o : t->pkt_off) o -= t->in_base;
+  for (uint64_t& o : t->parity_off) o -= t->out_base;
+  const size_t ng = pend->launched.size(), npk = t->pkt_len.size();
+  pend->plen.assign(ng, 0);
+  const uint32_t flags =
+      t->mapped ? (QFEC_PTR_MAPPED | (async ? QFEC_ASYNC : 0u)) : QFEC_PTR_HOST;
   const auto t1 = std::chrono::steady_clock::now();
-  pend->rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(in_base), pkt_off.data(),
-                                pkt_len.data(), grp_ptr.data(), launched.size(),
-                                reinterpret_cast<uint8_t*>(out_base), parity_off.data(),
+  pend->rc = qfec_encode_ragged(ctx, reinterpret_cast<const uint8_t*>(t->in_base),
+                                t->pkt_off.data(), t->pkt_len.data(), t->grp_ptr.data(), ng,
+                                reinterpret_cast<uint8_t*>(t->out_base), t->parity_off.data(),
                                 pend->plen.data(), flags);
   LaunchProfile& prof = launch_profile();
   const auto t2 = std::chrono::steady_clock::now();
   prof.tables_us += std::chrono::duration<double, std::micro>(t1 - t0).count();
   prof.call_us += std::chrono::duration<double, std::micro>(t2 - t1).count();
   ++prof.launches;
-  prof.groups += launched.size();
+  prof.groups += ng;
   prof.packets += npk;
   pend->ticket = pend->rc == QFEC_OK ? qfec_async_ticket(ctx) : 0;
   pend->live = pend->ticket != 0;  // else it completed synchronously
+  t->Clear();
   return pend->rc;
 }
 

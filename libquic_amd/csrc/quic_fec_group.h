@@ -97,6 +97,49 @@ struct StringPiece {
 };
 #endif  // QFEC_WITH_LIBQUIC
 
+// A vector whose first N elements live inside the object (trivially
+// copyable T): a group's payload tables take no heap allocation up to N
+// packets.  Thousands of groups are created and destroyed per event-loop turn
+// at thousands of connections, and their small vector blocks, once freed,
+// made the allocator consolidate for milliseconds at an unrelated later free
+// (measured inside QuicFecBatcher::Launch, round 4).
+template <typename T, size_t N>
+class QfecSmallVec {
+ public:
+  QfecSmallVec() = default;
+  QfecSmallVec(const QfecSmallVec&) = delete;
+  QfecSmallVec& operator=(const QfecSmallVec&) = delete;
+  ~QfecSmallVec() {
+    if (p_ != in_) delete[] p_;
+  }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T* begin() { return p_; }
+  T* end() { return p_ + n_; }
+  const T* begin() const { return p_; }
+  const T* end() const { return p_ + n_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  void push_back(const T& v) {
+    if (n_ == cap_) {
+      const size_t c = cap_ * 2;
+      T* q = new T[c];
+      for (size_t i = 0; i < n_; ++i) q[i] = p_[i];
+      if (p_ != in_) delete[] p_;
+      p_ = q;
+      cap_ = c;
+    }
+    p_[n_++] = v;
+  }
+
+ private:
+  T in_[N];
+  T* p_ = in_;
+  size_t n_ = 0, cap_ = N;
+};
+
 class QuicFecGroup {
  public:
   // `ctx` may be null: a per-thread context on device 0 is created on first use.
@@ -192,6 +235,28 @@ class QuicFecGroup {
   };
   static int Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* p,
                     bool async);
+
+  // The launch's index tables, built one group at a time as groups are queued
+  // (QuicFecBatcher appends a group when the connection hands it over, while
+  // its payload addresses are still in the connection thread's caches): the
+  // launch itself then only rebases the addresses and makes the call.  A
+  // group must take no packets once appended (closed / collected groups).
+  struct LaunchTables {
+    std::vector<QuicFecGroup*> groups;
+    std::vector<uint64_t> pkt_off;     // absolute payload addresses until the launch
+    std::vector<uint16_t> pkt_len;
+    std::vector<uint32_t> grp_ptr{0};
+    std::vector<uint64_t> parity_off;  // absolute accumulator addresses until the launch
+    uintptr_t in_base = UINTPTR_MAX, out_base = UINTPTR_MAX;
+    bool mapped = true;
+    int rc = QFEC_OK;  // an append failed (out of payload memory)
+    void Clear();
+    // false (and rc set) when the group's accumulator cannot be allocated;
+    // a group with nothing to compute is finished here and not added
+    bool Append(QuicFecGroup* g);
+  };
+  // Launch over prebuilt tables (cleared on return: the call stages them).
+  static int Launch(qfec_ctx* ctx, LaunchTables* t, Pending* p, bool async);
   // wait: block; otherwise QFEC_PENDING while the work runs.  Returns the
   // launch's qfec_* code (also in every launched group's detailed_error).
   static int Finish(Pending* p, bool wait);
@@ -255,8 +320,14 @@ class QuicFecGroup {
   };
   static Span ArenaAlloc(size_t n);
   static void ArenaFree(Span* s);
-  std::vector<Span> payloads_;
-  std::vector<uint16_t> lens_;
+  // up to kInlinePayloads payloads without a heap allocation (QfecSmallVec)
+  static constexpr size_t kInlinePayloads = 16;
+  QfecSmallVec<Span, kInlinePayloads> payloads_;
+  QfecSmallVec<uint16_t, kInlinePayloads> lens_;
+  // kept as payloads are folded, for Launch's table build
+  QfecSmallVec<uint64_t, kInlinePayloads> addrs_;  // payload addresses (payloads_[i].data)
+  uintptr_t min_data_ = UINTPTR_MAX;  // lowest payload address
+  bool payloads_mapped_ = true;       // every payload in a device-mapped slab
   mutable Span parity_;
   mutable size_t payload_parity_len_ = 0;
   mutable bool dirty_ = false;
