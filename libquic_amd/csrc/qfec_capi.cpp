@@ -9,7 +9,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -143,7 +145,56 @@ int bind(qfec_ctx* ctx) {
   return QFEC_OK;
 }
 
+// Ranges this library mapped itself (qfec_host_alloc, qfec_host_register):
+// QFEC_PTR_MAPPED's pointer check answers from them without
+// hipPointerGetAttributes (a runtime lookup under its lock) -- the connection
+// batcher's launches hand over payload-arena slabs, every one of them from
+// qfec_host_alloc.  A thread keeps the last range it matched; any free /
+// unregister bumps the generation, which drops every thread's copy.
+struct MappedRanges {
+  std::mutex mu;
+  std::vector<std::pair<uintptr_t, size_t>> r;  // [base, base + size)
+  std::atomic<uint64_t> gen{1};
+};
+MappedRanges& mapped_ranges() {
+  static MappedRanges* m = new MappedRanges();  // never destroyed (frees at exit)
+  return *m;
+}
+void note_mapped(const void* p, size_t n) {
+  MappedRanges& m = mapped_ranges();
+  std::lock_guard<std::mutex> g(m.mu);
+  m.r.emplace_back(reinterpret_cast<uintptr_t>(p), n);
+}
+void forget_mapped(const void* p) {
+  MappedRanges& m = mapped_ranges();
+  std::lock_guard<std::mutex> g(m.mu);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+  m.r.erase(std::remove_if(m.r.begin(), m.r.end(),
+                           [b](const std::pair<uintptr_t, size_t>& e) { return e.first == b; }),
+            m.r.end());
+  m.gen.fetch_add(1, std::memory_order_acq_rel);
+}
+bool known_mapped(const void* p) {
+  struct Hit {
+    uint64_t gen = 0;
+    uintptr_t base = 0;
+    size_t n = 0;
+  };
+  static thread_local Hit hit;
+  MappedRanges& m = mapped_ranges();
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (hit.gen == m.gen.load(std::memory_order_acquire) && a - hit.base < hit.n) return true;
+  std::lock_guard<std::mutex> g(m.mu);
+  for (const auto& e : m.r)
+    if (a - e.first < e.second) {
+      hit = Hit{m.gen.load(std::memory_order_relaxed), e.first, e.second};
+      return true;
+    }
+  return false;
+}
+
 bool is_pinned_or_device(const void* p) {
+  if (known_mapped(p)) return true;
   hipPointerAttribute_t attr;
   if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();
@@ -586,11 +637,14 @@ void* qfec_host_alloc(size_t bytes) {
          "QFEC_PTR_MAPPED needs them equal", bytes, dev, p, hipGetErrorString(d));
     return nullptr;
   }
+  note_mapped(p, bytes ? bytes : 1);
   return p;
 }
 
 void qfec_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  forget_mapped(p);
+  (void)hipHostFree(p);
 }
 
 int qfec_host_register(void* p, size_t bytes) {
@@ -607,10 +661,12 @@ int qfec_host_register(void* p, size_t bytes) {
                 "qfec_host_register(%p): device address %p differs from the host address (%s); "
                 "QFEC_PTR_MAPPED needs them equal", p, dev, hipGetErrorString(e));
   }
+  note_mapped(p, bytes);
   return QFEC_OK;
 }
 
 int qfec_host_unregister(void* p) {
+  forget_mapped(p);
   const hipError_t e = hipHostUnregister(p);
   if (e != hipSuccess)
     return fail(nullptr, QFEC_ERR_INTERNAL, "qfec_host_unregister(%p): %s", p,
