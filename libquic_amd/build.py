@@ -114,6 +114,37 @@ def build_cpp_tests(force: bool = False) -> list:
     return outs
 
 
+# Measurement tools that compile against the library's headers or kernels
+# (tools/tune): rebuilt whenever those change, so a tool never runs with a
+# stale view of a class layout (round 4: host_cost built before a
+# QuicFecGroup layout change corrupted its heap on the GPU box).
+TOOLS = [("host_cost.cc", False), ("pcie_duplex.hip", True), ("phased_copy.hip", True)]
+
+
+def build_tools(force: bool = False) -> list:
+    outs = []
+    tdir = os.path.join(ROOT, "tools", "tune")
+    bdir = os.path.join(tdir, "build")
+    for src_name, hip in TOOLS:
+        src = os.path.join(tdir, src_name)
+        out = os.path.join(bdir, os.path.splitext(src_name)[0])
+        if not os.path.exists(src):
+            continue
+        deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + \
+            [os.path.join(ROOT, "include", "qfec.h")]
+        deps += [os.path.join(CSRC, "qfec_kernels.hip")] if hip else [LIB]
+        if force or _stale(out, deps):
+            os.makedirs(bdir, exist_ok=True)
+            if hip:
+                _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", src, "-o", out])
+            else:
+                _run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+                      src, "-L", HERE, "-lqfec", "-Wl,-rpath,$ORIGIN/../../../libquic_amd",
+                      "-Wl,-rpath-link,/opt/rocm/lib", "-o", out])
+        outs.append(out)
+    return outs
+
+
 # the host C++ (payload arena, group bookkeeping, receive
 # map, CSR builders, batcher) under AddressSanitizer + UBSan on the CPU,
 # against tests/cpp/cpu_qfec_stub.c (test infrastructure: a CPU restatement of
@@ -160,3 +191,4 @@ if __name__ == "__main__":
     build_lib(force="--force" in sys.argv)
     build_cpp_tests(force="--force" in sys.argv)
     build_cpp_sanitized(force="--force" in sys.argv)
+    build_tools(force="--force" in sys.argv)

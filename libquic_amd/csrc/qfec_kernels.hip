@@ -1565,8 +1565,20 @@ constexpr uint32_t kPhMinPhases = 6;
 // phase_extra (tests/test_hip_phase.py) adds workgroups beyond one per CU,
 // which cannot all be resident, so the first meeting times out — the abandon
 // path.
+// Group sizes the phased kernel loses at (round 4, tools/phase_k_table.py,
+// profiles/round4/phase_k_table_r4a.txt, 2^20 groups of 1350 B, fraction of
+// 8 TB/s phased / one-pass): encode k = 2 0.47 / 0.77, k = 4 0.64 / 0.74,
+// k = 5 0.73 / 0.71, k = 8 0.79 / 0.72; recover k = 4 0.54 / 0.72, k = 5
+// 0.62 / 0.67, k = 8 0.745 / 0.740, k = 10 0.76 / 0.72 -- a phase of few
+// rows per group reads too little between its meetings.  So encode phases
+// from k = 5, recover from k = 8.  An explicit phase_min (test hook) keeps
+// the phase-count rule alone.
+constexpr uint32_t kPhMinKEncode = 5, kPhMinKRecover = 8;
+
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
   if (a.ncu == 0) return false;
+  if (a.phase_min == 0 && a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode))
+    return false;
   const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
   // the threshold counts phases of the LDS steps alone (the measured band);
   // the launch's phases hold the register steps too (k = 10)

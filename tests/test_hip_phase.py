@@ -2,10 +2,13 @@
 libquic_amd/csrc/qfec_kernels.hip), through the C-ABI.
 
 Large nt batches (>= kPhMinPhases = 6 phases of CUs x 40 steps x
-floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) run the phased
-kernel by default; QFEC_ONE_PASS forces the one-pass fixed kernel, and
-qfec_last_fixed_phased reports which one a call ran (every case here asserts
-it).  Every case is sized past that threshold (8 phases of 40 LDS steps) with
+floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) of k >= 5
+(encode) / k >= 8 (recover) run the phased kernel by default (round 4: below
+those group sizes the one-pass kernel is faster, tools/phase_k_table.py);
+QFEC_ONE_PASS forces the one-pass fixed kernel, qfec_debug_phase_min (here 6,
+the default count) keeps the phase-count rule alone so every k reaches the
+phased kernel, and qfec_last_fixed_phased reports which one a call ran (every
+case here asserts it).  Every case is sized past that threshold (8 phases of 40 LDS steps) with
 a ragged last phase, and checks the phased outputs byte-exact against the
 one-pass kernel's on the same buffers, against the oracle on sampled groups,
 and through the round-trip properties (revived row == erased row, parity XOR
@@ -49,6 +52,14 @@ def run_both(ctx, rows, miss, k, L, n, ps=None, os_=None, **strides):
     ps = ps or L
     os_ = os_ or L
     res = {}
+    ctx.debug_phase_min(6)  # the phase-count rule alone: phased for every k
+    try:
+        return _run_both(ctx, rows, miss, k, L, n, ps, os_, res, strides)
+    finally:
+        ctx.debug_phase_min(0)
+
+
+def _run_both(ctx, rows, miss, k, L, n, ps, os_, res, strides):
     for one_pass in (False, True):
         par = torch.full((n * ps,), 0xA5, dtype=torch.uint8, device=DEV)
         out = torch.full((n * os_,), 0x5A, dtype=torch.uint8, device=DEV)
@@ -65,6 +76,24 @@ def run_both(ctx, rows, miss, k, L, n, ps=None, os_=None, **strides):
         torch.cuda.synchronize()
         res[one_pass] = (par, out)
     return res
+
+
+@pytest.mark.parametrize("k", [2, 4, 5, 7, 8, 10])
+def test_default_kernel_choice_by_group_size(ctx, k):
+    """The default rule (no test hook): a batch past the phase-count threshold
+    runs phased for encode from k = 5 and for recover from k = 8, one-pass
+    below (round 4's per-k table)."""
+    L = 1350
+    n = 8 * phase_groups(L) + 777
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    par = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    out = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    miss = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    ctx.encode(rows, k, L, n, par)
+    assert ctx.last_fixed_phased() == (1 if k >= 5 else 0)
+    ctx.recover(rows, par, miss, k, L, n, out)
+    assert ctx.last_fixed_phased() == (1 if k >= 8 else 0)
+    ctx.sync()
 
 
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),

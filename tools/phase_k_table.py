@@ -47,6 +47,9 @@ def main():
         for r in range(rounds):
             for m in (1, 0, 2):  # 1: register steps (product), 0: LDS steps only, 2: one-pass
                 ctx.debug_phase_regsteps(m == 1)
+                # phased forms at every k (the library's default picks one-pass
+                # below k = 5 / 8 since round 4, from this very table)
+                ctx.debug_phase_min(6 if m != 2 else 0)
                 for op in ("enc", "rec"):
                     def run():
                         if op == "enc":
@@ -64,6 +67,7 @@ def main():
                     t[(m, op)].append(e0.elapsed_time(e1) / reps / 1e3)
                     phased[(m, op)] = ctx.last_fixed_phased()
         ctx.debug_phase_regsteps(True)
+        ctx.debug_phase_min(0)
         ctx.sync()
         torch.cuda.synchronize()
         same = torch.equal(par[0], par[1]) and torch.equal(out[0], out[1])  # one-pass wrote 0 last
