@@ -341,6 +341,7 @@ def test_phased_register_steps_identical(ctx, k, L):
     ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
     miss = torch.from_numpy(Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)).to(DEV)
     res = {}
+    ctx.debug_phase_min(6)  # phased at k = 4 too (the default picks one-pass there)
     try:
         for on in (True, False):
             ctx.debug_phase_regsteps(on)
@@ -354,6 +355,7 @@ def test_phased_register_steps_identical(ctx, k, L):
             res[on] = (par, out)
     finally:
         ctx.debug_phase_regsteps(True)
+        ctx.debug_phase_min(0)
     assert torch.equal(res[True][0], res[False][0])
     assert torch.equal(res[True][1], res[False][1])
     r3 = rows.view(n, k, L)
