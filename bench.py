@@ -1358,6 +1358,59 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
                                         in_len, npk, out, out_off)
                 host_out[c * ob:(c + 1) * ob].copy_(out, non_blocking=True)
 
+    # Duplex form (round 4): ONE stream per copy
+    # direction and one compute stream, ordered by events.  The link carries
+    # H2D and D2H at once only when each direction's copies sit in a queue of
+    # their own (tools/tune/pcie_duplex.hip: one copy each way on two streams
+    # 97 GB/s combined; the same bytes as 64-MiB chunks over 8 streams 64 GB/s,
+    # as the slot form's 3 streams that each copy in, compute and copy out).
+    h2d_st, cmp_st, d2h_st = (torch.cuda.Stream(device=dev) for _ in range(3))
+    cctx = qfec.Context(dev.index)
+    cctx.set_stream(cmp_st)
+    ev = {n: [torch.cuda.Event() for _ in range(slots)]
+          for n in ("in", "done", "buf_free", "out_free")}
+
+    seq = [0]  # chunks issued so far (slot = seq % slots; the first `slots` wait for nothing)
+
+    def chunk_duplex(c):
+        i = seq[0] % slots
+        first = seq[0] < slots
+        seq[0] += 1
+        buf, out = S[i]["buf"], S[i]["out"]
+        ob = npk * (L + 12)
+        with torch.cuda.stream(h2d_st):
+            if not first:
+                h2d_st.wait_event(ev["buf_free"][i])  # compute of chunk c - slots read buf
+            buf[:rows_b].copy_(host_rows[c * rows_b:(c + 1) * rows_b], non_blocking=True)
+            buf[rows_b + par_b:].copy_(host_hdr[c * hdr_b:(c + 1) * hdr_b], non_blocking=True)
+            ev["in"][i].record(h2d_st)
+        with torch.cuda.stream(cmp_st):
+            cmp_st.wait_event(ev["in"][i])
+            if not first:
+                cmp_st.wait_event(ev["out_free"][i])  # D2H of chunk c - slots read out
+            cctx.encode(buf[:rows_b], k, L, cg, buf[rows_b:rows_b + par_b])
+            cctx.aes128gcm_seal(key, pre, kidx, pn[c], None, buf, ad_off, ad_len, in_off, in_len,
+                                npk, out, out_off)
+            ev["buf_free"][i].record(cmp_st)
+            ev["done"][i].record(cmp_st)
+        with torch.cuda.stream(d2h_st):
+            d2h_st.wait_event(ev["done"][i])
+            host_out[c * ob:(c + 1) * ob].copy_(out, non_blocking=True)
+            ev["out_free"][i].record(d2h_st)
+
+    def timed_duplex():
+        for c in range(min(slots, nchunk)):  # warm
+            chunk_duplex(c)
+        torch.cuda.synchronize()
+        host_out.fill_(0)
+        reps = 2
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for c in range(nchunk):
+                chunk_duplex(c)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
     def verify_chunks():
         """chunk 0 and the last chunk: open on the device, plaintext == rows,
         FEC plaintext == XOR of the group's rows"""
@@ -1405,10 +1458,16 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
 
     wall_direct = timed(True)
     ok_direct = verify_chunks()
-    wall = timed(False)
-    ok = verify_chunks()
+    wall_slots = timed(False)
+    ok_slots = verify_chunks()
+    wall_duplex = timed_duplex()
+    ok_duplex = verify_chunks()
     for s in S:
         s["ctx"].close()
+    cctx.close()
+    # the leg's figure: the better of the two copy schedules
+    duplex_best = wall_duplex <= wall_slots
+    wall, ok = (wall_duplex, ok_duplex) if duplex_best else (wall_slots, ok_slots)
     payload = G * k * L
     res = {"groups": G, "chunk_groups": cg, "slots": slots, "header": hdr,
            "payload_GiBps": round(payload / wall / 2**30, 2),
@@ -1416,12 +1475,22 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
            "pcie_h2d_bytes": G * k * L + G * (k + 1) * hdr,
            "pcie_d2h_bytes": G * (k + 1) * (L + 12),
            "verified": bool(ok),
+           "schedule": "duplex" if duplex_best else "slots",
+           "duplex": {"payload_GiBps": round(payload / wall_duplex / 2**30, 2),
+                      "wall_ms": round(wall_duplex * 1e3, 2), "verified": bool(ok_duplex),
+                      "link_GBps_combined": round((G * k * L + G * (k + 1) * hdr +
+                                                   G * (k + 1) * (L + 12)) / wall_duplex / 1e9, 1),
+                      "note": "one H2D stream, one compute stream, one D2H stream, events "
+                              "between them (each copy direction in a queue of its own)"},
+           "slots": {"payload_GiBps": round(payload / wall_slots / 2**30, 2),
+                     "wall_ms": round(wall_slots * 1e3, 2), "verified": bool(ok_slots),
+                     "note": "3 streams, each: H2D, encode + seal, D2H"},
            "direct_out": {"payload_GiBps": round(payload / wall_direct / 2**30, 2),
                           "wall_ms": round(wall_direct * 1e3, 2), "verified": bool(ok_direct),
                           "note": "the seal kernel stores the ciphertexts into pinned host "
                                   "memory itself (no D2H copy)"},
            "note": "pinned host plaintext -> H2D -> FEC encode + AES-128-GCM-12 seal of data and "
-                   "FEC packets -> D2H ciphertext; one PCIe crossing each way, 3 streams"}
+                   "FEC packets -> D2H ciphertext; one PCIe crossing each way"}
     del host_rows, host_out, host_hdr, S
     torch.cuda.empty_cache()
     if cpu:
