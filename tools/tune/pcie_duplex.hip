@@ -9,6 +9,7 @@
 //   dma_h2d, dma_d2h        hipMemcpyAsync alone, one stream
 //   dma_both                H2D and D2H at once on two non-blocking streams
 //   dma_both_chunked        the same as 64-MiB chunks, 4 streams each way
+//   dma_both_2streams_chunkN  N-MiB chunks, one stream each way
 //   zc_read                 a kernel reading mapped host memory into HBM (the
 //                           QFEC_PTR_MAPPED input side)
 //   zc_write                a kernel writing HBM to mapped host memory
@@ -116,6 +117,18 @@ int main(int argc, char** argv) {
       CK(hipMemcpyAsync(h_out + o, d_out + o, n, hipMemcpyDeviceToHost, s[4 + c % 4]));
     }
   }, 8);
+  // one stream per direction, chunked (the fused leg's duplex schedule)
+  auto chunk2 = [&](size_t ch) {
+    return timed([&] {
+      for (size_t o = 0; o < B; o += ch) {
+        const size_t n = std::min(ch, B - o);
+        CK(hipMemcpyAsync(d_in + o, h_in + o, n, hipMemcpyHostToDevice, s[0]));
+        CK(hipMemcpyAsync(h_out + o, d_out + o, n, hipMemcpyDeviceToHost, s[1]));
+      }
+    }, 2);
+  };
+  const double t_c2_16 = chunk2(16ull << 20), t_c2_64 = chunk2(64ull << 20),
+               t_c2_256 = chunk2(256ull << 20);
   const double t_zcr = timed([&] { zcr(s[0]); }, 1);
   const double t_zcw = timed([&] { zcw(s[0]); }, 1);
   const double t_zcr_d2h = timed([&] { zcr(s[0]); d2h(s[1]); }, 2);
@@ -126,9 +139,12 @@ int main(int argc, char** argv) {
               "\"dma_h2d\": %.2f, \"dma_d2h\": %.2f, \"dma_both_combined\": %.2f, "
               "\"dma_both_chunked_combined\": %.2f, \"zc_read\": %.2f, \"zc_write\": %.2f, "
               "\"zc_read_plus_dma_d2h_combined\": %.2f, \"dma_h2d_plus_zc_write_combined\": %.2f, "
-              "\"zc_both_combined\": %.2f, \"unit\": \"GB/s\"}\n",
+              "\"zc_both_combined\": %.2f, \"dma_both_2streams_chunk16M\": %.2f, "
+              "\"dma_both_2streams_chunk64M\": %.2f, \"dma_both_2streams_chunk256M\": %.2f, "
+              "\"unit\": \"GB/s\"}\n",
               B, sdma ? sdma : "(unset)", g / t_h2d, g / t_d2h, 2 * g / t_both, 2 * g / t_chunk,
-              g / t_zcr, g / t_zcw, 2 * g / t_zcr_d2h, 2 * g / t_h2d_zcw, 2 * g / t_zc_both);
+              g / t_zcr, g / t_zcw, 2 * g / t_zcr_d2h, 2 * g / t_h2d_zcw, 2 * g / t_zc_both,
+              2 * g / t_c2_16, 2 * g / t_c2_64, 2 * g / t_c2_256);
   // check the data arrived (one byte per page)
   CK(hipDeviceSynchronize());
   std::vector<uint8_t> chk(B);
