@@ -18,10 +18,11 @@ def main():
     ctx = qfec.Context(0)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
-    for slots in (3, 4, 2):
-        r = bench.bench_fused(ctx, torch, dev, stream, 10, 1350, slots=slots, cpu=False)
-        print(json.dumps({"n_slots": slots, **{k: r[k] for k in ("payload_GiBps", "schedule", "duplex",
-                                                            "slots", "direct_out")}}), flush=True)
+    for slots, cg in ((3, 4096), (3, 16384), (2, 16384), (4, 8192)):
+        r = bench.bench_fused(ctx, torch, dev, stream, 10, 1350, cg=cg, slots=slots, cpu=False)
+        print(json.dumps({"n_slots": slots, "chunk_groups": cg,
+                          **{k: r[k] for k in ("payload_GiBps", "schedule", "duplex", "slots",
+                                               "direct_out")}}), flush=True)
     ctx.close()
 
 
