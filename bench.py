@@ -1330,12 +1330,20 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
     key = torch.arange(16, dtype=torch.uint8, device=dev) * 11 + 3
     pre = torch.tensor([0xA0, 0xA1, 0xA2, 0xA3], dtype=torch.uint8, device=dev)
     pn = [((c * cg + grp) * (k + 1) + idx + 1) for c in range(nchunk)]  # per chunk
-    S = []
-    for s in range(slots):
-        st = torch.cuda.Stream(device=dev)
+    # streams (and a context on each): slot i's stream in the slot schedule;
+    # the duplex schedule's H2D / compute / D2H streams are streams 0 / 1 / 2
+    # -- no more streams than the process's hardware queues (4 with the default
+    # stream): a stream that shares a queue with another runs behind its work
+    nst = max(3, slots)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
+    ctxs = []
+    for st in streams:
         c = qfec.Context(dev.index)
         c.set_stream(st)
-        S.append({"stream": st, "ctx": c,
+        ctxs.append(c)
+    S = []
+    for s in range(slots):
+        S.append({"stream": streams[s], "ctx": ctxs[s],
                   "buf": torch.empty(rows_b + par_b + hdr_b, dtype=torch.uint8, device=dev),
                   "out": torch.empty(npk * (L + 12), dtype=torch.uint8, device=dev)})
 
@@ -1364,9 +1372,8 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
     # their own (tools/tune/pcie_duplex.hip: one copy each way on two streams
     # 97 GB/s combined; the same bytes as 64-MiB chunks over 8 streams 64 GB/s,
     # as the slot form's 3 streams that each copy in, compute and copy out).
-    h2d_st, cmp_st, d2h_st = (torch.cuda.Stream(device=dev) for _ in range(3))
-    cctx = qfec.Context(dev.index)
-    cctx.set_stream(cmp_st)
+    h2d_st, cmp_st, d2h_st = streams[0], streams[1], streams[2]
+    cctx = ctxs[1]
     ev = {n: [torch.cuda.Event() for _ in range(slots)]
           for n in ("in", "done", "buf_free", "out_free")}
 
@@ -1462,9 +1469,8 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
     ok_slots = verify_chunks()
     wall_duplex = timed_duplex()
     ok_duplex = verify_chunks()
-    for s in S:
-        s["ctx"].close()
-    cctx.close()
+    for c in ctxs:
+        c.close()
     # the leg's figure: the better of the two copy schedules
     duplex_best = wall_duplex <= wall_slots
     wall, ok = (wall_duplex, ok_duplex) if duplex_best else (wall_slots, ok_slots)
