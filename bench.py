@@ -659,6 +659,12 @@ def line_summary(line):
     for leg, key in (("e2e_pinned_host", "encode_GiBps"), ("e2e_fec_gcm", "payload_GiBps")):
         if isinstance(line.get(leg), dict):
             s[f"{leg}_{key}"] = line[leg].get(key)
+    fg = line.get("e2e_fec_gcm")
+    if isinstance(fg, dict):
+        s["e2e_fec_gcm_link_frac_of_duplex_ceiling"] = fg.get("link_frac_of_duplex_ceiling")
+        cbv = g(fg, "cpu_baseline", "value")
+        if cbv:
+            s["e2e_fec_gcm_vs_cpu"] = round(fg["payload_GiBps"] / cbv, 2)
     ce = line.get("connection_e2e")
     if isinstance(ce, dict) and ce.get("runs"):
         s["connection_e2e_host_us_per_group"] = {
@@ -1293,7 +1299,7 @@ def bench_connection_e2e():
     return res
 
 
-def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slots=3, cpu=True):
+def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=16384, slots=3, cpu=True):
     """Host memory in, host memory out, FEC + packet protection on the device
     with ONE PCIe crossing each way:
     per chunk of cg groups, H2D of the plaintext payloads + headers, FEC encode
@@ -1463,6 +1469,23 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps
 
+    # the link's both-ways ceiling, measured here: 1 GiB each way at once, one
+    # stream per direction (tools/tune/pcie_duplex.hip: 94-97 GB/s with SDMA)
+    nb = 1 << 30
+    din = torch.empty(nb, dtype=torch.uint8, device=dev)
+    dout = torch.empty(nb, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    duplex_ceiling = 0.0
+    for _ in range(3):
+        t0 = time.perf_counter()
+        with torch.cuda.stream(streams[0]):
+            din.copy_(host_rows[:nb], non_blocking=True)
+        with torch.cuda.stream(streams[2]):
+            host_out[:nb].copy_(dout, non_blocking=True)
+        torch.cuda.synchronize()
+        duplex_ceiling = max(duplex_ceiling, 2 * nb / (time.perf_counter() - t0) / 1e9)
+    del din, dout
+    torch.cuda.empty_cache()
     wall_direct = timed(True)
     ok_direct = verify_chunks()
     wall_slots = timed(False)
@@ -1482,6 +1505,10 @@ def bench_fused(ctx0, torch, dev, stream, k, L, G=1 << 18, hdr=22, cg=4096, slot
            "pcie_d2h_bytes": G * (k + 1) * (L + 12),
            "verified": bool(ok),
            "schedule": "duplex" if duplex_best else "slots",
+           "pcie_duplex_ceiling_GBps": round(duplex_ceiling, 1),
+           "link_frac_of_duplex_ceiling": round((G * k * L + G * (k + 1) * hdr +
+                                                 G * (k + 1) * (L + 12)) / wall / 1e9 /
+                                                duplex_ceiling, 3),
            "duplex": {"payload_GiBps": round(payload / wall_duplex / 2**30, 2),
                       "wall_ms": round(wall_duplex * 1e3, 2), "verified": bool(ok_duplex),
                       "link_GBps_combined": round((G * k * L + G * (k + 1) * hdr +
