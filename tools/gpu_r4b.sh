@@ -9,7 +9,7 @@ TAG=${1:-r4b}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 240 tools/tune/build/phased_copy 4096 5 3 > "$OUT/phased_copy.txt" 2>&1 &&
+timeout -k 10 400 python -u tools/fused_probe.py > "$OUT/fused_probe.txt" 2>&1 &&
 bash tools/gpu_check.sh "$TAG" &&
 bash tools/pmc.sh "$TAG" &&
 bash tools/pmc_protect.sh "$TAG"
