@@ -118,7 +118,8 @@ def build_cpp_tests(force: bool = False) -> list:
 # (tools/tune): rebuilt whenever those change, so a tool never runs with a
 # stale view of a class layout (round 4: host_cost built before a
 # QuicFecGroup layout change corrupted its heap on the GPU box).
-TOOLS = [("host_cost.cc", False), ("pcie_duplex.hip", True), ("phased_copy.hip", True)]
+TOOLS = [("host_cost.cc", False), ("pcie_duplex.hip", True), ("phased_copy.hip", True),
+         ("null_phased.hip", True)]
 
 
 def build_tools(force: bool = False) -> list:
