@@ -1268,11 +1268,22 @@ def bench_connection_e2e():
     # (32-MiB hipHostMalloc slabs, reused once drained) are not per-group costs
     h.run(n_pairs=4096, group_size=10, drop_every=2, stream_len=20_000, batched=True,
           require_gpu=True)
+    def host_per_group(r):
+        return (r["fec_host_us"] - r["fec_wait_us"]) / max(1, r["groups_encoded"] +
+                                                             r["groups_revived"])
+
     for n, stream in ((1, 400_000), (64, 100_000), (4096, 20_000)):
-        t0 = time.perf_counter()
-        r = h.run(n_pairs=n, group_size=10, drop_every=2, stream_len=stream, batched=True,
-                  require_gpu=True)
-        wall = time.perf_counter() - t0
+        # three runs, the median one reported (a run has 4-300 launches: one
+        # slow launch moves a single run's per-group figure by tens of percent)
+        rs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = h.run(n_pairs=n, group_size=10, drop_every=2, stream_len=stream, batched=True,
+                      require_gpu=True)
+            rs.append((host_per_group(r), time.perf_counter() - t0, r))
+        rs.sort(key=lambda x: x[0])
+        _, wall, r = rs[1]
+        spread = [round(x[0], 3) for x in rs]
         groups = r["groups_encoded"] + r["groups_revived"]
         enc = max(1, r["groups_encoded"])
         res["runs"].append({
@@ -1285,6 +1296,7 @@ def bench_connection_e2e():
             # queueing) and the completion, without the time blocked waiting
             # for the device (a polling loop does other work then)
             "gpu_host_us_per_group": round((r["fec_host_us"] - r["fec_wait_us"]) / max(1, groups), 3),
+            "gpu_host_us_per_group_3runs": spread,
             "gpu_wait_us_per_launch": round(r["fec_wait_us"] / max(1, r["launches"]), 2),
             "launch_us_per_launch": round(r["fec_launch_us"] / max(1, r["launches"]), 2),
             # of the launch: CSR tables / C-ABI calls per group; the slowest launch
