@@ -408,6 +408,15 @@ int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on);
  * connection integration: groups go without FEC). */
 int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
 
+/* Small-batch service (round 4): QFEC_PTR_MAPPED ragged batches of at most 16
+ * groups are taken by a resident worker kernel from a ring in host-mapped
+ * memory instead of a kernel launch each; the worker leaves after 2 ms
+ * without work and is relaunched by the next such batch.  on = 1 / 0
+ * enables / disables it (0 also makes a running worker leave; -1 leaves the
+ * setting); stats (may be NULL) receives {worker launches, jobs finished,
+ * worker alive}.  Test / measurement hook; the service is on by default. */
+int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
+
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of
  * splitmix64(seed ^ ((g*256 + i) << 32) ^ (j/8)) — generated on the device so

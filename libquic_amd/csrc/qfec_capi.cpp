@@ -102,6 +102,7 @@ struct qfec_ctx {
   struct AsyncOp {
     bool live = false;
     bool direct = false;   // completion by the host-mapped flag (token)
+    bool svc = false;      // ... set by the small-batch service (no event)
     bool recover = false;
     uint32_t token = 0;
     uint64_t cnt = 0;
@@ -115,6 +116,18 @@ struct qfec_ctx {
   // reused, a synchronous call draining the slots), kept for
   // qfec_complete_ticket: each op's code reaches its own caller only
   std::map<uint64_t, int> finished;
+  // small-batch service (qfec_internal.h SvcJob): a resident worker on a
+  // stream of its own takes mapped async batches of <= kSvcGroups groups from
+  // a ring in host-mapped memory -- no kernel launch per batch
+  hipStream_t svc_stream = nullptr;
+  qfec::SvcShared* svc_sh = nullptr;  // host-mapped control words
+  qfec::SvcShared* svc_sh_dev = nullptr;
+  qfec::SvcJob* svc_ring = nullptr;   // host-mapped job ring
+  qfec::SvcJob* svc_ring_dev = nullptr;
+  uint64_t svc_published = 0;
+  uint32_t svc_seq = 0;
+  uint64_t svc_launches = 0;
+  bool svc_on = true;  // test hook qfec_debug_service
   // device scratch of the host-pointer xor / protection / entropy calls:
   // grow-only buffers kept for the context's life (no allocation per call)
   std::vector<void*> scratch_p;
@@ -230,6 +243,82 @@ int ensure_staging(qfec_ctx* ctx) {
   return QFEC_OK;
 }
 
+// ---- small-batch service ---------------------------------------------------
+constexpr uint64_t kSvcGroups = 16;           // batches up to this size use it
+constexpr uint64_t kSvcIdleTicks = 200000;   // 2 ms at the 100-MHz wall clock
+
+int ensure_service(qfec_ctx* ctx) {
+  if (ctx->svc_stream) return QFEC_OK;
+  const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
+  QFEC_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->svc_sh), sizeof(qfec::SvcShared), fl));
+  std::memset(static_cast<void*>(ctx->svc_sh), 0, sizeof(qfec::SvcShared));
+  QFEC_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->svc_ring),
+                              qfec::kSvcRing * sizeof(qfec::SvcJob), fl));
+  std::memset(static_cast<void*>(ctx->svc_ring), 0, qfec::kSvcRing * sizeof(qfec::SvcJob));
+  for (uint32_t i = 0; i < qfec::kSvcRing; ++i) ctx->svc_ring[i].seq = 0xFFFFFFFFu;  // none yet
+  QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_sh_dev), ctx->svc_sh, 0));
+  QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_ring_dev), ctx->svc_ring, 0));
+  QFEC_HIP(ctx, hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
+  return QFEC_OK;
+}
+
+// Queue batch `a` (tables in slot `slot`'s mapped buffer) as one job; its
+// completion is token in the slot's flag.  Publishes, then relaunches the
+// worker if it has left (or never ran).
+int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token) {
+  int rc = ensure_service(ctx);
+  if (rc) return rc;
+  qfec::SvcShared* sh = ctx->svc_sh;
+  // the ring entry of job seq - kSvcRing is free: at most kSlots jobs are
+  // outstanding (each holds a slot until completed) and kSvcRing > kSlots
+  static_assert(qfec::kSvcRing > kSlots, "service ring smaller than the slots");
+  const uint32_t seq = ctx->svc_seq++;
+  qfec::SvcJob& j = ctx->svc_ring[seq % qfec::kSvcRing];
+  j.a = a;
+  j.a.done_count = nullptr;
+  j.a.done_flag = nullptr;
+  j.start = ctx->svc_published;
+  j.recover = recover ? 1u : 0u;
+  j.flag_slot = (uint32_t)slot;
+  j.token = token;
+  __atomic_store_n(&j.seq, seq, __ATOMIC_RELEASE);
+  ctx->svc_published += a.n_groups;
+  __atomic_store_n(&sh->pub_end, ctx->svc_published, __ATOMIC_RELEASE);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) == 0u) {
+    __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
+    QFEC_HIP(ctx, qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_ring_dev, ctx->h_flag_dev,
+                                              kSvcIdleTicks, ctx->svc_stream));
+    ++ctx->svc_launches;
+  }
+  return QFEC_OK;
+}
+
+// Wait for a service job's token; the worker's stream is polled now and then,
+// so a worker that faulted or left without the job ends in an error, not a
+// hang.
+int wait_flag_svc(qfec_ctx* ctx, int si, uint32_t token) {
+  const uint32_t* f = ctx->h_flag + si;
+  for (uint32_t spins = 1;; ++spins) {
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
+    if ((spins & 4095u) == 0) {
+      const hipError_t q = hipStreamQuery(ctx->svc_stream);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
+        return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service left without finishing a job");
+      }
+      if (q != hipErrorNotReady) QFEC_HIP(ctx, q);
+    }
+  }
+}
+
+void stop_service(qfec_ctx* ctx) {
+  if (!ctx->svc_stream) return;
+  __atomic_store_n(&ctx->svc_sh->quit, 1u, __ATOMIC_SEQ_CST);
+  (void)hipStreamSynchronize(ctx->svc_stream);
+  __atomic_store_n(&ctx->svc_sh->alive, 0u, __ATOMIC_SEQ_CST);
+}
+
 // Wait for a launch_ragged_latency kernel by spinning on its host-mapped
 // completion flag (a few us sooner than the event's wait path); the slot's
 // event, recorded after the launch, is polled now and then so that a flag
@@ -259,7 +348,13 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   qfec_ctx::AsyncOp& op = ctx->async_ops[si];
   if (!op.live) return QFEC_OK;
   Slot& s = ctx->slots[si];
-  if (op.direct) {
+  if (op.svc) {
+    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token)
+      return QFEC_PENDING;
+    op.live = false;
+    const int wrc = wait_flag_svc(ctx, si, op.token);
+    if (wrc) return wrc;
+  } else if (op.direct) {
     if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
       const hipError_t q = hipEventQuery(s.done);
       if (q == hipErrorNotReady) return QFEC_PENDING;
@@ -800,7 +895,11 @@ qfec_ctx* qfec_create(int device) {
 void qfec_destroy(qfec_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  stop_service(ctx);  // before the device-wide wait: a resident worker would hold it
   (void)hipDeviceSynchronize();
+  if (ctx->svc_stream) (void)hipStreamDestroy(ctx->svc_stream);
+  if (ctx->svc_sh) (void)hipHostFree(ctx->svc_sh);
+  if (ctx->svc_ring) (void)hipHostFree(ctx->svc_ring);
   for (auto& s : ctx->slots) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -1208,13 +1307,14 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   struct Pend {
     uint64_t g0 = 0, cnt = 0;
     uint32_t token = 0;  // direct: the completion flag's value
+    bool svc = false;    // ... set by the small-batch service
     bool live = false;
   } pend[kSlots];
   auto finish = [&](int si) -> int {
     Pend& c = pend[si];
     if (!c.live) return QFEC_OK;
     if (c.token) {
-      const int wrc = wait_flag(ctx, si, c.token);
+      const int wrc = c.svc ? wait_flag_svc(ctx, si, c.token) : wait_flag(ctx, si, c.token);
       if (wrc) return wrc;
     } else {
       QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
@@ -1294,26 +1394,34 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       a.out = parity_out;
     }
     uint32_t token = 0;
+    bool svc = false;
     if (direct) {
       token = ++ctx->flag_token ? ctx->flag_token : ++ctx->flag_token;  // never 0
       a.done_count = ctx->d_done + slot;
       a.done_flag = ctx->h_flag_dev + slot;
       a.done_token = token;
-      if (cnt <= kDirectGroups)
+      // a few groups: the resident service worker takes them from its ring
+      // (no launch); a flag is all their completion needs
+      svc = ctx->svc_on && cnt <= kSvcGroups;
+      if (svc)
+        rc = svc_submit(ctx, slot, a, recover, token);
+      else if (cnt <= kDirectGroups)
         QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
       else
         QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+      if (rc) return rc;
     } else {
       QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
     }
     if (!recover && !direct)
       QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
                                    hipMemcpyDeviceToHost, s.stream));
-    QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
+    if (!svc) QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
     if (async) {  // the whole batch in this slot: completed by qfec_complete
       qfec_ctx::AsyncOp& op = ctx->async_ops[slot];
       op.live = true;
       op.direct = direct;
+      op.svc = svc;
       op.recover = recover;
       op.token = token;
       op.cnt = cnt;
@@ -1326,6 +1434,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     pend[slot].g0 = g0;
     pend[slot].cnt = cnt;
     pend[slot].token = token;
+    pend[slot].svc = svc;
     pend[slot].live = true;
     slot = (slot + 1) % kSlots;
   }
@@ -1700,6 +1809,24 @@ int qfec_phase_abandons(qfec_ctx* ctx, uint32_t* count) {
 int qfec_phase_backoff(qfec_ctx* ctx) { return ctx ? (int)ctx->phase_backoff : -1; }
 
 int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_phased : -1; }
+
+int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  if (on >= 0) {
+    ctx->svc_on = on != 0;
+    if (!ctx->svc_on) {
+      stop_service(ctx);  // a resident worker leaves at once
+    } else if (ctx->svc_sh) {
+      __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
+    }
+  }
+  if (stats) {
+    stats[0] = ctx->svc_launches;
+    stats[1] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->jobs, __ATOMIC_ACQUIRE) : 0;
+    stats[2] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) : 0;
+  }
+  return QFEC_OK;
+}
 
 int qfec_debug_fail_launches(qfec_ctx* ctx, int on) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");

@@ -80,6 +80,34 @@ struct RaggedArgs {
   uint32_t done_token;
 };
 
+// Small-batch service (round 4): one resident workgroup that takes mapped
+// ragged batches from a ring in host-mapped memory instead of a kernel launch
+// per batch (the launch is most of a small flush's connection-thread cost).
+// The host writes a job, then publishes pub_end (the groups published so
+// far); the worker processes every published group (one wave per group, the
+// small-batch kernel's body), stores each job's token into its slot's flag
+// and `consumed`, and exits after idle_ticks without work (alive = 0, then one
+// more look at pub_end: the host, after publishing, relaunches it if it
+// reads alive == 0 -- each side writes, fences, then reads the other's word).
+struct SvcJob {
+  RaggedArgs a;       // tables in the mapped slot buffer, as the direct path
+  uint64_t start;     // the job's first group in the global group sequence
+  uint32_t seq;       // job number (ring index = seq % kSvcRing)
+  uint32_t recover;
+  uint32_t flag_slot; // index into the context's host-mapped flags
+  uint32_t token;
+};
+struct SvcShared {
+  uint64_t pub_end;   // host: groups published
+  uint64_t consumed;  // worker: groups finished (a new worker starts here)
+  uint32_t alive;     // host: 1 when it launches a worker; worker: 0 on its way out
+  uint32_t quit;      // host: exit now (context destroyed)
+  uint64_t jobs;      // worker: jobs finished (stats)
+};
+constexpr uint32_t kSvcRing = 8;
+hipError_t launch_ragged_service(SvcShared* sh, const SvcJob* ring, uint32_t* flags,
+                                 uint64_t idle_ticks, hipStream_t s);
+
 // Packet protection batch (qpp_kernels.hip): packet p's associated data (the
 // packet header) is ad_len[p] bytes at bytes + ad_off[p], its input payload
 // in_len[p] bytes at bytes + in_off[p], its output at out + out_off[p].

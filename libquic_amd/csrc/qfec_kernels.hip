@@ -1387,6 +1387,118 @@ __global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
   ragged_signal_done(a);
 }
 
+// The small-batch service worker (qfec_internal.h SvcJob / SvcShared): ONE
+// workgroup of kSvcWaves waves, resident while batches keep coming.  Thread 0
+// polls the host-mapped pub_end; every published group is then taken by one
+// wave (window_group, as the small-batch kernel); after a barrier every
+// thread's outputs are made visible system-wide and thread 0 stores each
+// finished job's token into its flag.  Host memory is read through a
+// system-scope acquire after each poll (a resident kernel gets no cache
+// invalidation from a dispatch: the tables and payloads of a reused slot
+// buffer would otherwise be read stale).  Exit: idle_ticks without work, or
+// quit.  All control stores are vector stores.
+constexpr int kSvcWaves = 8;
+
+__device__ __forceinline__ uint64_t svc_load64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t svc_load32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShared* sh,
+                                                                        const SvcJob* ring,
+                                                                        uint32_t* flags,
+                                                                        uint64_t idle_ticks) {
+  __shared__ uint32_t s_par[kSvcWaves][4 * kParWin];
+  __shared__ uint64_t s_head[kSvcWaves][kParWin];
+  __shared__ u32x4 s_meta[kSvcWaves][64];
+  __shared__ uint64_t s_from, s_to;
+  __shared__ uint32_t s_job, s_exit;
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) {
+    // where the previous worker stopped: jobs are finished whole and in
+    // order, so the next job's number is the count finished
+    s_from = svc_load64(&sh->consumed);
+    s_job = (uint32_t)svc_load64(&sh->jobs);
+  }
+  __syncthreads();
+  for (;;) {
+    if (tid == 0) {
+      const uint64_t from = s_from;
+      uint64_t to = svc_load64(&sh->pub_end);
+      uint64_t t0 = wall_clock64();
+      uint32_t ex = 0;
+      while (to == from) {
+        if (svc_load32(&sh->quit) != 0u) {
+          ex = 1;
+          break;
+        }
+        if (wall_clock64() - t0 > idle_ticks) {
+          // leaving: say so, then look once more (the host publishes, then
+          // reads alive: one of the two sees the other's store)
+          __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+          __atomic_thread_fence(__ATOMIC_SEQ_CST);
+          to = svc_load64(&sh->pub_end);
+          if (to == from) {
+            ex = 1;
+            break;
+          }
+          __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+        to = svc_load64(&sh->pub_end);
+      }
+      s_to = to;
+      s_exit = ex;
+    }
+    __syncthreads();
+    if (s_exit) break;
+    // every thread: drop cached copies of host memory (slot tables, payloads)
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint64_t from = s_from, to = s_to;
+    uint32_t j = s_job;  // wave-uniform: the job holding the next group
+    for (uint64_t gi = from + wv; gi < to; gi += kSvcWaves) {
+      const SvcJob* jb = ring + (j % kSvcRing);
+      uint32_t hops = 0;  // bounded: a group outside every ring entry is skipped
+      while ((jb->seq != j || gi < jb->start || gi >= jb->start + jb->a.n_groups) &&
+             hops < kSvcRing) {
+        ++j;
+        ++hops;
+        jb = ring + (j % kSvcRing);
+      }
+      if (hops == kSvcRing) continue;  // never with a well-formed ring
+      const uint64_t g = gi - jb->start;
+      if (jb->recover)
+        window_group<true, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+      else
+        window_group<false, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+    }
+    __threadfence_system();  // every output visible before any token
+    __syncthreads();
+    if (tid == 0) {
+      // every job published below `to` is finished (a ring entry not yet
+      // rewritten for job jj still carries job jj - kSvcRing: its seq says so)
+      uint32_t jj = s_job;
+      for (;;) {
+        const SvcJob* jb = ring + (jj % kSvcRing);
+        if (jb->seq != jj || jb->start >= to) break;
+        __hip_atomic_store(flags + jb->flag_slot, jb->token, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        ++jj;
+      }
+      s_job = jj;
+      s_from = to;
+      __hip_atomic_store(&sh->consumed, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&sh->jobs, (uint64_t)jj, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------------------
 // out ^= in (XorBuffers).
 // ---------------------------------------------------------------------------
@@ -1710,6 +1822,13 @@ hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t 
   else
     hipLaunchKernelGGL((ragged_window_kernel<false, true, 16>), dim3((uint32_t)blocks),
                        dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ragged_service(SvcShared* sh, const SvcJob* ring, uint32_t* flags,
+                                 uint64_t idle_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(ragged_service_kernel, dim3(1), dim3(64 * kSvcWaves), 0, s, sh, ring, flags,
+                     idle_ticks);
   return hipGetLastError();
 }
 

@@ -98,6 +98,7 @@ SIGNATURES = [
     ("qfec_debug_phase_regsteps", C.c_int, [_vp, C.c_int]),
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
+    ("qfec_debug_service", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
     ("qfec_complete_ticket", C.c_int, [_vp, C.c_uint64, C.c_int]),
@@ -411,6 +412,13 @@ class Context:
         raises its own error only."""
         rc = self.lib.qfec_complete_ticket(self.ctx, ticket, 1 if wait else 0)
         return rc if rc == 1 else self._check(rc)
+
+    def debug_service(self, on=None):
+        """Small-batch service hook: on True / False enables / disables the
+        resident worker (None leaves it); returns {launches, jobs, alive}."""
+        st = (C.c_uint64 * 3)()
+        self._check(self.lib.qfec_debug_service(self.ctx, -1 if on is None else int(bool(on)), st))
+        return {"launches": st[0], "jobs": st[1], "alive": st[2]}
 
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""

@@ -1,0 +1,116 @@
+"""GPU tests of the small-batch service (round 4; qfec_capi.cpp svc_submit,
+qfec_kernels.hip ragged_service_kernel): QFEC_PTR_MAPPED ragged batches of at
+most 16 groups are taken by ONE resident worker workgroup from a job ring in
+host-mapped memory instead of a kernel launch each.  The worker leaves after
+2 ms without work and the next batch relaunches it (the host publishes, then
+reads the worker's alive word; the worker clears it, then reads the published
+count once more).  Every result is bit-exact against the oracle; the cases
+below cross the idle exit on purpose, mix service jobs with launched batches
+on one context, and close a context while its worker is resident.
+"""
+import time
+
+import numpy as np
+import pytest
+
+from libquic_amd import qfec
+from test_hip_mapped import _mapped_case
+from test_hip_ragged import run_ragged
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(ctx, z, want_l):
+    par, plen, out = run_ragged(ctx, z, host="mapped")
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, z["parity"])
+    assert np.array_equal(out, z["recovered"])
+
+
+def test_service_parity_across_idle_exits():
+    """Small batches of every shape (k 1-80: groups beyond the fast form run
+    the exact per-group body; packets 1-1452 B), with pauses before some of
+    them longer than the worker's 2-ms idle time: every result exact, and the
+    worker was relaunched after leaving."""
+    ctx = qfec.Context(0)
+    try:
+        rng = np.random.default_rng(11)
+        calls = 0
+        for it in range(40):
+            n = int(rng.integers(1, 17))
+            z, want_l = _mapped_case(n, g0=20000 + 50 * it, kmin=1, kmax=80, lmin=1, lmax=1452,
+                                     seed=it)
+            _check(ctx, z, want_l)
+            calls += 2  # an encode and a recover
+            time.sleep([0.0, 0.0, 0.001, 0.004][it % 4])
+        st = ctx.debug_service()
+        assert st["jobs"] >= calls, st
+        assert st["launches"] >= 5, st  # idle exits (4 ms pauses) and relaunches
+    finally:
+        ctx.close()
+
+
+def test_service_off_matches_on():
+    """The same batches with the service off (the launched small-batch kernel)
+    give the same bytes; no worker is launched while it is off."""
+    ctx = qfec.Context(0)
+    try:
+        z, want_l = _mapped_case(9, g0=31000, kmin=2, kmax=20, lmin=1, lmax=1452, seed=5)
+        _check(ctx, z, want_l)
+        on = ctx.debug_service()
+        assert on["jobs"] >= 2
+        ctx.debug_service(False)
+        before = ctx.debug_service()
+        for _ in range(5):
+            _check(ctx, z, want_l)
+        after = ctx.debug_service()
+        assert after["launches"] == before["launches"] and after["jobs"] == before["jobs"]
+        ctx.debug_service(True)
+        _check(ctx, z, want_l)
+        assert ctx.debug_service()["jobs"] >= before["jobs"] + 2
+    finally:
+        ctx.close()
+
+
+def test_service_async_mixed_with_launched_batches():
+    """QFEC_ASYNC on one context: small batches (service) and a 2,000-group
+    batch (the block kernel) queued back to back, completed by ticket in
+    reverse order; every output exact."""
+    ctx = qfec.Context(0)
+    bufs = []
+    try:
+        cases = []
+        for i, n in enumerate((3, 2000, 7)):
+            z, want_l = _mapped_case(n, g0=40000 + 3000 * i, kmin=2, kmax=30, lmin=1, lmax=1452,
+                                     seed=20 + i)
+            data = qfec.HostBuffer(len(z["data"]))
+            data.array[:] = z["data"]
+            par = qfec.HostBuffer(n * 1452)
+            bufs += [data, par]
+            plen = np.zeros(n, dtype=np.uint16)
+            ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n, par.array,
+                              z["parity_off"], plen, mapped=True, async_=True)
+            cases.append((ctx.async_ticket(), z, want_l, par, plen, n))
+        for t, z, want_l, par, plen, n in reversed(cases):
+            assert ctx.complete_ticket(t) == 0
+            assert np.array_equal(plen, want_l)
+            for g in range(n):
+                o, m = int(z["parity_off"][g]), int(want_l[g])
+                assert np.array_equal(par.array[o:o + m], z["parity"][o:o + m]), (n, g)
+    finally:
+        for b in bufs:
+            b.close()
+        ctx.close()
+
+
+def test_service_close_while_resident():
+    """A context closed right after a service job (its worker still resident,
+    waiting for more) closes at once: the worker leaves on the quit word."""
+    z, want_l = _mapped_case(4, g0=50000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=9)
+    for _ in range(5):
+        ctx = qfec.Context(0)
+        _check(ctx, z, want_l)
+        ctx.debug_service()  # usually still resident here (2-ms idle)
+        t0 = time.perf_counter()
+        ctx.close()
+        assert time.perf_counter() - t0 < 1.0
