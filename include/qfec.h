@@ -410,8 +410,9 @@ int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
 
 /* Small-batch service (round 4): QFEC_PTR_MAPPED ragged batches of at most 16
  * groups are taken by a resident worker kernel from a ring in host-mapped
- * memory instead of a kernel launch each; the worker leaves after 2 ms
- * without work and is relaunched by the next such batch.  on = 1 / 0
+ * memory instead of a kernel launch each; the worker leaves after 100 us
+ * without work (or before a phased launch of its context) and is relaunched
+ * by the next such batch.  on = 1 / 0
  * enables / disables it (0 also makes a running worker leave; -1 leaves the
  * setting); stats (may be NULL) receives {worker launches, jobs finished,
  * worker alive}.  Test / measurement hook; the service is on by default. */

@@ -245,7 +245,11 @@ int ensure_staging(qfec_ctx* ctx) {
 
 // ---- small-batch service ---------------------------------------------------
 constexpr uint64_t kSvcGroups = 16;           // batches up to this size use it
-constexpr uint64_t kSvcIdleTicks = 200000;   // 2 ms at the 100-MHz wall clock
+// idle time before the worker leaves: 100 us (100-MHz wall clock) -- below the
+// phased kernel's 200-us meeting timeout, so a worker of another context never
+// makes a phased launch give up its meetings; a flush loop that comes back
+// within it finds the worker resident
+constexpr uint64_t kSvcIdleTicks = 10000;
 
 int ensure_service(qfec_ctx* ctx) {
   if (ctx->svc_stream) return QFEC_OK;
@@ -692,6 +696,14 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
       --ctx->phase_backoff;
       a.phase_sync = nullptr;  // one-pass while contention persists
     } else {
+      // the phased kernel wants one workgroup on every CU: this context's
+      // resident small-batch worker (if any) leaves first (it holds a CU's
+      // LDS; a worker of another context leaves within kSvcIdleTicks, below
+      // the meetings' timeout)
+      if (ctx->svc_sh && __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u) {
+        stop_service(ctx);
+        __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
+      }
       if (ctx->phase_recorded && ctx->phase_stream != ctx->stream)
         QFEC_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->phase_done, 0));
       QFEC_HIP(ctx, qfec::launch_fixed(a, nt, ctx->stream));

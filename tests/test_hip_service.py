@@ -2,7 +2,7 @@
 qfec_kernels.hip ragged_service_kernel): QFEC_PTR_MAPPED ragged batches of at
 most 16 groups are taken by ONE resident worker workgroup from a job ring in
 host-mapped memory instead of a kernel launch each.  The worker leaves after
-2 ms without work and the next batch relaunches it (the host publishes, then
+100 us without work and the next batch relaunches it (the host publishes, then
 reads the worker's alive word; the worker clears it, then reads the published
 count once more).  Every result is bit-exact against the oracle; the cases
 below cross the idle exit on purpose, mix service jobs with launched batches
@@ -30,7 +30,7 @@ def _check(ctx, z, want_l):
 def test_service_parity_across_idle_exits():
     """Small batches of every shape (k 1-80: groups beyond the fast form run
     the exact per-group body; packets 1-1452 B), with pauses before some of
-    them longer than the worker's 2-ms idle time: every result exact, and the
+    them longer than the worker's 100-us idle time: every result exact, and the
     worker was relaunched after leaving."""
     ctx = qfec.Context(0)
     try:
@@ -45,7 +45,7 @@ def test_service_parity_across_idle_exits():
             time.sleep([0.0, 0.0, 0.001, 0.004][it % 4])
         st = ctx.debug_service()
         assert st["jobs"] >= calls, st
-        assert st["launches"] >= 5, st  # idle exits (4 ms pauses) and relaunches
+        assert st["launches"] >= 5, st  # idle exits (1-4 ms pauses) and relaunches
     finally:
         ctx.close()
 
@@ -110,7 +110,43 @@ def test_service_close_while_resident():
     for _ in range(5):
         ctx = qfec.Context(0)
         _check(ctx, z, want_l)
-        ctx.debug_service()  # usually still resident here (2-ms idle)
+        ctx.debug_service()
         t0 = time.perf_counter()
         ctx.close()
         assert time.perf_counter() - t0 < 1.0
+
+
+@pytest.mark.parametrize("same_ctx", [True, False])
+def test_phased_launch_right_after_service_job(same_ctx):
+    """The phased fixed-shape kernel wants one workgroup on every CU.  Right
+    after a service job -- its worker still resident -- a phased encode on the
+    same context (the worker is stopped first) or on another context (the
+    worker leaves within its 100-us idle time, below the meetings' 200-us
+    timeout) keeps its meetings: no abandoned launch."""
+    import torch
+    from oracle import qfec_np as Q
+    a = qfec.Context(0)
+    b = a if same_ctx else qfec.Context(0)
+    try:
+        k, L = 10, 1350
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        n = 8 * ncu * 40 * (256 // ((L + 15) // 16)) + 17
+        rows = torch.empty(n * k * L, dtype=torch.uint8, device="cuda:0")
+        b.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+        par = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        want = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        b.encode(rows, k, L, n, want, one_pass=True)
+        b.sync()
+        z, want_l = _mapped_case(5, g0=60000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=4)
+        for _ in range(3):
+            before = b.phase_abandons()
+            _check(a, z, want_l)  # a service job: the worker is resident now
+            b.encode(rows, k, L, n, par)
+            assert b.last_fixed_phased() == 1
+            b.sync()
+            assert b.phase_abandons() == before
+            assert torch.equal(par, want)
+    finally:
+        if not same_ctx:
+            b.close()
+        a.close()
