@@ -298,6 +298,11 @@ int main(int argc, char** argv) {
       {"prod recover 40+32", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32>},
       {"prod recover 40+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
       {"prod recover 40+48 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 48, true>},
+      // round 4: recover with fewer / other register steps
+      {"prod recover 40+24 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 24, true>},
+      {"prod recover 40+16 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 16, true>},
+      {"prod recover 32+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 32, 256, false, true, true, false, true, 32, true>},
+      {"prod recover 40+32 rpf again", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
       {"prod 256 x 40+56", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 56>},
       {"prod 256 x 40+48", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 48>},
   };
@@ -342,6 +347,9 @@ int main(int argc, char** argv) {
     if (pks[w].first.find("40+40") != std::string::npos) st = 80;
     if (pks[w].first.find("40+48") != std::string::npos) st = 88;
     if (pks[w].first.find("40+64") != std::string::npos) st = 104;
+    if (pks[w].first.find("40+24") != std::string::npos) st = 64;
+    if (pks[w].first.find("40+16") != std::string::npos) st = 56;
+    if (pks[w].first.find("32+32") != std::string::npos) st = 64;
     const uint32_t gpb = nt / 85u, grid = ncu * bpc;
     const uint64_t per = (uint64_t)grid * st * gpb;
     const uint32_t nph = (uint32_t)((G + per - 1) / per);
