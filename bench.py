@@ -605,13 +605,16 @@ def main(argv=None):
             line["entropy"] = bench_entropy(ctx, torch, dev, stream,
                                             cpu=not args.no_cpu_baseline)
         _progress("entropy done")
-        if not args.no_e2e:
-            line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
-        _progress("e2e done")
+        # the fused leg before the host-pointer leg: that one creates the
+        # context's staging streams, and the fewer streams the process has,
+        # the likelier each copy direction gets a hardware queue of its own
         if not args.no_fused:
             line["e2e_fec_gcm"] = bench_fused(ctx, torch, dev, stream, k, L,
                                               cpu=not args.no_cpu_baseline)
         _progress("fused e2e done")
+        if not args.no_e2e:
+            line["e2e_pinned_host"] = bench_e2e(ctx, torch, k, L)
+        _progress("e2e done")
         if not args.no_connection:
             line["connection"] = bench_connection(cpu=not args.no_cpu_baseline)
             _progress("connection flush done")
