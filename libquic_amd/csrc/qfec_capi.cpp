@@ -1415,13 +1415,18 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       // a few groups: the resident service worker takes them from its ring
       // (no launch); a flag is all their completion needs
       svc = ctx->svc_on && cnt <= kSvcGroups;
-      if (svc)
-        rc = svc_submit(ctx, slot, a, recover, token);
-      else if (cnt <= kDirectGroups)
-        QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
-      else
-        QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
-      if (rc) return rc;
+      if (svc && svc_submit(ctx, slot, a, recover, token) != QFEC_OK) {
+        // the service could not be set up or (re)launched: off for this
+        // context, this batch launched as before (same flag and token)
+        ctx->svc_on = false;
+        svc = false;
+      }
+      if (!svc) {
+        if (cnt <= kDirectGroups)
+          QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
+        else
+          QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+      }
     } else {
       QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
     }
