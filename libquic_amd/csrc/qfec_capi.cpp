@@ -291,8 +291,19 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
   if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) == 0u) {
     __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
-    QFEC_HIP(ctx, qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_ring_dev, ctx->h_flag_dev,
-                                              kSvcIdleTicks, ctx->svc_stream));
+    const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_ring_dev,
+                                                     ctx->h_flag_dev, kSvcIdleTicks,
+                                                     ctx->svc_stream);
+    if (e != hipSuccess) {
+      // no worker runs (none was alive): take the job back, so that no later
+      // worker ever runs it over a reused slot buffer
+      __atomic_store_n(&sh->alive, 0u, __ATOMIC_SEQ_CST);
+      ctx->svc_published -= a.n_groups;
+      __atomic_store_n(&sh->pub_end, ctx->svc_published, __ATOMIC_RELEASE);
+      __atomic_store_n(&j.seq, 0xFFFFFFFFu, __ATOMIC_RELEASE);
+      --ctx->svc_seq;
+      return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
+    }
     ++ctx->svc_launches;
   }
   return QFEC_OK;
