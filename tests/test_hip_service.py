@@ -150,3 +150,35 @@ def test_phased_launch_right_after_service_job(same_ctx):
         if not same_ctx:
             b.close()
         a.close()
+
+
+def test_service_idle_boundary_stress():
+    """Small async batches spaced around the worker's 100-us idle time (the
+    window where it may be leaving just as a batch is published): every one
+    completes, exact, and the worker was relaunched many times."""
+    ctx = qfec.Context(0)
+    z, want_l = _mapped_case(2, g0=70000, kmin=3, kmax=10, lmin=16, lmax=1350, seed=6)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(2 * 1452)
+    try:
+        rng = np.random.default_rng(3)
+        for it in range(300):
+            par.array[:] = 0
+            plen = np.zeros(2, dtype=np.uint16)
+            ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 2, par.array,
+                              z["parity_off"], plen, mapped=True, async_=True)
+            assert ctx.complete_ticket(ctx.async_ticket()) == 0
+            assert np.array_equal(plen, want_l), it
+            for g in range(2):
+                o, m = int(z["parity_off"][g]), int(want_l[g])
+                assert np.array_equal(par.array[o:o + m], z["parity"][o:o + m]), (it, g)
+            t_end = time.perf_counter() + float(rng.uniform(40e-6, 200e-6))
+            while time.perf_counter() < t_end:  # busy-wait: sleep() is too coarse
+                pass
+        st = ctx.debug_service()
+        assert st["jobs"] >= 300 and st["launches"] >= 10, st
+    finally:
+        data.close()
+        par.close()
+        ctx.close()
