@@ -1496,7 +1496,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
     }
     __syncthreads();
   }
-  if (tid == 0) __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (no store to `alive` here: an idle exit cleared it before its last look,
+  // and a late store could clobber the 1 the host wrote for a worker it has
+  // already queued behind this one; stop_service clears it after a quit)
 }
 
 // ---------------------------------------------------------------------------
