@@ -279,7 +279,8 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
 // register file to spare).
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
-          bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0, bool RPF = false>
+          bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0, bool RPF = false,
+          bool RPFE = false>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
@@ -330,6 +331,10 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         m_next[u] = lane_on && g < a.n_groups ? a.missing[g] : 0u;
       }
     }
+    // RPFE (tools/tune): the register steps' parity rows too, right after the
+    // LDS steps' ones -- the phase's whole parity range as one stream
+    u32x4 racc[RS > 0 ? RS : 1];
+    static_assert(!RPFE || (RS > 0 && RECOVER && RPF && PF), "RPFE: recover register steps, RPF");
     if constexpr (PF) {
       // PARFIRST: the phase's parity rows first, into the accumulators (one
       // stream over the parity buffer), then the received rows only
@@ -345,6 +350,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (i + j < STEPS) s_par[i + j][tid] = w[j];
+      }
+      if constexpr (RPFE) {
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          const uint64_t g = gidx(STEPS + j);
+          const bool on = lane_on && g < a.n_groups && STEPS + j < SP;
+          racc[j] = ld16t<NTLD>(a.parity + (on ? g : 0) * a.parity_stride + off);
+        }
       }
     }
 #pragma unroll 1
@@ -455,7 +468,6 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
       for (int u = 0; u < kPhU; ++u) s_par[i + u][tid] = acc[u];
     }
-    u32x4 racc[RS > 0 ? RS : 1];
     uint32_t ron[2] = {0u, 0u};  // step j's lane is on: bit j % 32 of word j / 32
     bool rbad = false;           // recover: a register step's lost slot out of range
     if constexpr (RS > 0) {
@@ -466,7 +478,7 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
       const uint64_t dq = B * gpb * a.group_stride;
       const uint8_t* qp = RECOVER ? a.parity + g0r * a.parity_stride + off : nullptr;
       const uint64_t dqp = RECOVER ? B * gpb * a.parity_stride : 0u;
-      if constexpr (RECOVER && RPF) {
+      if constexpr (RECOVER && RPF && !RPFE) {
         // RPF: every register step's parity row first (one stream, as the
         // LDS steps' PARFIRST), then the received rows step by step
 #pragma unroll

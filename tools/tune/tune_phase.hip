@@ -299,10 +299,9 @@ int main(int argc, char** argv) {
       {"prod recover 40+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
       {"prod recover 40+48 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 48, true>},
       // round 4: recover with fewer / other register steps
-      {"prod recover 40+24 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 24, true>},
-      {"prod recover 40+16 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 16, true>},
-      {"prod recover 32+32 rpf", qfec::phase_xor_kernel<10, true, false, false, 1, 32, 256, false, true, true, false, true, 32, true>},
+      {"prod recover 40+32 rpf early", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true, true>},
       {"prod recover 40+32 rpf again", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true>},
+      {"prod recover 40+32 rpf early again", qfec::phase_xor_kernel<10, true, false, false, 1, 40, 256, false, true, true, false, true, 32, true, true>},
       {"prod 256 x 40+56", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 56>},
       {"prod 256 x 40+48", qfec::phase_xor_kernel<10, false, false, false, 1, 40, 256, false, true, true, false, true, 48>},
   };
