@@ -182,3 +182,33 @@ def test_service_idle_boundary_stress():
         data.close()
         par.close()
         ctx.close()
+
+
+def test_service_two_threads_two_contexts():
+    """One context per host thread (the C-ABI's threading rule), each with its
+    own resident worker: two threads flushing small batches at once, every
+    result exact on both."""
+    import threading
+    errors = []
+
+    def worker(seed):
+        try:
+            ctx = qfec.Context(0)
+            try:
+                z, want_l = _mapped_case(3, g0=80000 + 100 * seed, kmin=2, kmax=14, lmin=1,
+                                         lmax=1452, seed=seed)
+                for _ in range(60):
+                    _check(ctx, z, want_l)
+                assert ctx.debug_service()["jobs"] >= 120
+            finally:
+                ctx.close()
+        except Exception as e:  # reported on the main thread
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in (1, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
