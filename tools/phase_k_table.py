@@ -7,7 +7,7 @@ process on the same buffers.  The outputs of the two forms are compared
 byte for byte, and the round trip (revived row == lost row) is checked.
 GPU box; one JSON line per k, then a summary.
 
-  python tools/phase_k_table.py [rounds=3] [reps=8]
+  python tools/phase_k_table.py [rounds=3] [reps=8] [k,k,...]
 
 The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers.
 """
@@ -34,7 +34,8 @@ def main():
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
     out_rows = []
-    for k in (2, 4, 5, 8, 10, 16):
+    ks = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2, 4, 5, 8, 10, 16]
+    for k in ks:
         rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
         ctx.synth_fixed(rows, k, L, 0, G, 0x5EED0000 + k)
         miss = torch.from_numpy(
