@@ -1697,13 +1697,19 @@ constexpr uint32_t kPhMinPhases = 6;
 // k = 5 0.73 / 0.71, k = 8 0.79 / 0.72; recover k = 4 0.54 / 0.72, k = 5
 // 0.62 / 0.67, k = 8 0.745 / 0.740, k = 10 0.76 / 0.72 -- a phase of few
 // rows per group reads too little between its meetings.  So encode phases
-// from k = 5, recover from k = 8.  An explicit phase_min (test hook) keeps
-// the phase-count rule alone.
+// from k = 5, recover from k = 8.  And only for the templated group sizes:
+// the runtime-k phased body loses everywhere but at very large k
+// (profiles/round4/phase_k_table_nontemplated_r4o.txt, phased / one-pass:
+// encode k = 6 0.27 / 0.69, k = 9 0.63 / 0.66, k = 12 0.46 / 0.66, k = 20
+// 0.56 / 0.64, k = 33 0.77 / 0.71; recover k = 9 0.49 / 0.66, k = 33
+// 0.68 / 0.70).  An explicit phase_min (test hook) keeps the phase-count
+// rule alone.
 constexpr uint32_t kPhMinKEncode = 5, kPhMinKRecover = 8;
 
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
   if (a.ncu == 0) return false;
-  if (a.phase_min == 0 && a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode))
+  if (a.phase_min == 0 &&
+      (a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode) || phase_reg_steps(a.k) == 0))
     return false;
   const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
   // the threshold counts phases of the LDS steps alone (the measured band);

@@ -2,9 +2,10 @@
 libquic_amd/csrc/qfec_kernels.hip), through the C-ABI.
 
 Large nt batches (>= kPhMinPhases = 6 phases of CUs x 40 steps x
-floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) of k >= 5
-(encode) / k >= 8 (recover) run the phased kernel by default (round 4: below
-those group sizes the one-pass kernel is faster, tools/phase_k_table.py);
+floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) of a templated
+k >= 5 (encode) / k >= 8 (recover) run the phased kernel by default (round 4:
+below those group sizes, and at every runtime k, the one-pass kernel is
+faster, tools/phase_k_table.py);
 QFEC_ONE_PASS forces the one-pass fixed kernel, qfec_debug_phase_min (here 6,
 the default count) keeps the phase-count rule alone so every k reaches the
 phased kernel, and qfec_last_fixed_phased reports which one a call ran (every
@@ -78,11 +79,14 @@ def _run_both(ctx, rows, miss, k, L, n, ps, os_, res, strides):
     return res
 
 
-@pytest.mark.parametrize("k", [2, 4, 5, 7, 8, 10])
+@pytest.mark.parametrize("k", [2, 4, 5, 7, 8, 10, 12])
 def test_default_kernel_choice_by_group_size(ctx, k):
     """The default rule (no test hook): a batch past the phase-count threshold
     runs phased for encode from k = 5 and for recover from k = 8, one-pass
-    below (round 4's per-k table)."""
+    below -- and only at the templated group sizes (2, 4, 5, 8, 10, 16): the
+    runtime-k phased body loses to one-pass (round 4's per-k tables,
+    DESIGN.md §4)."""
+    templated = k in (2, 4, 5, 8, 10, 16)
     L = 1350
     n = 8 * phase_groups(L) + 777
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
@@ -90,9 +94,9 @@ def test_default_kernel_choice_by_group_size(ctx, k):
     out = torch.empty(n * L, dtype=torch.uint8, device=DEV)
     miss = torch.zeros(n, dtype=torch.uint8, device=DEV)
     ctx.encode(rows, k, L, n, par)
-    assert ctx.last_fixed_phased() == (1 if k >= 5 else 0)
+    assert ctx.last_fixed_phased() == (1 if templated and k >= 5 else 0)
     ctx.recover(rows, par, miss, k, L, n, out)
-    assert ctx.last_fixed_phased() == (1 if k >= 8 else 0)
+    assert ctx.last_fixed_phased() == (1 if templated and k >= 8 else 0)
     ctx.sync()
 
 
