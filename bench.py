@@ -379,6 +379,57 @@ def result_line(world, steps, warmup, elapsed, G, k, L, bytes_encode, bytes_reco
     return line
 
 
+def bench_inslot(work, steps, verify=True):
+    """the in-slot recover (qfec_recover_inslot_batch) on the
+    same rows and the same 14,850 B per group as the headline recover -- the
+    redundancy placed in each group's lost row m, so the lost packet is the
+    XOR of the k rows (one contiguous stream).  Out of place (into `out`) and
+    in place (into row m; an involution, so an even number of launches leaves
+    the redundancy there).  The rows are restored afterwards (untimed)."""
+    torch, G, k, L = work.torch, work.G, work.k, work.L
+    r3 = work.rows.view(G, k, L)
+    idx = torch.arange(G, device=work.dev)
+    m = work.miss.long()
+    lost = r3[idx, m].clone()
+    r3[idx, m] = work.par.view(G, L)  # the redundancy into the lost slot
+    work.out.fill_(0x5A)
+    work.synchronize()
+    res = {"bytes_per_launch": G * (k * L + L),
+           "note": "recover with the redundancy in the lost row: k rows read + L written per "
+                   "group, the headline recover's algorithmic bytes"}
+    for tag, out in (("out_of_place", work.out), ("in_place", None)):
+        work.ctx.recover_inslot(work.rows, work.miss, k, L, G, out)  # warm (in place: twice)
+        if out is None:
+            work.ctx.recover_inslot(work.rows, work.miss, k, L, G, out)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        ev[0].record(work.stream)
+        for i in range(steps):
+            work.ctx.recover_inslot(work.rows, work.miss, k, L, G, out)
+            ev[i + 1].record(work.stream)
+        work.synchronize()
+        us = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])) * 1e3
+        res[tag] = {"us": round(us, 2),
+                    "frac": round(res["bytes_per_launch"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                    "GiBps": round(res["bytes_per_launch"] / (us * 1e-6) / 2**30, 2),
+                    "phased": work.ctx.last_fixed_phased() == 1}
+    ok = None
+    if verify:
+        # out of place: every group's revived row; in place (even count): the
+        # redundancy is back; one more in-place call revives into the rows
+        ok = bool(torch.equal(work.out.view(G, L), lost)) and \
+            bool(torch.equal(r3[idx, m], work.par.view(G, L)))
+        work.ctx.recover_inslot(work.rows, work.miss, k, L, G, None)
+        work.synchronize()
+        ok = ok and bool(torch.equal(r3[idx, m], lost))
+    r3[idx, m] = lost  # the original rows (untimed)
+    work.synchronize()
+    del lost
+    res["verified"] = ok
+    res["kernel"] = fixed_kernel_name(k, res["out_of_place"]["phased"]) + \
+        " (in place: the INPL form, stores into row m)"
+    return res
+
+
 def measured_traffic(G, k, L, phased=False):
     """PMC bytes per encode launch (tools/pmc.sh -> profiles/traffic_latest.json),
     when that run measured this shape with the same kernel (phased or one-pass)."""
@@ -571,6 +622,9 @@ def main(argv=None):
             "note": "QFEC_ONE_PASS: the one-pass fixed kernel on the same buffers, same steps "
                     "(its rate depends on the buffers' DRAM placement, DESIGN.md §4)"}
         work.one_pass = False
+    if extras and not args.one_pass:
+        line["recover_inslot"] = bench_inslot(work, max(4, args.steps // 2 * 2),
+                                              verify=not args.no_verify)
     if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
         if line["roofline"]:  # the encode kernel against this box's measured streaming read
@@ -653,6 +707,9 @@ def line_summary(line):
     for leg in ("one_pass", "ragged", "ragged_packed"):
         if isinstance(line.get(leg), dict):
             s[leg] = {kk: line[leg].get(kk) for kk in ("encode_frac", "recover_frac")}
+    ri = line.get("recover_inslot")
+    if isinstance(ri, dict):
+        s["recover_inslot_frac"] = {kk: g(ri, kk, "frac") for kk in ("out_of_place", "in_place")}
     if isinstance(line.get("ceilings"), dict):
         s["encode_frac_of_read_ceiling"] = line["ceilings"].get("encode_frac_of_read_ceiling")
     pr = line.get("protect")

@@ -185,6 +185,24 @@ int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity
                        const uint8_t* missing_idx, uint32_t k, uint32_t L, uint64_t n_groups,
                        uint8_t* out, uint32_t flags);
 
+/* In-slot recover: the receiver has written the FEC packet's redundancy
+ * (L bytes) into row missing_idx[g] of group g -- the slot of the lost packet,
+ * where the framer would have put it -- so the lost packet is the XOR of the
+ * group's k rows.  The kernels then read ONE contiguous stream of k rows per
+ * group (qfec_recover_batch reads k-1 rows around the lost row's hole plus a
+ * separate parity stream); the same 14,850 B per group at 10 x 1350 B.
+ *   out != NULL: out[g] = XOR_i rows[g][i]; missing_idx is not read (may be
+ *                NULL); the rows are not written.  Any pointer mode (flags).
+ *   out == NULL: in place, rows[g][missing_idx[g]] receives the lost packet
+ *                (missing_idx[g] < k, else -QUIC_INVALID_FEC_DATA as
+ *                qfec_recover_batch); device pointers only.  Applying it twice
+ *                restores the redundancy.
+ * Replaces the same historical QuicFecGroup::UpdateFec + Revive as
+ * qfec_recover_batch, at the receive hook QuicConnection::ProcessValidatedPacket
+ * (src/net/quic/core/quic_connection.cc:1388-1392). */
+int qfec_recover_inslot_batch(qfec_ctx* ctx, uint8_t* rows, const uint8_t* missing_idx, uint32_t k,
+                              uint32_t L, uint64_t n_groups, uint8_t* out, uint32_t flags);
+
 /* Strided forms (padding study: row_stride >= L, group_stride >= k*row_stride,
  * parity/out strides >= L; all in bytes). */
 int qfec_encode_batch_strided(qfec_ctx* ctx, const uint8_t* rows, uint32_t k, uint32_t L,
@@ -195,6 +213,10 @@ int qfec_recover_batch_strided(qfec_ctx* ctx, const uint8_t* rows, const uint8_t
                                uint64_t row_stride, uint64_t group_stride,
                                uint64_t parity_stride, uint64_t n_groups, uint8_t* out,
                                uint64_t out_stride, uint32_t flags);
+int qfec_recover_inslot_batch_strided(qfec_ctx* ctx, uint8_t* rows, const uint8_t* missing_idx,
+                                      uint32_t k, uint32_t L, uint64_t row_stride,
+                                      uint64_t group_stride, uint64_t n_groups, uint8_t* out,
+                                      uint64_t out_stride, uint32_t flags);
 
 /* ---- ragged batches (CSR) ---------------------------------------------- */
 /* Group g holds packets p in [grp_ptr[g], grp_ptr[g+1]) (1..255 of them);
@@ -414,8 +436,12 @@ int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
  * without work (or before a phased launch of its context) and is relaunched
  * by the next such batch.  on = 1 / 0
  * enables / disables it (0 also makes a running worker leave; -1 leaves the
- * setting); stats (may be NULL) receives {worker launches, jobs finished,
- * worker alive}.  Test / measurement hook; the service is on by default. */
+ * setting; 2 enables it and writes the NEXT job's ring entry with a wrong job
+ * number -- a malformed ring, whose job must fail with QFEC_ERR_INTERNAL and
+ * turn the service off rather than report stale output); stats (may be NULL)
+ * receives {worker launches, jobs finished, worker alive}.  Test /
+ * measurement hook; the service is on by default.  Any failed service job
+ * turns the service off for the context (small batches then launch). */
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */

@@ -153,7 +153,10 @@ def build_tools(force: bool = False) -> list:
 # (ThreadSanitizer as well for the group test: worker threads fill groups
 # whose arena slabs outlive them.)
 SAN_TESTS = [("san", "test_quic_fec_group"), ("san", "test_quic_fec_connection"),
-             ("tsan", "test_quic_fec_group")]
+             ("tsan", "test_quic_fec_group"), ("san", "test_layout_guard")]
+# per-test defines: the layout-guard test plays a caller built against a
+# different quic_fec_group.h
+SAN_DEFINES = {"test_layout_guard": ["-DQFEC_TEST_STALE_LAYOUT"]}
 HOST_SRCS = ["quic_fec_group.cc", "quic_fec_wire.cc", "quic_fec_connection.cc"]
 SAN_FLAGS = {
     "san": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
@@ -181,8 +184,13 @@ def build_cpp_sanitized(force: bool = False) -> list:
                 _run(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "include"),
                       "-c", c, "-o", o])
                 objs.append(o)
+            # the test TU alone gets its defines; the host sources build as shipped
+            tobj = os.path.join(bdir, f"{kind}_{name}.o")
+            _run(["g++", "-std=c++17", "-Wall", *flags, *SAN_DEFINES.get(name, []),
+                  "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-I", os.path.join(ROOT, "oracle"),
+                  "-c", src, "-o", tobj])
             _run(["g++", "-std=c++17", "-Wall", *flags, "-I", os.path.join(ROOT, "include"),
-                  "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), src, *hosts, *objs,
+                  "-I", CSRC, "-I", os.path.join(ROOT, "oracle"), tobj, *hosts, *objs,
                   "-lpthread", "-o", out])
         outs.append(out)
     return outs

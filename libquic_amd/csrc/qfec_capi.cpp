@@ -113,9 +113,14 @@ struct qfec_ctx {
   uint64_t async_seq = 0;
   uint64_t last_ticket = 0;  // of the last ragged mapped call, 0 if it ran synchronously
   // results of async ops finished by a call other than their owner's (a slot
-  // reused, a synchronous call draining the slots), kept for
-  // qfec_complete_ticket: each op's code reaches its own caller only
-  std::map<uint64_t, int> finished;
+  // reused, a synchronous call draining the slots, qfec_complete), kept for
+  // qfec_complete_ticket: each op's code reaches its own ticket's caller;
+  // `reported` once qfec_complete has returned it (it reports each code once)
+  struct Kept {
+    int code = QFEC_OK;
+    bool reported = false;
+  };
+  std::map<uint64_t, Kept> finished;
   // small-batch service (qfec_internal.h SvcJob): a resident worker on a
   // stream of its own takes mapped async batches of <= kSvcGroups groups from
   // a ring in host-mapped memory -- no kernel launch per batch
@@ -128,6 +133,7 @@ struct qfec_ctx {
   uint32_t svc_seq = 0;
   uint64_t svc_launches = 0;
   bool svc_on = true;  // test hook qfec_debug_service
+  bool svc_poison_next = false;  // test hook: the next job's ring entry malformed
   // device scratch of the host-pointer xor / protection / entropy calls:
   // grow-only buffers kept for the context's life (no allocation per call)
   std::vector<void*> scratch_p;
@@ -285,7 +291,9 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   j.recover = recover ? 1u : 0u;
   j.flag_slot = (uint32_t)slot;
   j.token = token;
-  __atomic_store_n(&j.seq, seq, __ATOMIC_RELEASE);
+  const uint32_t wseq = ctx->svc_poison_next ? seq ^ 0x80000000u : seq;  // test hook
+  ctx->svc_poison_next = false;
+  __atomic_store_n(&j.seq, wseq, __ATOMIC_RELEASE);
   ctx->svc_published += a.n_groups;
   __atomic_store_n(&sh->pub_end, ctx->svc_published, __ATOMIC_RELEASE);
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
@@ -320,6 +328,10 @@ int wait_flag_svc(qfec_ctx* ctx, int si, uint32_t token) {
       const hipError_t q = hipStreamQuery(ctx->svc_stream);
       if (q == hipSuccess) {
         if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
+        if (__atomic_load_n(&ctx->svc_sh->fault, __ATOMIC_ACQUIRE) != 0u)
+          return fail(ctx, QFEC_ERR_INTERNAL,
+                      "small-batch service: a published group lies in no ring entry (job "
+                      "withheld)");
         return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service left without finishing a job");
       }
       if (q != hipErrorNotReady) QFEC_HIP(ctx, q);
@@ -332,6 +344,25 @@ void stop_service(qfec_ctx* ctx) {
   __atomic_store_n(&ctx->svc_sh->quit, 1u, __ATOMIC_SEQ_CST);
   (void)hipStreamSynchronize(ctx->svc_stream);
   __atomic_store_n(&ctx->svc_sh->alive, 0u, __ATOMIC_SEQ_CST);
+}
+
+// A service job failed (no token: the worker faulted, missed a ring entry or
+// left): stop every worker, rewind the ring to what the workers finished and
+// turn the service off for this context -- the failed job's slot is handed
+// to the next call, so no later worker may run it over the reused tables.
+// The context's small batches then take the direct path.
+void svc_abandon(qfec_ctx* ctx) {
+  ctx->svc_on = false;
+  if (!ctx->svc_sh) return;
+  stop_service(ctx);
+  for (uint32_t i = 0; i < qfec::kSvcRing; ++i)
+    __atomic_store_n(&ctx->svc_ring[i].seq, 0xFFFFFFFFu, __ATOMIC_RELEASE);
+  const uint64_t consumed = __atomic_load_n(&ctx->svc_sh->consumed, __ATOMIC_ACQUIRE);
+  ctx->svc_published = consumed;
+  ctx->svc_seq = (uint32_t)__atomic_load_n(&ctx->svc_sh->jobs, __ATOMIC_ACQUIRE);
+  __atomic_store_n(&ctx->svc_sh->pub_end, consumed, __ATOMIC_RELEASE);
+  __atomic_store_n(&ctx->svc_sh->fault, 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
 }
 
 // Wait for a launch_ragged_latency kernel by spinning on its host-mapped
@@ -364,11 +395,26 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   if (!op.live) return QFEC_OK;
   Slot& s = ctx->slots[si];
   if (op.svc) {
-    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token)
-      return QFEC_PENDING;
+    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
+      // a worker that is gone without the token (fault, ring miss, exit)
+      // must end in an error, not QFEC_PENDING forever
+      const hipError_t q = hipStreamQuery(ctx->svc_stream);
+      if (q == hipErrorNotReady) return QFEC_PENDING;
+      if (q != hipSuccess) {
+        op.live = false;
+        svc_abandon(ctx);
+        QFEC_HIP(ctx, q);
+      }
+      // drained: the flag is final; wait_flag_svc reports a missing token
+    }
     op.live = false;
     const int wrc = wait_flag_svc(ctx, si, op.token);
-    if (wrc) return wrc;
+    if (wrc) {
+      // the job may still be published in the ring while its slot is handed
+      // to the next call: no later worker may run it
+      svc_abandon(ctx);
+      return wrc;
+    }
   } else if (op.direct) {
     if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
       const hipError_t q = hipEventQuery(s.done);
@@ -394,6 +440,13 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   return op.direct ? QFEC_OK : collect_error(ctx, s.stream, kErrSlot0 + si);
 }
 
+// Keep op `t`'s code for its ticket's qfec_complete_ticket (at most 4096
+// unclaimed codes; the oldest goes first).
+void keep_code(qfec_ctx* ctx, uint64_t t, int rc, bool reported) {
+  if (ctx->finished.size() >= 4096) ctx->finished.erase(ctx->finished.begin());
+  ctx->finished[t] = qfec_ctx::Kept{rc, reported};
+}
+
 // Finish the op of slot `si` (if live) for a caller that does not own it: its
 // code is kept for its owner's qfec_complete_ticket.
 void retire_async_op(qfec_ctx* ctx, int si) {
@@ -401,8 +454,7 @@ void retire_async_op(qfec_ctx* ctx, int si) {
   if (!op.live) return;
   const uint64_t t = op.seq;
   const int rc = complete_async_op(ctx, si, true);
-  if (ctx->finished.size() >= 4096) ctx->finished.erase(ctx->finished.begin());
-  ctx->finished[t] = rc;
+  keep_code(ctx, t, rc, false);
 }
 
 // Every outstanding op retired (synchronous calls that use the slots).
@@ -415,18 +467,23 @@ void drain_async(qfec_ctx* ctx) {
 // one is still running: the ones before it are finished).
 int complete_async(qfec_ctx* ctx, bool wait) {
   int first = QFEC_OK;
-  // ops retired by other calls report here too (then they are claimed)
-  for (const auto& f : ctx->finished)
-    if (f.second && !first) first = f.second;
-  ctx->finished.clear();
+  // ops retired by other calls report here too, once; their codes stay
+  // claimable by their tickets (QuicFecGroup::Finish on a context
+  // another caller completed)
+  for (auto& f : ctx->finished) {
+    if (f.second.code && !f.second.reported && !first) first = f.second.code;
+    f.second.reported = true;
+  }
   for (;;) {
     int si = -1;
     for (int i = 0; i < kSlots; ++i)
       if (ctx->async_ops[i].live && (si < 0 || ctx->async_ops[i].seq < ctx->async_ops[si].seq))
         si = i;
     if (si < 0) return first;
+    const uint64_t t = ctx->async_ops[si].seq;
     const int rc = complete_async_op(ctx, si, wait);
     if (rc == QFEC_PENDING) return first ? first : QFEC_PENDING;
+    keep_code(ctx, t, rc, true);
     if (rc && !first) first = rc;
   }
 }
@@ -711,7 +768,10 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
       // resident small-batch worker (if any) leaves first (it holds a CU's
       // LDS; a worker of another context leaves within kSvcIdleTicks, below
       // the meetings' timeout)
-      if (ctx->svc_sh && __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u) {
+      // (also when `alive` reads 0 but the worker stream still has work: a
+      // worker queued behind one that was leaving)
+      if (ctx->svc_sh && (__atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ||
+                          hipStreamQuery(ctx->svc_stream) == hipErrorNotReady)) {
         stop_service(ctx);
         __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
       }
@@ -975,7 +1035,7 @@ int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait) {
   if (rc) return rc;
   auto f = ctx->finished.find(ticket);
   if (f != ctx->finished.end()) {
-    rc = f->second;
+    rc = f->second.code;
     ctx->finished.erase(f);
     return rc;
   }
@@ -1068,6 +1128,45 @@ int qfec_recover_batch(qfec_ctx* ctx, const uint8_t* rows, const uint8_t* parity
                        uint8_t* out, uint32_t flags) {
   return qfec_recover_batch_strided(ctx, rows, parity, missing_idx, k, L, L, (uint64_t)k * L, L,
                                     n_groups, out, L, flags);
+}
+
+// In-slot recover: the redundancy sits in the lost
+// packet's row, so the lost packet is the XOR of the k rows -- the encode
+// kernels over one contiguous stream; in place (out == NULL) the kernels
+// write each group's result into its row missing_idx[g].
+int qfec_recover_inslot_batch_strided(qfec_ctx* ctx, uint8_t* rows, const uint8_t* missing_idx,
+                                      uint32_t k, uint32_t L, uint64_t row_stride,
+                                      uint64_t group_stride, uint64_t n_groups, uint8_t* out,
+                                      uint64_t out_stride, uint32_t flags) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (out) return qfec_encode_batch_strided(ctx, rows, k, L, row_stride, group_stride, n_groups,
+                                            out, out_stride, flags);
+  if ((rc = check_fixed(ctx, k, L, row_stride, group_stride, L, L))) return rc;
+  if (n_groups == 0) return QFEC_OK;
+  if (!rows || !missing_idx) return fail(ctx, QFEC_ERR_INTERNAL, "null buffer");
+  if (flags & (QFEC_PTR_HOST | QFEC_PTR_MAPPED))
+    return fail(ctx, QFEC_ERR_INTERNAL,
+                "in-slot recover in place: device pointers only (pass out for host memory)");
+  qfec::FixedArgs a{};
+  a.rows = rows;
+  a.out = rows;  // unused: every output row is a row of `rows`
+  a.inplace_missing = missing_idx;
+  a.row_stride = row_stride;
+  a.group_stride = group_stride;
+  a.parity_stride = L;
+  a.out_stride = L;
+  a.n_groups = n_groups;
+  a.k = k;
+  a.L = L;
+  a.err = ctx->d_err;
+  return fixed_device(ctx, a, flags);
+}
+
+int qfec_recover_inslot_batch(qfec_ctx* ctx, uint8_t* rows, const uint8_t* missing_idx, uint32_t k,
+                              uint32_t L, uint64_t n_groups, uint8_t* out, uint32_t flags) {
+  return qfec_recover_inslot_batch_strided(ctx, rows, missing_idx, k, L, L, (uint64_t)k * L,
+                                           n_groups, out, L, flags);
 }
 
 // ---- ragged ---------------------------------------------------------------
@@ -1840,7 +1939,13 @@ int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_p
 
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
-  if (on >= 0) {
+  if (on == 2) {
+    // test hook: the next job's ring entry is written with
+    // a wrong job number, so the worker finds its groups in no entry
+    ctx->svc_on = true;
+    ctx->svc_poison_next = true;
+    if (ctx->svc_sh) __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
+  } else if (on >= 0) {
     ctx->svc_on = on != 0;
     if (!ctx->svc_on) {
       stop_service(ctx);  // a resident worker leaves at once

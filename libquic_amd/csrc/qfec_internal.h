@@ -53,6 +53,10 @@ struct FixedArgs {
   // test hook (qfec_debug_phase_regsteps): phased launches without the
   // register-held steps (the A/B of DESIGN.md §4's per-k table)
   uint32_t no_regsteps = 0;
+  // in-slot recover written in place (qfec_recover_inslot_batch with out ==
+  // NULL; encode form, parity == nullptr): group g's output row is its own
+  // row inplace_missing[g], which holds the redundancy on entry; nullptr: out
+  const uint8_t* inplace_missing = nullptr;
 };
 
 // True if launch_fixed(a, nontemporal, ...) runs the phased kernel.
@@ -100,9 +104,13 @@ struct SvcJob {
 struct SvcShared {
   uint64_t pub_end;   // host: groups published
   uint64_t consumed;  // worker: groups finished (a new worker starts here)
-  uint32_t alive;     // host: 1 when it launches a worker; worker: 0 on its way out
+  uint32_t alive;     // host: 1 when it launches a worker; worker: 1 when it starts,
+                      // 0 on its way out
   uint32_t quit;      // host: exit now (context destroyed)
   uint64_t jobs;      // worker: jobs finished (stats)
+  uint32_t fault;     // worker: a published group lay in no ring entry; it left
+                      // without finishing (no token for any job of that turn)
+  uint32_t pad;
 };
 constexpr uint32_t kSvcRing = 8;
 hipError_t launch_ragged_service(SvcShared* sh, const SvcJob* ring, uint32_t* flags,

@@ -93,18 +93,94 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
   return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
 }
 
+// N rows r .. r+N-1 of a group, all N loads in flight before the first XOR
+// (recover: row m is the parity row `par`).  The runtime-k bodies use it for
+// their full batches AND their remainder (a switch on k - r picks N): round
+// 4's remainder was a rolled loop, one load in flight per lane, which made
+// the runtime-k phased kernel 1.1-2.5x slower than one-pass
+// (profiles/round4/phase_k_table_nontemplated_r4o.txt, k = 6: 0.27 vs 0.69).
+template <int N, bool RECOVER, bool NT>
+__device__ __forceinline__ void xor_rows_n(u32x4& acc, const uint8_t* src, uint64_t row_stride,
+                                           uint32_t r, uint32_t m, const uint8_t* par) {
+  u32x4 v[N];
+#pragma unroll
+  for (int w = 0; w < N; ++w) {
+    const uint8_t* q = (RECOVER && r + (uint32_t)w == m) ? par : src + (uint64_t)(r + w) * row_stride;
+    v[w] = ld16t<NT>(q);
+  }
+#pragma unroll
+  for (int w = 0; w < N; ++w) acc ^= v[w];
+}
+
+// Rows [0, k) of a group at runtime k: batches of B loads, then the
+// remainder as one batch of k mod B (a wave-uniform switch).
+template <int B, bool RECOVER, bool NT>
+__device__ __forceinline__ void xor_rows_rt(u32x4& acc, const uint8_t* src, uint64_t row_stride,
+                                            uint32_t k, uint32_t m, const uint8_t* par) {
+  static_assert(B == 8 || B == 16, "batch of 8 or 16 rows");
+  uint32_t r = 0;
+  for (; r + B <= k; r += B) xor_rows_n<B, RECOVER, NT>(acc, src, row_stride, r, m, par);
+  switch (k - r) {
+#define QFEC_REM(N)                                                 \
+  case N:                                                           \
+    xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
+    break;
+    QFEC_REM(1) QFEC_REM(2) QFEC_REM(3) QFEC_REM(4) QFEC_REM(5) QFEC_REM(6) QFEC_REM(7)
+#undef QFEC_REM
+    default:
+      break;
+  }
+  if constexpr (B == 16) {
+    switch (k - r) {
+#define QFEC_REM(N)                                                 \
+  case N:                                                           \
+    xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
+    break;
+      QFEC_REM(8) QFEC_REM(9) QFEC_REM(10) QFEC_REM(11) QFEC_REM(12) QFEC_REM(13) QFEC_REM(14)
+      QFEC_REM(15)
+#undef QFEC_REM
+      default:
+        break;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Fixed shape, L >= 16.
 // ---------------------------------------------------------------------------
 // SM (recover, gpb <= 8): lost-slot indices by scalar loads, see below.
-template <int KC, bool RECOVER, bool NT, bool SM, bool XCD = false>
+// INPL (encode form only): the in-slot recover written in place -- the
+// group's output row is its own row missing[g] (which held the redundancy);
+// a barrier between the loads and the stores keeps a wave from overwriting
+// the bytes the overlapping last window of a neighbouring wave still reads.
+template <int KC, bool RECOVER, bool NT, bool SM, bool XCD = false, bool INPL = false>
 __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t C,
                                                            uint32_t gpb) {
+  static_assert(!(INPL && RECOVER), "in place: the encode form over the k rows");
   const uint32_t tid = threadIdx.x;
   const uint32_t gl = tid / C;  // group within the workgroup
   const uint32_t t = tid - gl * C;
   const uint64_t gb = (uint64_t)(XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) * gpb;
   const uint64_t g = gb + gl;
+  if constexpr (INPL) {
+    // no early return before the barrier: every wave reaches it
+    const bool on = gl < gpb && g < a.n_groups;
+    const uint64_t gg = on ? g : 0;
+    const uint32_t off = min(t * 16u, a.L - 16u);
+    const uint8_t* src = a.rows + gg * a.group_stride + off;
+    const uint32_t k = KC > 0 ? (uint32_t)KC : a.k;
+    const uint32_t m = on ? (uint32_t)a.inplace_missing[gg] : 0u;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    if constexpr (KC > 0) {
+      xor_rows_n<(KC > 0 ? KC : 1), false, NT>(acc, src, a.row_stride, 0, 0, nullptr);
+    } else {
+      xor_rows_rt<8, false, NT>(acc, src, a.row_stride, k, 0, nullptr);
+    }
+    __syncthreads();
+    if (on && m < k) st16t<NT>(const_cast<uint8_t*>(src) + (uint64_t)m * a.row_stride, acc);
+    if (on && m >= k && t == 0) atomicOr(a.err, kErrMissingIndex);
+    return;
+  }
   uint64_t mw0 = 0, mw1 = 0;
   if constexpr (RECOVER) {
     // SM: the block's lost-slot indices by (at most) two SCALAR loads of the
@@ -146,36 +222,14 @@ __global__ __launch_bounds__(kBlock) void fixed_xor_kernel(FixedArgs a, uint32_t
         acc ^= ld16t<NT>(p);
       }
     } else {
-      uint32_t i = 0;
-      for (; i + 8 <= k; i += 8) {
-        u32x4 v[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) {
-          const uint8_t* p = (i + u == m) ? par : src + (i + u) * a.row_stride;
-          v[u] = ld16t<NT>(p);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) acc ^= v[u];
-      }
-      for (; i < k; ++i) {
-        const uint8_t* p = (i == m) ? par : src + i * a.row_stride;
-        acc ^= ld16t<NT>(p);
-      }
+      xor_rows_rt<8, true, NT>(acc, src, a.row_stride, k, m, par);
     }
   } else {
     if constexpr (KC > 0) {
 #pragma unroll
       for (uint32_t i = 0; i < (uint32_t)KC; ++i) acc ^= ld16t<NT>(src + i * a.row_stride);
     } else {
-      uint32_t i = 0;
-      for (; i + 8 <= k; i += 8) {
-        u32x4 v[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) v[u] = ld16t<NT>(src + (i + u) * a.row_stride);
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) acc ^= v[u];
-      }
-      for (; i < k; ++i) acc ^= ld16t<NT>(src + i * a.row_stride);
+      xor_rows_rt<8, false, NT>(acc, src, a.row_stride, k, 0, nullptr);
     }
   }
   st16t<NT>(a.out + g * a.out_stride + off, acc);
@@ -280,9 +334,10 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
           bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0, bool RPF = false,
-          bool RPFE = false>
+          bool RPFE = false, bool INPL = false>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
+  static_assert(!(INPL && RECOVER), "in place: the encode form over the k rows");
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
   static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
   static_assert(RS == 0 || (KC > 0 && kPhU == 1 && !XCDW && RS <= 64 &&
@@ -434,26 +489,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
           for (int r = 0; r < KC; ++r) acc[u] ^= v[u][r];
       } else {
+        // runtime k (> 16: every k up to 16 is templated): batches of 16
+        // loads in flight, the remainder as one batch (xor_rows_rt)
 #pragma unroll
         for (int u = 0; u < kPhU; ++u) {
           const uint64_t g = gidx(i + u);
           const uint8_t* par = RECOVER ? a.parity + (lane_on && g < a.n_groups ? g : 0) * a.parity_stride + off
                                        : nullptr;
-          uint32_t r = 0;
-          for (; r + 8 <= k; r += 8) {
-            u32x4 v[8];
-#pragma unroll
-            for (uint32_t w = 0; w < 8; ++w) {
-              const uint8_t* q = (RECOVER && r + w == m[u]) ? par : src[u] + (r + w) * a.row_stride;
-              v[w] = ld16t<NTLD>(q);
-            }
-#pragma unroll
-            for (uint32_t w = 0; w < 8; ++w) acc[u] ^= v[w];
-          }
-          for (; r < k; ++r) {
-            const uint8_t* q = (RECOVER && r == m[u]) ? par : src[u] + r * a.row_stride;
-            acc[u] ^= ld16t<NTLD>(q);
-          }
+          xor_rows_rt<16, RECOVER, NTLD>(acc[u], src[u], a.row_stride, k, m[u], par);
         }
       }
       if constexpr (RECOVER) {
@@ -531,19 +574,41 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
       if (((bad_lo | bad_hi) != 0u || rbad) && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
     phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
+    // INPL: the output row of group g is its own row missing[g] (the in-slot
+    // recover written in place; every read of the phase is done by now, and
+    // no other workgroup reads this group)
+    bool ibad = false;
+    auto dst = [&](uint64_t g, bool& on) -> uint8_t* {
+      if constexpr (INPL) {
+        const uint32_t m = a.inplace_missing[g];
+        if (m >= k) {
+          ibad = ibad || on;
+          on = false;
+        }
+        return const_cast<uint8_t*>(a.rows) + g * a.group_stride + (uint64_t)m * a.row_stride + off;
+      } else {
+        return a.out + g * a.out_stride + off;
+      }
+    };
 #pragma unroll 4
     for (int i = 0; i < STEPS; ++i) {
       const uint64_t g = gidx(i);
       const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
-      if (lane_on && g < a.n_groups && !skip && i < NL)
-        st16t<true>(a.out + g * a.out_stride + off, s_par[i][tid]);
+      bool on = lane_on && g < a.n_groups && !skip && i < NL;
+      uint8_t* d = dst(on ? g : 0, on);
+      if (on) st16t<true>(d, s_par[i][tid]);
     }
     if constexpr (RS > 0) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = gidx(STEPS + j);
-        if ((ron[j / 32] >> (j % 32)) & 1u) st16t<true>(a.out + g * a.out_stride + off, racc[j]);
+        bool on = ((ron[j / 32] >> (j % 32)) & 1u) != 0u;
+        uint8_t* d = dst(on ? g : 0, on);
+        if (on) st16t<true>(d, racc[j]);
       }
+    }
+    if constexpr (INPL) {
+      if (ibad && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
     if constexpr (MEET2) phase_meet(a.phase_sync, 2u * p + 2u);
   }
@@ -570,6 +635,16 @@ __global__ __launch_bounds__(kBlock) void fixed_small_kernel(FixedArgs a) {
       if (i != m) acc ^= src[i * a.row_stride];
   } else {
     for (uint32_t i = 0; i < a.k; ++i) acc ^= src[i * a.row_stride];
+  }
+  if (a.inplace_missing) {
+    // in-slot recover in place: this lane alone reads and writes byte j
+    const uint32_t m = a.inplace_missing[g];
+    if (m >= a.k) {
+      if (j == 0) atomicOr(a.err, kErrMissingIndex);
+      return;
+    }
+    const_cast<uint8_t*>(src)[(uint64_t)m * a.row_stride] = acc;
+    return;
   }
   a.out[g * a.out_stride + j] = acc;
 }
@@ -1434,6 +1509,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
     // order, so the next job's number is the count finished
     s_from = svc_load64(&sh->consumed);
     s_job = (uint32_t)svc_load64(&sh->jobs);
+    // running: a worker queued behind one that cleared `alive` on its way out
+    // says so itself (the host then stops it before a phased launch)
+    __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   for (;;) {
@@ -1472,24 +1550,37 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     const uint64_t from = s_from, to = s_to;
     uint32_t j = s_job;  // wave-uniform: the job holding the next group
+    bool miss = false;
     for (uint64_t gi = from + wv; gi < to; gi += kSvcWaves) {
       const SvcJob* jb = ring + (j % kSvcRing);
-      uint32_t hops = 0;  // bounded: a group outside every ring entry is skipped
+      uint32_t hops = 0;  // bounded: a group outside every ring entry
       while ((jb->seq != j || gi < jb->start || gi >= jb->start + jb->a.n_groups) &&
              hops < kSvcRing) {
         ++j;
         ++hops;
         jb = ring + (j % kSvcRing);
       }
-      if (hops == kSvcRing) continue;  // never with a well-formed ring
+      if (hops == kSvcRing) {  // a malformed ring: nothing of this turn is done
+        miss = true;
+        break;
+      }
       const uint64_t g = gi - jb->start;
       if (jb->recover)
         window_group<true, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
       else
         window_group<false, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
     }
+    if (miss && lane == 0u) s_exit = 1u;  // benign race: every writer stores 1
     __threadfence_system();  // every output visible before any token
     __syncthreads();
+    if (s_exit) {
+      // ring miss: latch the fault and leave WITHOUT a
+      // token -- the host's wait sees the stream drained and the fault word
+      // and fails the job instead of reporting stale output as finished
+      if (tid == 0)
+        __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
     if (tid == 0) {
       // every job published below `to` is finished (a ring entry not yet
       // rewritten for job jj still carries job jj - kSvcRing: its seq says so)
@@ -1614,66 +1705,62 @@ __global__ __launch_bounds__(kBlock) void synth_ragged_kernel(uint8_t* bytes,
   }
 }
 
-template <bool RECOVER, bool NT, bool SM>
+// Every group size up to 16 is templated (round 5; round 4 had 2, 4, 5, 8,
+// 10, 16 and ran the others through the runtime-k bodies).
+#define QFEC_K_ALL(X) \
+  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
+template <bool RECOVER, bool NT, bool SM, bool INPL = false>
 hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t blocks,
                           hipStream_t s) {
   switch (a.k) {
-#define QFEC_K_CASE(KV)                                                                     \
-  case KV:                                                                                   \
-    hipLaunchKernelGGL((fixed_xor_kernel<KV, RECOVER, NT, SM>), dim3((uint32_t)blocks),      \
-                       dim3(kBlock), 0, s, a, C, gpb);                                       \
+#define QFEC_K_CASE(KV)                                                                       \
+  case KV:                                                                                     \
+    hipLaunchKernelGGL((fixed_xor_kernel<KV, RECOVER, NT, SM, false, INPL>),                   \
+                       dim3((uint32_t)blocks), dim3(kBlock), 0, s, a, C, gpb);                 \
     break;
-    QFEC_K_CASE(2)
-    QFEC_K_CASE(4)
-    QFEC_K_CASE(5)
-    QFEC_K_CASE(8)
-    QFEC_K_CASE(10)
-    QFEC_K_CASE(16)
+    QFEC_K_ALL(QFEC_K_CASE)
 #undef QFEC_K_CASE
     default:
-      hipLaunchKernelGGL((fixed_xor_kernel<0, RECOVER, NT, SM>), dim3((uint32_t)blocks),
-                         dim3(kBlock), 0, s, a, C, gpb);
+      hipLaunchKernelGGL((fixed_xor_kernel<0, RECOVER, NT, SM, false, INPL>),
+                         dim3((uint32_t)blocks), dim3(kBlock), 0, s, a, C, gpb);
   }
   return hipGetLastError();
 }
 
 // Register-held steps per phase for a templated group size (0: none): every
 // templated k takes kPhRegSteps (round 4; round 3 had
-// them for k = 10 only).  Non-templated k run the LDS steps alone.
+// them for k = 10 only; round 5 templates every k up to 16).  Larger k run
+// the runtime-k body with the LDS steps alone.
 __host__ __device__ constexpr uint32_t phase_reg_steps(uint32_t k) {
-  return (k == 2u || k == 4u || k == 5u || k == 8u || k == 10u || k == 16u) ? (uint32_t)kPhRegSteps
-                                                                            : 0u;
+  return (k >= 2u && k <= 16u) ? (uint32_t)kPhRegSteps : 0u;
 }
 
-template <bool RECOVER>
+template <bool RECOVER, bool INPL = false>
 hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t grid,
                           uint32_t nphase, hipStream_t s) {
   const bool rs = a.no_regsteps == 0u;
   switch (a.k) {
     // templated k: kPhRegSteps more steps per phase held in registers after
     // the LDS steps (recover: their parity rows first, RPF), or without them
-    // (test hook)
+    // (test hook; not for the in-place form)
 #define QFEC_K_CASE(KV)                                                                        \
   case KV:                                                                                      \
-    if (rs)                                                                                     \
+    if (rs || INPL)                                                                             \
       hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER, false, false, kPhUDefault, kPhSteps,    \
                                            kBlock, false, true, true, false, true, kPhRegSteps, \
-                                           true>),                                              \
+                                           true, false, INPL>),                                 \
                          dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);                    \
     else                                                                                        \
       hipLaunchKernelGGL((phase_xor_kernel<KV, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C, \
                          gpb, nphase);                                                          \
     break;
-    QFEC_K_CASE(2)
-    QFEC_K_CASE(4)
-    QFEC_K_CASE(5)
-    QFEC_K_CASE(8)
-    QFEC_K_CASE(10)
-    QFEC_K_CASE(16)
+    QFEC_K_ALL(QFEC_K_CASE)
 #undef QFEC_K_CASE
     default:
-      hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER>), dim3(grid), dim3(kBlock), 0, s, a, C,
-                         gpb, nphase);
+      hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
+                                           false, true, true, false, true, 0, false, false, INPL>),
+                         dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
   }
   return hipGetLastError();
 }
@@ -1697,19 +1784,19 @@ constexpr uint32_t kPhMinPhases = 6;
 // k = 5 0.73 / 0.71, k = 8 0.79 / 0.72; recover k = 4 0.54 / 0.72, k = 5
 // 0.62 / 0.67, k = 8 0.745 / 0.740, k = 10 0.76 / 0.72 -- a phase of few
 // rows per group reads too little between its meetings.  So encode phases
-// from k = 5, recover from k = 8.  And only for the templated group sizes:
-// the runtime-k phased body loses everywhere but at very large k
-// (profiles/round4/phase_k_table_nontemplated_r4o.txt, phased / one-pass:
-// encode k = 6 0.27 / 0.69, k = 9 0.63 / 0.66, k = 12 0.46 / 0.66, k = 20
-// 0.56 / 0.64, k = 33 0.77 / 0.71; recover k = 9 0.49 / 0.66, k = 33
-// 0.68 / 0.70).  An explicit phase_min (test hook) keeps the phase-count
-// rule alone.
+// from k = 5, recover from k = 8.  Round 4 phased only the templated k: the
+// runtime-k phased body then loaded the rows past the last batch of 8 one at
+// a time (profiles/round4/phase_k_table_nontemplated_r4o.txt: k = 6 0.27 vs
+// 0.69 one-pass); round 5 templates every k up to 16 and gives the runtime
+// body (k > 16) batches of 16 with a one-batch remainder (xor_rows_rt), so
+// the rule is by k alone again (tools/phase_k_table.py).  An
+// explicit phase_min (test hook) keeps the phase-count rule alone.
 constexpr uint32_t kPhMinKEncode = 5, kPhMinKRecover = 8;
 
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
   if (a.ncu == 0) return false;
   if (a.phase_min == 0 &&
-      (a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode) || phase_reg_steps(a.k) == 0))
+      a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode))
     return false;
   const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
   // the threshold counts phases of the LDS steps alone (the measured band);
@@ -1718,7 +1805,8 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   const uint64_t np = (a.n_groups + per - 1) / per;
   if (np < (a.phase_min ? a.phase_min : kPhMinPhases) || np > 0xFFFFFFFFull) return false;
   const uint64_t per_l =
-      (uint64_t)wg * (kPhSteps + (a.no_regsteps ? 0u : phase_reg_steps(a.k))) * gpb;
+      (uint64_t)wg *
+      (kPhSteps + (a.no_regsteps && !a.inplace_missing ? 0u : phase_reg_steps(a.k))) * gpb;
   *grid = wg;
   *nphase = (uint32_t)((a.n_groups + per_l - 1) / per_l);
   return true;
@@ -1753,6 +1841,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
         a.missing = a0.missing + g;
       }
       a.out = a0.out + g * a0.out_stride;
+      if (a0.inplace_missing) a.inplace_missing = a0.inplace_missing + g;
       const uint64_t blocks = (a.n_groups * a.L + kBlock - 1) / kBlock;
       if (recover)
         hipLaunchKernelGGL(fixed_small_kernel<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
@@ -1769,6 +1858,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
   if (a0.phase_sync && nontemporal && phase_plan(a0, gpb, &grid, &nphase)) {
     FixedArgs a = a0;
     a.phase_steps = phase_steps_for(a0, gpb, grid, nphase);
+    if (a.inplace_missing) return launch_phase_k<false, true>(a, C, gpb, grid, nphase, s);
     return recover ? launch_phase_k<true>(a, C, gpb, grid, nphase, s)
                    : launch_phase_k<false>(a, C, gpb, grid, nphase, s);
   }
@@ -1782,9 +1872,12 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
       a.missing = a0.missing + g;
     }
     a.out = a0.out + g * a0.out_stride;
+    if (a0.inplace_missing) a.inplace_missing = a0.inplace_missing + g;
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
     hipError_t e;
-    if (recover && gpb <= 8u)
+    if (a.inplace_missing)
+      e = launch_fixed_k<false, true, false, true>(a, C, gpb, blocks, s);
+    else if (recover && gpb <= 8u)
       e = nontemporal ? launch_fixed_k<true, true, true>(a, C, gpb, blocks, s)
                       : launch_fixed_k<true, false, true>(a, C, gpb, blocks, s);
     else if (recover)

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -149,10 +150,22 @@ qfec_ctx* thread_default_ctx() {
 
 }  // namespace
 
-QuicFecGroup::QuicFecGroup(QuicFecGroupNumber fec_group_number, qfec_ctx* ctx)
-    : fec_group_number_(fec_group_number), ctx_(ctx) {}
+// Layout guard (quic_fec_group.h): the caller's tag against this library's.
+bool QuicFecGroup::StaleLayout(uint64_t tag) {
+  constexpr uint64_t kMine = QFEC_FEC_GROUP_LAYOUT_TAG;
+  if (tag == kMine) return false;
+  static std::atomic<bool> said{false};
+  if (!said.exchange(true))
+    std::fprintf(stderr,
+                 "libqfec: QuicFecGroup used by code built against a different "
+                 "quic_fec_group.h (layout tag %016llx, library %016llx): refused "
+                 "(QUIC_INTERNAL_ERROR); rebuild the caller\n",
+                 (unsigned long long)tag, (unsigned long long)kMine);
+  return true;
+}
 
-QuicFecGroup::~QuicFecGroup() {
+void QuicFecGroup::ReleaseStorage() {
+  if (StaleLayout()) return;  // nothing of a foreign layout is touched
   for (Span& sp : payloads_) ArenaFree(&sp);
   ArenaFree(&parity_);
 }
@@ -200,13 +213,12 @@ QuicFecGroup::PacketBuffer& QuicFecGroup::PacketBuffer::operator=(PacketBuffer&&
   return *this;
 }
 
-QuicFecGroup::PacketBuffer QuicFecGroup::AllocPacketBuffer(size_t n) {
-  PacketBuffer b;
+void QuicFecGroup::AllocPacketBufferInto(size_t n, uint64_t caller_tag, PacketBuffer* b) {
+  if (StaleLayout(caller_tag) || b == nullptr) return;
   const Span sp = ArenaAlloc(n);
-  b.p_ = sp.p;
-  b.slab_ = sp.slab;
-  b.n_ = sp.p ? n : 0;
-  return b;
+  b->p_ = sp.p;
+  b->slab_ = sp.slab;
+  b->n_ = sp.p ? n : 0;
 }
 
 bool QuicFecGroup::Fold(StringPiece payload, bool completes_group, PacketBuffer* adopt,
@@ -274,11 +286,13 @@ void QuicFecGroup::MarkReceived(QuicPacketNumber n) {
 
 bool QuicFecGroup::Update(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                           StringPiece decrypted_payload) {
+  if (StaleLayout()) return false;
   return UpdateImpl(encryption_level, header, decrypted_payload, nullptr, 0);
 }
 
 bool QuicFecGroup::UpdateInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                                  PacketBuffer* buf, size_t offset, size_t len) {
+  if (StaleLayout()) return false;
   if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
     detailed_error_ = "payload outside its packet buffer";
     return false;
@@ -311,12 +325,14 @@ bool QuicFecGroup::UpdateImpl(EncryptionLevel encryption_level, const QuicPacket
 
 bool QuicFecGroup::UpdateFec(EncryptionLevel encryption_level, const QuicPacketHeader& header,
                              StringPiece redundancy) {
+  if (StaleLayout()) return false;
   return UpdateFecImpl(encryption_level, header, redundancy, nullptr, 0);
 }
 
 bool QuicFecGroup::UpdateFecInPlace(EncryptionLevel encryption_level,
                                     const QuicPacketHeader& header, PacketBuffer* buf,
                                     size_t offset, size_t len) {
+  if (StaleLayout()) return false;
   if (buf == nullptr || buf->empty() || offset > buf->size() || len > buf->size() - offset) {
     detailed_error_ = "redundancy outside its packet buffer";
     return false;
@@ -363,11 +379,12 @@ QuicPacketCount QuicFecGroup::NumMissingPackets() const {
   return (max_protected_packet_ - min_protected_packet_ + 1) - num_received_;
 }
 
-bool QuicFecGroup::CanRevive() const { return NumMissingPackets() == 1; }
+bool QuicFecGroup::CanRevive() const { return !StaleLayout() && NumMissingPackets() == 1; }
 
-bool QuicFecGroup::IsFinished() const { return NumMissingPackets() == 0; }
+bool QuicFecGroup::IsFinished() const { return !StaleLayout() && NumMissingPackets() == 0; }
 
 bool QuicFecGroup::IsWaitingForPacketBefore(QuicPacketNumber num) const {
+  if (StaleLayout()) return false;
   // Entire range is larger than the threshold.
   if (min_protected_packet_ != kInvalidPacketNumber && min_protected_packet_ >= num) return false;
   // The group is anchored at fec_group_number_: nothing below it is protected.
@@ -382,6 +399,7 @@ int QuicFecGroup::EnsureParity() const {
 }
 
 StringPiece QuicFecGroup::PayloadParity() const {
+  if (StaleLayout()) return StringPiece();
   if (unkept_payload_) {
     detailed_error_ = "finished group of 256 payloads: its accumulator was not kept";
     return StringPiece();
@@ -391,6 +409,7 @@ StringPiece QuicFecGroup::PayloadParity() const {
 }
 
 size_t QuicFecGroup::ReviveInPlace(QuicPacketHeader* header, StringPiece* payload) {
+  if (StaleLayout()) return 0;
   if (!CanRevive()) return 0;
   QuicPacketNumber missing = kInvalidPacketNumber;
   for (QuicPacketNumber i = min_protected_packet_; i <= max_protected_packet_; ++i) {
@@ -412,6 +431,7 @@ size_t QuicFecGroup::ReviveInPlace(QuicPacketHeader* header, StringPiece* payloa
 }
 
 size_t QuicFecGroup::Revive(QuicPacketHeader* header, char* decrypted_payload, size_t len) {
+  if (StaleLayout()) return 0;
   if (!CanRevive()) return 0;
   if (EnsureParity() != QFEC_OK) return 0;
   if (payload_parity_len_ > len) {
@@ -447,6 +467,7 @@ void QuicFecGroup::LaunchTables::Clear() {
 }
 
 bool QuicFecGroup::LaunchTables::Append(QuicFecGroup* g) {
+  if (StaleLayout(layout_tag) || (g && g->StaleLayout())) return false;
   if (!g || !g->dirty_) return true;
   if (g->lens_.empty()) {  // only empty payloads folded: parity is empty
     g->payload_parity_len_ = 0;
@@ -475,8 +496,18 @@ bool QuicFecGroup::LaunchTables::Append(QuicFecGroup* g) {
 
 int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* pend,
                          bool async) {
-  // the tables built here, in one pass over the groups (the batcher builds
-  // them as groups are queued instead)
+  if (pend == nullptr || StaleLayout(pend->layout_tag)) return QFEC_ERR_INTERNAL;
+  for (QuicFecGroup* g : groups)
+    if (g && g->StaleLayout()) {  // refused whole: no group of it is launched
+      pend->ctx = nullptr;
+      pend->launched.clear();
+      pend->plen.clear();
+      pend->live = false;
+      pend->ticket = 0;
+      return pend->rc = QFEC_ERR_INTERNAL;
+    }
+  // the tables built here, in one pass over the groups (a thread-local table
+  // set, cleared per launch with its capacity kept)
   static thread_local LaunchTables t;
   t.Clear();
   const auto t0 = std::chrono::steady_clock::now();
@@ -498,6 +529,9 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups
 }
 
 int QuicFecGroup::Launch(qfec_ctx* ctx, LaunchTables* t, Pending* pend, bool async) {
+  if (t == nullptr || pend == nullptr || StaleLayout(t->layout_tag) ||
+      StaleLayout(pend->layout_tag))
+    return QFEC_ERR_INTERNAL;
   const auto t0 = std::chrono::steady_clock::now();
   // reset, keeping the vectors' capacity (a batcher's Pending is reused every
   // loop turn: no large block freed and reallocated per launch)
@@ -558,6 +592,7 @@ int QuicFecGroup::Launch(qfec_ctx* ctx, LaunchTables* t, Pending* pend, bool asy
 }
 
 int QuicFecGroup::Finish(Pending* pend, bool wait) {
+  if (pend == nullptr || StaleLayout(pend->layout_tag)) return QFEC_ERR_INTERNAL;
   if (pend->live) {
     const int rc = qfec_complete_ticket(pend->ctx, pend->ticket, wait ? 1 : 0);
     if (rc == QFEC_PENDING) return QFEC_PENDING;

@@ -140,11 +140,35 @@ class QfecSmallVec {
   size_t n_ = 0, cap_ = N;
 };
 
+// Layout guard.  QuicFecGroup and the structs a caller
+// hands it are C++ objects exported from libqfec.so: a caller compiled against
+// an older quic_fec_group.h allocates them with its own size and offsets, and
+// the library's code then writes past them (round 4: a stale tool build
+// corrupted its heap).  The caller's inline constructors store a tag of the
+// layout THEY were compiled with as the objects' first word (offset 0 in any
+// version); every library entry point compares it with the library's own tag
+// and refuses a mismatch -- false / 0 / QFEC_ERR_INTERNAL, nothing touched,
+// one line on stderr -- instead of corrupting memory.  Bump the version with
+// any change to these classes' members.
+#define QFEC_FEC_GROUP_LAYOUT_VERSION 5u
+#define QFEC_FEC_GROUP_LAYOUT_TAG                                                        \
+  ((uint64_t)sizeof(::net::QuicFecGroup) |                                             \
+   ((uint64_t)alignof(::net::QuicFecGroup) << 20) |                                    \
+   ((uint64_t)(sizeof(::net::QuicFecGroup::Pending) & 1023u) << 26) |                  \
+   ((uint64_t)(sizeof(::net::QuicFecGroup::LaunchTables) & 1023u) << 36) |             \
+   ((uint64_t)(sizeof(::net::QuicFecGroup::PacketBuffer) & 1023u) << 46) |             \
+   ((uint64_t)QFEC_FEC_GROUP_LAYOUT_VERSION << 56))
+
 class QuicFecGroup {
  public:
   // `ctx` may be null: a per-thread context on device 0 is created on first use.
-  explicit QuicFecGroup(QuicFecGroupNumber fec_group_number, qfec_ctx* ctx = nullptr);
-  ~QuicFecGroup();
+  // Inline (caller-compiled): every member is initialised with the caller's
+  // own layout, and the layout tag recorded first.
+  explicit QuicFecGroup(QuicFecGroupNumber fec_group_number, qfec_ctx* ctx = nullptr)
+      : layout_tag_(QFEC_FEC_GROUP_LAYOUT_TAG), fec_group_number_(fec_group_number), ctx_(ctx) {}
+  // Inline too: the library releases the payloads only for a matching layout;
+  // the members' destructors then run with the caller's layout.
+  ~QuicFecGroup() { ReleaseStorage(); }
   QuicFecGroup(const QuicFecGroup&) = delete;
   QuicFecGroup& operator=(const QuicFecGroup&) = delete;
 
@@ -180,8 +204,13 @@ class QuicFecGroup {
     void* slab_ = nullptr;
     size_t n_ = 0;
   };
-  // n <= the arena slab size; an empty buffer when no arena memory is left.
-  static PacketBuffer AllocPacketBuffer(size_t n);
+  // n <= the arena slab size; an empty buffer when no arena memory is left
+  // (or the caller's layout does not match the library's).
+  static PacketBuffer AllocPacketBuffer(size_t n) {
+    PacketBuffer b;
+    AllocPacketBufferInto(n, QFEC_FEC_GROUP_LAYOUT_TAG, &b);
+    return b;
+  }
   // Update() for a payload at buf->data() + [offset, offset + len): on
   // success the group owns *buf (it is left empty), the payload is not copied.
   bool UpdateInPlace(EncryptionLevel encryption_level, const QuicPacketHeader& header,
@@ -226,6 +255,7 @@ class QuicFecGroup {
   // another op's of the same context) and sets every group's parity.  The
   // groups must stay alive and take no packets in between.
   struct Pending {
+    uint64_t layout_tag = QFEC_FEC_GROUP_LAYOUT_TAG;  // first: the layout guard
     qfec_ctx* ctx = nullptr;
     std::vector<QuicFecGroup*> launched;
     std::vector<uint16_t> plen;  // parity_len_out, filled at completion
@@ -236,12 +266,12 @@ class QuicFecGroup {
   static int Launch(qfec_ctx* ctx, const std::vector<QuicFecGroup*>& groups, Pending* p,
                     bool async);
 
-  // The launch's index tables, built one group at a time as groups are queued
-  // (QuicFecBatcher appends a group when the connection hands it over, while
-  // its payload addresses are still in the connection thread's caches): the
-  // launch itself then only rebases the addresses and makes the call.  A
-  // group must take no packets once appended (closed / collected groups).
+  // The launch's index tables, built in Launch one group at a time (Append)
+  // in one pass over the groups; reused across launches (cleared, capacity
+  // kept).  A group must take no packets once appended (closed / collected
+  // groups).
   struct LaunchTables {
+    uint64_t layout_tag = QFEC_FEC_GROUP_LAYOUT_TAG;  // first: the layout guard
     std::vector<QuicFecGroup*> groups;
     std::vector<uint64_t> pkt_off;     // absolute payload addresses until the launch
     std::vector<uint16_t> pkt_len;
@@ -286,6 +316,13 @@ class QuicFecGroup {
   const std::string& detailed_error() const { return detailed_error_; }
 
  private:
+  // Layout guard: true (and one line on stderr) when `tag` -- an object's
+  // first word, written by the caller's inline constructor -- is not the
+  // library's own layout tag.
+  static bool StaleLayout(uint64_t tag);
+  bool StaleLayout() const { return StaleLayout(layout_tag_); }
+  static void AllocPacketBufferInto(size_t n, uint64_t caller_tag, PacketBuffer* out);
+  void ReleaseStorage();
   bool Fold(StringPiece payload, bool completes_group, PacketBuffer* adopt = nullptr,
             size_t adopt_offset = 0);
   bool UpdateImpl(EncryptionLevel encryption_level, const QuicPacketHeader& header,
@@ -296,6 +333,13 @@ class QuicFecGroup {
   QuicPacketCount NumMissingPackets() const;
   qfec_ctx* context() const;
 
+  // FIRST data member, at offset 0 in every layout version (the guard reads it
+  // before trusting any other offset)
+  uint64_t layout_tag_;
+#ifdef QFEC_TEST_STALE_LAYOUT
+  // test only (tests/cpp/test_layout_guard.cc): a caller whose header differs
+  char stale_test_pad_[64] = {};
+#endif
   QuicFecGroupNumber fec_group_number_;
   qfec_ctx* ctx_;
   // Received packet numbers: the 256 a group can span (uint8 offset from

@@ -59,6 +59,11 @@ SIGNATURES = [
     ("qfec_recover_batch_strided", C.c_int,
      [_vp, _u8p, _u8p, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64, _u8p, C.c_uint64, C.c_uint32]),
+    ("qfec_recover_inslot_batch", C.c_int,
+     [_vp, _u8p, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint32]),
+    ("qfec_recover_inslot_batch_strided", C.c_int,
+     [_vp, _u8p, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, _u8p,
+      C.c_uint64, C.c_uint32]),
     ("qfec_encode_ragged", C.c_int,
      [_vp, _u8p, _vp, _vp, _vp, C.c_uint64, _u8p, _vp, _vp, C.c_uint32]),
     ("qfec_recover_ragged", C.c_int,
@@ -295,6 +300,24 @@ class Context:
                                                      _ptr(out), os_, fl)
         return self._check(rc)
 
+    def recover_inslot(self, rows, missing, k, L, n_groups, out=None, *, row_stride=None,
+                       group_stride=None, out_stride=None, host=False, cached=False,
+                       mapped=False, one_pass=False):
+        """In-slot recover: rows[g][missing[g]] holds the redundancy; out=None
+        writes the lost packet in place there (device pointers only)."""
+        fl = _fl(host, mapped, cached, one_pass)
+        if row_stride is None and group_stride is None and out_stride is None:
+            rc = self.lib.qfec_recover_inslot_batch(self.ctx, _ptr(rows), _ptr(missing), k, L,
+                                                    n_groups, _ptr(out), fl)
+        else:
+            rs = L if row_stride is None else row_stride
+            gs = k * rs if group_stride is None else group_stride
+            os_ = L if out_stride is None else out_stride
+            rc = self.lib.qfec_recover_inslot_batch_strided(self.ctx, _ptr(rows), _ptr(missing),
+                                                            k, L, rs, gs, n_groups, _ptr(out),
+                                                            os_, fl)
+        return self._check(rc)
+
     # -- ragged ------------------------------------------------------------
     def encode_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity_out, parity_off,
                       parity_len_out, *, host=False, mapped=False, async_=False):
@@ -413,11 +436,13 @@ class Context:
         rc = self.lib.qfec_complete_ticket(self.ctx, ticket, 1 if wait else 0)
         return rc if rc == 1 else self._check(rc)
 
-    def debug_service(self, on=None):
+    def debug_service(self, on=None, poison_next=False):
         """Small-batch service hook: on True / False enables / disables the
-        resident worker (None leaves it); returns {launches, jobs, alive}."""
+        resident worker (None leaves it); poison_next malforms the next job's
+        ring entry (test of the ring-miss path); returns {launches, jobs, alive}."""
         st = (C.c_uint64 * 3)()
-        self._check(self.lib.qfec_debug_service(self.ctx, -1 if on is None else int(bool(on)), st))
+        mode = 2 if poison_next else (-1 if on is None else int(bool(on)))
+        self._check(self.lib.qfec_debug_service(self.ctx, mode, st))
         return {"launches": st[0], "jobs": st[1], "alive": st[2]}
 
     def debug_phase_regsteps(self, on):

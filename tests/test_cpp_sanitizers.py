@@ -27,7 +27,7 @@ def binaries():
 
 
 @pytest.mark.parametrize("name", ["san_test_quic_fec_group", "san_test_quic_fec_connection",
-                                  "tsan_test_quic_fec_group"])
+                                  "tsan_test_quic_fec_group", "san_test_layout_guard"])
 def test_host_cpp_under_sanitizers(binaries, name):
     exe = os.path.join(ROOT, "tests", "cpp", "build", name)
     assert exe in binaries
@@ -38,3 +38,7 @@ def test_host_cpp_under_sanitizers(binaries, name):
     assert r.returncode == 0, out[-4000:]
     assert " 0 failures" in out, out[-2000:]
     assert "Sanitizer" not in out and "runtime error" not in out, out[-4000:]
+    if name == "san_test_layout_guard":
+        # a caller built against another quic_fec_group.h
+        # is refused loudly, and nothing is written (ASan clean above)
+        assert "refused (QUIC_INTERNAL_ERROR)" in out, out[-2000:]

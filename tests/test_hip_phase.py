@@ -4,8 +4,9 @@ libquic_amd/csrc/qfec_kernels.hip), through the C-ABI.
 Large nt batches (>= kPhMinPhases = 6 phases of CUs x 40 steps x
 floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) of a templated
 k >= 5 (encode) / k >= 8 (recover) run the phased kernel by default (round 4:
-below those group sizes, and at every runtime k, the one-pass kernel is
-faster, tools/phase_k_table.py);
+below those group sizes the one-pass kernel is faster, tools/phase_k_table.py;
+round 5: every k up to 16 templated, the runtime-k body for k > 16 with
+batched loads, so the rule is by k alone);
 QFEC_ONE_PASS forces the one-pass fixed kernel, qfec_debug_phase_min (here 6,
 the default count) keeps the phase-count rule alone so every k reaches the
 phased kernel, and qfec_last_fixed_phased reports which one a call ran (every
@@ -79,14 +80,14 @@ def _run_both(ctx, rows, miss, k, L, n, ps, os_, res, strides):
     return res
 
 
-@pytest.mark.parametrize("k", [2, 4, 5, 7, 8, 10, 12])
+@pytest.mark.parametrize("k", [2, 4, 5, 6, 7, 8, 10, 12, 20])
 def test_default_kernel_choice_by_group_size(ctx, k):
     """The default rule (no test hook): a batch past the phase-count threshold
     runs phased for encode from k = 5 and for recover from k = 8, one-pass
-    below -- and only at the templated group sizes (2, 4, 5, 8, 10, 16): the
-    runtime-k phased body loses to one-pass (round 4's per-k tables,
-    DESIGN.md §4)."""
-    templated = k in (2, 4, 5, 8, 10, 16)
+    below (round 4's per-k tables).  Round 4 phased only the
+    templated sizes (2, 4, 5, 8, 10, 16); round 5 templates every k up to 16
+    and fixed the runtime-k body (k > 16), so the rule is by k alone."""
+    templated = True
     L = 1350
     n = 8 * phase_groups(L) + 777
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
@@ -101,7 +102,8 @@ def test_default_kernel_choice_by_group_size(ctx, k):
 
 
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
-                                 (5, 17), (2, 16), (4, 1350), (8, 1001)])
+                                 (5, 17), (2, 16), (4, 1350), (8, 1001), (6, 1350), (12, 1350),
+                                 (20, 1350), (17, 100), (40, 64)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)

@@ -212,3 +212,94 @@ def test_service_two_threads_two_contexts():
         t.join(timeout=120)
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors
+
+
+def test_service_ring_miss_fails_the_job_and_turns_off():
+    """a published group that lies in no ring entry (the
+    test hook writes the next job with a wrong job number) makes the worker
+    latch a fault and leave WITHOUT storing any token: the call fails with
+    QUIC_INTERNAL_ERROR instead of reporting stale output as finished, the
+    output buffer is untouched, the context turns its service off (the next
+    batches launch and are exact), and re-enabling the service works again."""
+    ctx = qfec.Context(0)
+    z, want_l = _mapped_case(3, g0=90000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=12)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(3 * 1452)
+    try:
+        _check(ctx, z, want_l)  # the service works
+        ctx.debug_service(poison_next=True)
+        par.array[:] = 0xEE
+        plen = np.zeros(3, dtype=np.uint16)
+        with pytest.raises(qfec.QfecError) as ei:
+            ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 3, par.array,
+                              z["parity_off"], plen, mapped=True)
+        assert ei.value.code == qfec.QFEC_ERR_INTERNAL
+        assert "ring" in str(ei.value), str(ei.value)
+        assert (par.array == 0xEE).all()  # nothing reported, nothing written
+        st = ctx.debug_service()
+        for _ in range(3):  # service off now: launched small batches, exact
+            _check(ctx, z, want_l)
+        assert ctx.debug_service()["launches"] == st["launches"]
+        ctx.debug_service(True)
+        _check(ctx, z, want_l)
+        assert ctx.debug_service()["jobs"] > st["jobs"]
+    finally:
+        data.close()
+        par.close()
+        ctx.close()
+
+
+def test_service_nowait_completion_of_a_failed_job():
+    """qfec_complete(ctx, 0) on a service job whose worker
+    left without its token returns an error once the worker stream has
+    drained, not QFEC_PENDING forever."""
+    ctx = qfec.Context(0)
+    z, want_l = _mapped_case(2, g0=91000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=13)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(2 * 1452)
+    try:
+        ctx.debug_service(poison_next=True)
+        plen = np.zeros(2, dtype=np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 2, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        t = ctx.async_ticket()
+        assert t != 0
+        deadline = time.perf_counter() + 10.0
+        rc = 1
+        while time.perf_counter() < deadline:
+            rc = ctx.lib.qfec_complete_ticket(ctx.ctx, t, 0)
+            if rc != 1:
+                break
+            time.sleep(0.001)
+        assert rc == qfec.QFEC_ERR_INTERNAL, rc
+        _check(ctx, z, want_l)  # the context goes on (service off)
+    finally:
+        data.close()
+        par.close()
+        ctx.close()
+
+
+def test_ticket_claimable_after_qfec_complete():
+    """qfec_complete finishes every op, ticketed ones included; a
+    ticket's owner can still claim its own code afterwards (QFEC_OK), once."""
+    ctx = qfec.Context(0)
+    z, want_l = _mapped_case(2, g0=92000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=14)
+    data = qfec.HostBuffer(len(z["data"]))
+    data.array[:] = z["data"]
+    par = qfec.HostBuffer(2 * 1452)
+    try:
+        plen = np.zeros(2, dtype=np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 2, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        t = ctx.async_ticket()
+        assert ctx.complete() == 0
+        assert np.array_equal(plen, want_l)
+        assert ctx.complete_ticket(t) == 0
+        with pytest.raises(qfec.QfecError):
+            ctx.complete_ticket(t)  # claimed once
+    finally:
+        data.close()
+        par.close()
+        ctx.close()

@@ -1,5 +1,5 @@
 """Per-group-size table of the phased fixed-shape kernel (DESIGN.md §4,
-VERDICT r3 item 7): for every templated k, 2^20 groups x k x 1350 B,
+VERDICT r3 item 7, r4 item 3): for every k given, 2^20 groups x k x 1350 B,
 encode and recover with the register-held phase steps (the product since
 round 4) and without them (qfec_debug_phase_regsteps(0): 40 LDS steps per
 phase, round 3's kernel for k != 10), alternated round by round in one
@@ -9,7 +9,9 @@ GPU box; one JSON line per k, then a summary.
 
   python tools/phase_k_table.py [rounds=3] [reps=8] [k,k,...]
 
-The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers.
+The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers,
+and the library's default choice (no test hook) after them.  k > 16 has no
+register steps (runtime-k body): its two phased columns are the same kernel.
 """
 import json
 import os
@@ -43,14 +45,16 @@ def main():
         par = {m: torch.empty(G * L, dtype=torch.uint8, device=dev) for m in (0, 1)}
         out = {m: torch.empty(G * L, dtype=torch.uint8, device=dev) for m in (0, 1)}
         par[2], out[2] = par[0], out[0]  # one-pass writes where LDS-only did (compared below)
-        t = {(m, op): [] for m in (0, 1, 2) for op in ("enc", "rec")}
+        par[3], out[3] = par[2], out[2]
+        t = {(m, op): [] for m in (0, 1, 2, 3) for op in ("enc", "rec")}
         phased = {}
         for r in range(rounds):
-            for m in (1, 0, 2):  # 1: register steps (product), 0: LDS steps only, 2: one-pass
-                ctx.debug_phase_regsteps(m == 1)
+            for m in (1, 0, 2, 3):  # 1: register steps, 0: LDS steps only, 2: one-pass,
+                # 3: the library's default choice (no hook)
+                ctx.debug_phase_regsteps(m != 0)
                 # phased forms at every k (the library's default picks one-pass
                 # below k = 5 / 8 since round 4, from this very table)
-                ctx.debug_phase_min(6 if m != 2 else 0)
+                ctx.debug_phase_min(6 if m in (0, 1) else 0)
                 for op in ("enc", "rec"):
                     def run():
                         if op == "enc":
@@ -77,7 +81,7 @@ def main():
         b = G * (k + 1) * L  # encode: k rows read + parity written; recover: k-1 + parity + out
         rec = {"k": k, "groups": G, "L": L, "identical": bool(same), "round_trip": bool(trip),
                "phased": {f"{m}{op}": phased[(m, op)] for (m, op) in phased}}
-        for m, tag in ((1, "regsteps"), (0, "lds_only"), (2, "one_pass")):
+        for m, tag in ((1, "regsteps"), (0, "lds_only"), (2, "one_pass"), (3, "default")):
             for op in ("enc", "rec"):
                 s = float(np.median(t[(m, op)]))
                 rec[f"{tag}_{op}_us"] = round(s * 1e6, 1)
@@ -86,13 +90,16 @@ def main():
         out_rows.append(rec)
         del rows, par, out
         torch.cuda.empty_cache()
-    print("\n| k | encode: register steps / LDS steps only / one-pass | "
-          "recover: register steps / LDS steps only / one-pass |")
+    print("\n| k | encode: register steps / LDS steps only / one-pass -> default (kernel) | "
+          "recover: register steps / LDS steps only / one-pass -> default (kernel) |")
     print("|---|---|---|")
     for r in out_rows:
+        ke = "phased" if r["phased"]["3enc"] == 1 else "one-pass"
+        kr = "phased" if r["phased"]["3rec"] == 1 else "one-pass"
         print(f"| {r['k']} | {r['regsteps_enc_frac']:.3f} / {r['lds_only_enc_frac']:.3f} / "
-              f"{r['one_pass_enc_frac']:.3f} | {r['regsteps_rec_frac']:.3f} / "
-              f"{r['lds_only_rec_frac']:.3f} / {r['one_pass_rec_frac']:.3f} |")
+              f"{r['one_pass_enc_frac']:.3f} -> **{r['default_enc_frac']:.3f}** ({ke}) | "
+              f"{r['regsteps_rec_frac']:.3f} / {r['lds_only_rec_frac']:.3f} / "
+              f"{r['one_pass_rec_frac']:.3f} -> **{r['default_rec_frac']:.3f}** ({kr}) |")
     ok = all(r["identical"] and r["round_trip"] for r in out_rows)
     print("all identical and round trips exact:", ok)
     return 0 if ok else 2
