@@ -1437,7 +1437,11 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     if (!c.live) return QFEC_OK;
     if (c.token) {
       const int wrc = c.svc ? wait_flag_svc(ctx, si, c.token) : wait_flag(ctx, si, c.token);
-      if (wrc) return wrc;
+      if (wrc) {
+        c.live = false;
+        if (c.svc) svc_abandon(ctx);  // no later worker may run the failed job
+        return wrc;
+      }
     } else {
       QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
     }

@@ -112,36 +112,43 @@ __device__ __forceinline__ void xor_rows_n(u32x4& acc, const uint8_t* src, uint6
   for (int w = 0; w < N; ++w) acc ^= v[w];
 }
 
-// Rows [0, k) of a group at runtime k: batches of B loads, then the
-// remainder as one batch of k mod B (a wave-uniform switch).
+// Rows [0, k) of a group at runtime k: ceil(k / B) batches of loads in
+// flight, their sizes as even as possible (k = 20, B = 16: 10 + 10, not
+// 16 + 4 -- a batch is a round trip; tools/phase_k_table.py, round 5).
 template <int B, bool RECOVER, bool NT>
 __device__ __forceinline__ void xor_rows_rt(u32x4& acc, const uint8_t* src, uint64_t row_stride,
                                             uint32_t k, uint32_t m, const uint8_t* par) {
   static_assert(B == 8 || B == 16, "batch of 8 or 16 rows");
+  const uint32_t nb = (k + B - 1) / B;
+  const uint32_t base = nb ? k / nb : 0u, extra = k - base * nb;
   uint32_t r = 0;
-  for (; r + B <= k; r += B) xor_rows_n<B, RECOVER, NT>(acc, src, row_stride, r, m, par);
-  switch (k - r) {
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t n = base + (b < extra ? 1u : 0u);
+    switch (n) {
 #define QFEC_REM(N)                                                 \
   case N:                                                           \
     xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
     break;
-    QFEC_REM(1) QFEC_REM(2) QFEC_REM(3) QFEC_REM(4) QFEC_REM(5) QFEC_REM(6) QFEC_REM(7)
-#undef QFEC_REM
-    default:
-      break;
-  }
-  if constexpr (B == 16) {
-    switch (k - r) {
-#define QFEC_REM(N)                                                 \
-  case N:                                                           \
-    xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
-    break;
-      QFEC_REM(8) QFEC_REM(9) QFEC_REM(10) QFEC_REM(11) QFEC_REM(12) QFEC_REM(13) QFEC_REM(14)
-      QFEC_REM(15)
+      QFEC_REM(1) QFEC_REM(2) QFEC_REM(3) QFEC_REM(4) QFEC_REM(5) QFEC_REM(6) QFEC_REM(7)
+      QFEC_REM(8)
 #undef QFEC_REM
       default:
+        if constexpr (B == 16) {
+          switch (n) {
+#define QFEC_REM(N)                                                 \
+  case N:                                                           \
+    xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
+    break;
+            QFEC_REM(9) QFEC_REM(10) QFEC_REM(11) QFEC_REM(12) QFEC_REM(13) QFEC_REM(14)
+            QFEC_REM(15) QFEC_REM(16)
+#undef QFEC_REM
+            default:
+              break;
+          }
+        }
         break;
     }
+    r += n;
   }
 }
 
@@ -1789,9 +1796,11 @@ constexpr uint32_t kPhMinPhases = 6;
 // a time (profiles/round4/phase_k_table_nontemplated_r4o.txt: k = 6 0.27 vs
 // 0.69 one-pass); round 5 templates every k up to 16 and gives the runtime
 // body (k > 16) batches of 16 with a one-batch remainder (xor_rows_rt), so
-// the rule is by k alone again (tools/phase_k_table.py).  An
+// the rule is by k alone again (tools/phase_k_table.py); its
+// round-5 table moved recover's threshold to k = 7 (phased 0.719 vs one-pass
+// 0.697; k = 6 0.684 vs 0.720: profiles/round5/phase_k_table_r5b.txt).  An
 // explicit phase_min (test hook) keeps the phase-count rule alone.
-constexpr uint32_t kPhMinKEncode = 5, kPhMinKRecover = 8;
+constexpr uint32_t kPhMinKEncode = 5, kPhMinKRecover = 7;
 
 bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* nphase) {
   if (a.ncu == 0) return false;

@@ -3,7 +3,7 @@ libquic_amd/csrc/qfec_kernels.hip), through the C-ABI.
 
 Large nt batches (>= kPhMinPhases = 6 phases of CUs x 40 steps x
 floor(256 / ceil(L/16)) groups, qfec_kernels.hip phase_plan) of a templated
-k >= 5 (encode) / k >= 8 (recover) run the phased kernel by default (round 4:
+k >= 5 (encode) / k >= 7 (recover) run the phased kernel by default (round 4:
 below those group sizes the one-pass kernel is faster, tools/phase_k_table.py;
 round 5: every k up to 16 templated, the runtime-k body for k > 16 with
 batched loads, so the rule is by k alone);
@@ -83,8 +83,8 @@ def _run_both(ctx, rows, miss, k, L, n, ps, os_, res, strides):
 @pytest.mark.parametrize("k", [2, 4, 5, 6, 7, 8, 10, 12, 20])
 def test_default_kernel_choice_by_group_size(ctx, k):
     """The default rule (no test hook): a batch past the phase-count threshold
-    runs phased for encode from k = 5 and for recover from k = 8, one-pass
-    below (round 4's per-k tables).  Round 4 phased only the
+    runs phased for encode from k = 5 and for recover from k = 7 (round 5's
+    table; round 4 had 8), one-pass below.  Round 4 phased only the
     templated sizes (2, 4, 5, 8, 10, 16); round 5 templates every k up to 16
     and fixed the runtime-k body (k > 16), so the rule is by k alone."""
     templated = True
@@ -97,7 +97,7 @@ def test_default_kernel_choice_by_group_size(ctx, k):
     ctx.encode(rows, k, L, n, par)
     assert ctx.last_fixed_phased() == (1 if templated and k >= 5 else 0)
     ctx.recover(rows, par, miss, k, L, n, out)
-    assert ctx.last_fixed_phased() == (1 if templated and k >= 8 else 0)
+    assert ctx.last_fixed_phased() == (1 if templated and k >= 7 else 0)
     ctx.sync()
 
 
