@@ -580,14 +580,27 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     if constexpr (RECOVER) {
       if (((bad_lo | bad_hi) != 0u || rbad) && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
-    phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
     // INPL: the output row of group g is its own row missing[g] (the in-slot
-    // recover written in place; every read of the phase is done by now, and
-    // no other workgroup reads this group)
+    // recover written in place; every read of the phase is done by the
+    // meeting, and no other workgroup reads this group).  The phase's lost
+    // indices are loaded before the meeting, all at once (one round trip
+    // under the meeting's wait instead of one per unrolled batch of stores:
+    // 0.76 vs 0.81 of 8 TB/s, profiles/round5/bench_r5b.json), and the store
+    // loops are unrolled so that they index them statically.
+    constexpr int TSI = INPL ? TS : 1;
+    uint32_t mi[TSI];
+    if constexpr (INPL) {
+#pragma unroll
+      for (int i = 0; i < TS; ++i) {
+        const uint64_t g = gidx(i);
+        mi[i] = lane_on && g < a.n_groups && i < SP ? (uint32_t)a.inplace_missing[g] : 0u;
+      }
+    }
+    phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
     bool ibad = false;
-    auto dst = [&](uint64_t g, bool& on) -> uint8_t* {
+    auto dst = [&](uint64_t g, int i, bool& on) -> uint8_t* {
       if constexpr (INPL) {
-        const uint32_t m = a.inplace_missing[g];
+        const uint32_t m = mi[INPL ? i : 0];
         if (m >= k) {
           ibad = ibad || on;
           on = false;
@@ -597,20 +610,30 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         return a.out + g * a.out_stride + off;
       }
     };
+    if constexpr (INPL) {
+#pragma unroll
+      for (int i = 0; i < STEPS; ++i) {
+        const uint64_t g = gidx(i);
+        bool on = lane_on && g < a.n_groups && i < NL;
+        uint8_t* d = dst(on ? g : 0, i, on);
+        if (on) st16t<true>(d, s_par[i][tid]);
+      }
+    } else {
 #pragma unroll 4
-    for (int i = 0; i < STEPS; ++i) {
-      const uint64_t g = gidx(i);
-      const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
-      bool on = lane_on && g < a.n_groups && !skip && i < NL;
-      uint8_t* d = dst(on ? g : 0, on);
-      if (on) st16t<true>(d, s_par[i][tid]);
+      for (int i = 0; i < STEPS; ++i) {
+        const uint64_t g = gidx(i);
+        const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
+        bool on = lane_on && g < a.n_groups && !skip && i < NL;
+        uint8_t* d = dst(on ? g : 0, 0, on);
+        if (on) st16t<true>(d, s_par[i][tid]);
+      }
     }
     if constexpr (RS > 0) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = gidx(STEPS + j);
         bool on = ((ron[j / 32] >> (j % 32)) & 1u) != 0u;
-        uint8_t* d = dst(on ? g : 0, on);
+        uint8_t* d = dst(on ? g : 0, STEPS + j, on);
         if (on) st16t<true>(d, racc[j]);
       }
     }

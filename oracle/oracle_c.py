@@ -73,6 +73,10 @@ def lib():
         L.qo_group_digest.restype = C.c_uint64
         L.qo_group_digest.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p,
                                       C.c_void_p, C.c_int]
+        L.qo_ragged_digests.restype = None
+        L.qo_ragged_digests.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.qo_fixed_digests.restype = None
         L.qo_fixed_digests.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
                                        C.c_uint32, C.c_int, C.POINTER(C.c_uint64),
@@ -205,6 +209,14 @@ def fixed_digests(seed, drop_seed, g0, n, k, L, threads=None):
     threads = threads or min(16, os.cpu_count() or 1)
     a, b = C.c_uint64(0), C.c_uint64(0)
     lib().qo_fixed_digests(seed, drop_seed, g0, n, k, L, threads, C.byref(a), C.byref(b))
+    return int(a.value), int(b.value)
+
+
+def ragged_digests(seed, drop_seed, g0, n, kmin=5, kmax=15, lmin=64, lmax=1350, threads=None):
+    threads = threads or min(16, os.cpu_count() or 1)
+    a, b = C.c_uint64(0), C.c_uint64(0)
+    lib().qo_ragged_digests(seed, drop_seed, g0, n, kmin, kmax, lmin, lmax, threads, C.byref(a),
+                            C.byref(b))
     return int(a.value), int(b.value)
 
 

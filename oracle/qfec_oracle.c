@@ -349,6 +349,68 @@ void qo_fixed_digests(uint64_t seed, uint64_t drop_seed, uint64_t g0, uint64_t n
   free(rh);
 }
 
+/* Ragged (configs[3]) digests without materialising the batch: group g has
+ * k = qo_ragged_k(seed, g, kmin, kmax) packets of qo_ragged_len(seed, g, i,
+ * lmin, lmax) bytes filled by qo_synth_row; its parity is parity_len = max len
+ * bytes (zero padded XOR, as qo_encode_ragged), its revived row the lost
+ * packet qo_drop_index(drop_seed, g, k) zero padded to parity_len (as
+ * qo_recover_ragged). */
+typedef struct {
+  uint64_t seed, drop_seed, g0, n;
+  uint32_t kmin, kmax, lmin, lmax;
+  uint64_t *ph, *rh;
+} qo_rdig_job;
+
+static void* qo_rdig_run(void* arg) {
+  qo_rdig_job* j = (qo_rdig_job*)arg;
+  uint8_t row[QO_MAX_PACKET_SIZE], par[QO_MAX_PACKET_SIZE], lost[QO_MAX_PACKET_SIZE];
+  for (uint64_t g = 0; g < j->n; ++g) {
+    const uint64_t gg = j->g0 + g;
+    const uint32_t k = qo_ragged_k(j->seed, gg, j->kmin, j->kmax);
+    const uint32_t m = qo_drop_index(j->drop_seed, gg, k);
+    uint32_t plen = 0;
+    memset(par, 0, sizeof(par));
+    memset(lost, 0, sizeof(lost));
+    for (uint32_t i = 0; i < k; ++i) {
+      const uint32_t len = qo_ragged_len(j->seed, gg, i, j->lmin, j->lmax);
+      qo_synth_row(j->seed, gg, i, len, row);
+      for (uint32_t b = 0; b < len; ++b) par[b] ^= row[b];
+      if (i == m) memcpy(lost, row, len);
+      if (len > plen) plen = len;
+    }
+    j->ph[g] = qo_fnv1a64(par, plen, 0);
+    j->rh[g] = qo_fnv1a64(lost, plen, 0);
+  }
+  return NULL;
+}
+
+void qo_ragged_digests(uint64_t seed, uint64_t drop_seed, uint64_t g0, uint64_t n, uint32_t kmin,
+                       uint32_t kmax, uint32_t lmin, uint32_t lmax, int threads,
+                       uint64_t* parity_digest, uint64_t* recovered_digest) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  uint64_t* ph = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+  uint64_t* rh = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+  qo_rdig_job jobs[256];
+  pthread_t tid[256];
+  uint64_t per = (n + threads - 1) / threads;
+  int started = 0;
+  for (int t = 0; t < threads; ++t) {
+    uint64_t a = per * t;
+    if (a >= n) break;
+    qo_rdig_job jb = {seed, drop_seed, g0 + a, (a + per > n) ? n - a : per,
+                      kmin, kmax, lmin, lmax, ph + a, rh + a};
+    jobs[t] = jb;
+    pthread_create(&tid[t], NULL, qo_rdig_run, &jobs[t]);
+    ++started;
+  }
+  for (int t = 0; t < started; ++t) pthread_join(tid[t], NULL);
+  *parity_digest = qo_fnv1a64((const uint8_t*)ph, n * sizeof(uint64_t), 0);
+  *recovered_digest = qo_fnv1a64((const uint8_t*)rh, n * sizeof(uint64_t), 0);
+  free(ph);
+  free(rh);
+}
+
 double qo_time_single_group_ns(uint32_t k, uint32_t L, uint64_t iters) {
   uint8_t* rows = (uint8_t*)malloc((size_t)k * L);
   uint8_t par[QO_MAX_PACKET_SIZE], out[QO_MAX_PACKET_SIZE];

@@ -101,6 +101,14 @@ void qo_fixed_digests(uint64_t seed, uint64_t drop_seed, uint64_t g0, uint64_t n
                       uint32_t L, int threads, uint64_t* parity_digest,
                       uint64_t* recovered_digest);
 
+/* The same for the ragged configs[3] workload (qo_ragged_k / qo_ragged_len
+ * shapes, qo_synth_row bytes): digests of the parity rows (parity_len = max
+ * len bytes each) and of the revived rows (the lost packet zero padded to
+ * parity_len).  Layout independent: the digests cover the bytes of each row. */
+void qo_ragged_digests(uint64_t seed, uint64_t drop_seed, uint64_t g0, uint64_t n, uint32_t kmin,
+                       uint32_t kmax, uint32_t lmin, uint32_t lmax, int threads,
+                       uint64_t* parity_digest, uint64_t* recovered_digest);
+
 #ifdef __cplusplus
 }
 #endif

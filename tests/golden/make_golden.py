@@ -92,6 +92,25 @@ def main():
         with open(os.path.join(HERE, "full_digests.json"), "w") as f:
             json.dump(out, f, indent=1)
             f.write("\n")
+    if "--full" in sys.argv or "--full-ragged" in sys.argv:
+        # configs[3] at full size: 2^20 ragged groups, k 5-15,
+        # payloads 64-1350 B, parity rows and revived rows (layout independent)
+        from oracle import oracle_c as OC
+        n = 1 << 20
+        path = os.path.join(HERE, "full_digests.json")
+        with open(path) as f:
+            out = json.load(f)
+        pd, rd = OC.ragged_digests(Q.SEED_RAGGED, Q.SEED_DROP, 0, n, 5, 15, 64, 1350)
+        out["ragged"] = {"seed": Q.SEED_RAGGED, "drop_seed": Q.SEED_DROP, "k": [5, 15],
+                         "len": [64, 1350],
+                         "digests": {"g0=0,n=1048576": {"parity": f"{pd:#018x}",
+                                                        "recovered": f"{rd:#018x}"}},
+                         "definition": "as above, over each group's parity_len bytes of parity "
+                                       "(resp. of the revived row: the lost packet zero padded "
+                                       "to parity_len); oracle/qfec_oracle.c qo_ragged_digests"}
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+            f.write("\n")
     print("golden fixtures written to", HERE)
 
 

@@ -61,6 +61,42 @@ def test_bench_cli_spawns_ranks_cpu_workload():
         assert s["digests"][1] == hashlib.sha256(out[sl].tobytes()).hexdigest()[:32]
 
 
+def test_bench_cli_eight_ranks_disjoint_verified_shards():
+    """the 8-GPU launch shape on the CPU -- `bench.py --gpus
+    8 --cpu-workload` starts 8 ranks (gloo); the line says n_gpus 8, the 8
+    shards are disjoint and cover [0, 8G) in order, every one is verified, and
+    each shard's digests equal the oracle's over its range."""
+    G = 16
+    p = _bench_cli(["--gpus", "8", "--cpu-workload", "--groups", str(G), "--steps", "1",
+                    "--warmup", "0", "--no-cpu-baseline"], timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert line["n_gpus"] == 8 and line["verified"] is True
+    shards = sorted(line["shards"], key=lambda s: s["rank"])
+    assert [s["rank"] for s in shards] == list(range(8))
+    assert [s["g0"] for s in shards] == [r * G for r in range(8)]
+    assert all(s["groups"] == G and s["verified"] for s in shards)
+    import hashlib
+    from oracle import oracle_c as OC
+    import bench
+    k, L = 10, 1350
+    rows = OC.synth_fixed(bench.SEED_FIXED, 0, 8 * G, k, L)
+    rc, par = OC.encode_fixed(rows, k, L, 8 * G)
+    miss = bench.drop_indices(0, 8 * G, k)
+    rc2, out = OC.recover_fixed(rows, par, miss, k, L, 8 * G)
+    assert rc == 0 and rc2 == 0
+    for s in shards:
+        sl = slice(s["g0"] * L, (s["g0"] + G) * L)
+        assert s["digests"][0] == hashlib.sha256(par[sl].tobytes()).hexdigest()[:32]
+        assert s["digests"][1] == hashlib.sha256(out[sl].tobytes()).hexdigest()[:32]
+
+
+def test_numa_cpulist_parser():
+    import bench
+    assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench._cpulist("") == set()
+
+
 def test_bench_cli_one_rank_matches_two_rank_shard0():
     G = 32
     p1 = _bench_cli(["--gpus", "1", "--cpu-workload", "--groups", str(G), "--steps", "1",
@@ -138,6 +174,13 @@ def test_bench_cli_two_ranks_on_one_gpu():
         assert rc == 0 and rc2 == 0
         assert s["digests"][0] == hashlib.sha256(par.tobytes()).hexdigest()[:32]
         assert s["digests"][1] == hashlib.sha256(out.tobytes()).hexdigest()[:32]
+    # the host-memory leg on every rank of an N>1 line,
+    # per rank and aggregated, each rank bound to its GPU's NUMA node
+    e2e = line["e2e_pinned_host"]
+    assert [r["rank"] for r in sorted(e2e["per_rank"], key=lambda r: r["rank"])] == [0, 1]
+    assert e2e["verified"] is True
+    assert e2e["aggregate_encode_GiBps"] > 0 and e2e["min_rank_encode_GiBps"] > 0
+    assert all("numa" in r for r in e2e["per_rank"])
 
 
 @pytest.mark.gpu

@@ -367,3 +367,39 @@ def test_ragged_large_batch_odd_groups(ctx):
         o = int(poff[g])
         assert np.array_equal(par_h[o:o + L], wp[:L]), g
         assert np.array_equal(out_h[o:o + L], wo[:L]), g
+
+
+@pytest.mark.parametrize("align,slot", [(16, 1536), (1, 1452)])
+def test_full_size_ragged_digest(ctx, align, slot):
+    """configs[3] at full size: 2^20 groups, k 5-15,
+    payloads 64-1350 B, on the bench's layouts (16-B-aligned payloads with
+    1,536-B slots, and byte-packed with 1,452-B slots): the parity rows and
+    the revived rows against the committed oracle digests
+    (tests/golden/full_digests.json "ragged", oracle qo_ragged_digests), and
+    every group's revived row equal to its lost packet on the device."""
+    import json
+    import os
+    from conftest import GOLDEN
+    from libquic_amd import synth
+    with open(os.path.join(GOLDEN, "full_digests.json")) as f:
+        dg = json.load(f)["ragged"]["digests"]["g0=0,n=1048576"]
+    G = 1 << 20
+    ks, ptr, ln, off = synth.ragged_layout(0, G, 5, 15, 64, 1350, Q.SEED_RAGGED, align=align)
+    miss = synth.drop_indices(Q.SEED_DROP, np.arange(G, dtype=np.uint64), ks).astype(np.uint8)
+    poff = np.arange(G, dtype=np.uint64) * np.uint64(slot)
+    data = torch.full((int(off[-1]) + int(ln[-1]),), 0x77, dtype=torch.uint8, device=DEV)
+    t_off, t_len, t_ptr = dview(off), dview(ln), dview(ptr)
+    t_poff = dview(poff)
+    ctx.synth_ragged(data, t_off, t_len, t_ptr, 0, G, Q.SEED_RAGGED)
+    par = torch.full((G * slot,), 0xA5, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(G, dtype=torch.int16, device=DEV)
+    out = torch.full((G * slot,), 0x5A, dtype=torch.uint8, device=DEV)
+    ctx.encode_ragged(data, t_off, t_len, t_ptr, G, par, t_poff, plen)
+    ctx.recover_ragged(data, t_off, t_len, t_ptr, G, par, t_poff, plen, dview(miss), out, t_poff)
+    ctx.sync()
+    torch.cuda.synchronize()
+    plen_h = plen.cpu().numpy().view(np.uint16)
+    assert np.array_equal(plen_h, np.maximum.reduceat(ln, ptr[:-1].astype(np.int64)))
+    par_h, out_h = par.cpu().numpy(), out.cpu().numpy()
+    assert f"{OC.group_digest(par_h, G, off=poff, lens=plen_h):#018x}" == dg["parity"]
+    assert f"{OC.group_digest(out_h, G, off=poff, lens=plen_h):#018x}" == dg["recovered"]

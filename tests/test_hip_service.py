@@ -303,3 +303,63 @@ def test_ticket_claimable_after_qfec_complete():
         data.close()
         par.close()
         ctx.close()
+
+
+def test_phased_launch_beside_a_continuously_fed_service():
+    """context B's small-batch worker kept resident by a
+    thread feeding it continuously, while context A runs phased encodes of a
+    large batch.  The worker holds one CU's LDS, so A's one-workgroup-per-CU
+    grid may not be resident at once: its meetings then time out and the
+    launch abandons them (a slower, identical result).  A's parity must equal
+    its one-pass parity; the abandoned-launch count is reported; B's results
+    stay exact throughout."""
+    import threading
+    import torch
+    from oracle import qfec_np as Q
+    a = qfec.Context(0)
+    stop = threading.Event()
+    errors, fed = [], [0]
+
+    def feeder():
+        try:
+            b = qfec.Context(0)
+            try:
+                z, want_l = _mapped_case(3, g0=93000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=15)
+                while not stop.is_set():
+                    _check(b, z, want_l)
+                    fed[0] += 1
+            finally:
+                b.close()
+        except Exception as e:  # reported on the main thread
+            errors.append(repr(e))
+
+    th = threading.Thread(target=feeder)
+    th.start()
+    try:
+        k, L = 10, 1350
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        n = 8 * ncu * 40 * (256 // ((L + 15) // 16)) + 5
+        rows = torch.empty(n * k * L, dtype=torch.uint8, device="cuda:0")
+        a.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+        want = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        a.encode(rows, k, L, n, want, one_pass=True)
+        a.sync()
+        while fed[0] < 5 and not errors:  # the worker is resident and busy
+            pass
+        before = a.phase_abandons()
+        par = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        for _ in range(3):
+            a.debug_phase(0, reset_backoff=True)  # try the phased kernel every time
+            par.fill_(0)
+            a.encode(rows, k, L, n, par)
+            assert a.last_fixed_phased() == 1
+            a.sync()
+            assert torch.equal(par, want)
+        print(f"phased launches beside a fed service worker: abandoned "
+              f"{a.phase_abandons() - before} of 3; service batches meanwhile {fed[0]}")
+    finally:
+        stop.set()
+        th.join(timeout=120)
+        a.close()
+    assert not th.is_alive()
+    assert not errors, errors

@@ -192,6 +192,40 @@ def test_full_digests_committed():
     assert f"{rd:#018x}" == d["digests"]["g0=0,n=1048576"]["recovered"]
 
 
+def test_ragged_digest_definition_matches_oracle_batch():
+    """qo_ragged_digests (the full-size configs[3] digests) equals the digests
+    of qo_encode_ragged / qo_recover_ragged over the same batch, built by the
+    bench's layout generator (libquic_amd/synth.py) on 3,000 groups, packed
+    and 16-B aligned."""
+    from libquic_amd import synth
+    n = 3000
+    pd, rd = OC.ragged_digests(Q.SEED_RAGGED, Q.SEED_DROP, 0, n, 5, 15, 64, 1350, threads=2)
+    for align in (1, 16):
+        ks, ptr, ln, off = synth.ragged_layout(0, n, 5, 15, 64, 1350, Q.SEED_RAGGED, align=align)
+        data = np.zeros(int(off[-1]) + int(ln[-1]), np.uint8)
+        for p in range(ln.size):
+            g = int(np.searchsorted(ptr, p, side="right") - 1)
+            row = np.zeros(int(ln[p]), np.uint8)
+            OC.lib().qo_synth_row(Q.SEED_RAGGED, g, int(p - ptr[g]), int(ln[p]), OC._p(row))
+            data[int(off[p]):int(off[p]) + int(ln[p])] = row
+        poff = np.arange(n, dtype=np.uint64) * np.uint64(1452)
+        miss = synth.drop_indices(Q.SEED_DROP, np.arange(n, dtype=np.uint64), ks).astype(np.uint8)
+        rc, par, plen = OC.encode_ragged(data, off, ln, ptr, poff, n * 1452)
+        rc2, out = OC.recover_ragged(data, off, ln, ptr, par, poff, plen, miss, poff, n * 1452)
+        assert rc == 0 and rc2 == 0
+        assert OC.group_digest(par, n, off=poff, lens=plen) == pd, align
+        assert OC.group_digest(out, n, off=poff, lens=plen) == rd, align
+
+
+def test_full_ragged_digests_committed():
+    with open(os.path.join(GOLDEN, "full_digests.json")) as f:
+        d = json.load(f)["ragged"]
+    assert d["seed"] == Q.SEED_RAGGED and d["k"] == [5, 15] and d["len"] == [64, 1350]
+    pd, rd = OC.ragged_digests(Q.SEED_RAGGED, Q.SEED_DROP, 0, 1 << 20, 5, 15, 64, 1350)
+    assert f"{pd:#018x}" == d["digests"]["g0=0,n=1048576"]["parity"]
+    assert f"{rd:#018x}" == d["digests"]["g0=0,n=1048576"]["recovered"]
+
+
 def test_cpu_multithread_equals_single():
     k, L, n = 10, 1350, 1000
     rows = OC.synth_fixed(Q.SEED_FIXED, 0, n, k, L)
