@@ -250,7 +250,9 @@ int ensure_staging(qfec_ctx* ctx) {
 }
 
 // ---- small-batch service ---------------------------------------------------
-constexpr uint64_t kSvcGroups = 16;           // batches up to this size use it
+// batches up to this size use it (round 5: 64, with the tables inline in the
+// ring entry; round 4: 16)
+constexpr uint64_t kSvcGroups = 64;
 // idle time before the worker leaves: 100 us (100-MHz wall clock) -- below the
 // phased kernel's 200-us meeting timeout, so a worker of another context never
 // makes a phased launch give up its meetings; a flush loop that comes back
@@ -272,16 +274,27 @@ int ensure_service(qfec_ctx* ctx) {
   return QFEC_OK;
 }
 
-// Queue batch `a` (tables in slot `slot`'s mapped buffer) as one job; its
-// completion is token in the slot's flag.  Publishes, then relaunches the
-// worker if it has left (or never ran).
-int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token) {
+// The ring entry the next job goes into (its tables are written straight
+// into entry->tab by the caller, then svc_submit publishes it).  The entry of
+// job seq - kSvcRing is free: at most kSlots jobs are outstanding (each holds
+// a slot until completed) and kSvcRing > kSlots.
+qfec::SvcJob* svc_next_entry(qfec_ctx* ctx) {
+  static_assert(qfec::kSvcRing > kSlots, "service ring smaller than the slots");
+  return &ctx->svc_ring[ctx->svc_seq % qfec::kSvcRing];
+}
+
+// Queue batch `a` (payload pointers; its index tables already inline in
+// svc_next_entry(ctx)->tab at the offsets given) as one job; its completion
+// is token in the slot's flag.  Publishes, then relaunches the worker if it
+// has left (or never ran).
+struct SvcTabs {
+  uint32_t bytes, off, len, ptr, poff, plen, miss, ooff;
+};
+int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token,
+               const SvcTabs& tb) {
   int rc = ensure_service(ctx);
   if (rc) return rc;
   qfec::SvcShared* sh = ctx->svc_sh;
-  // the ring entry of job seq - kSvcRing is free: at most kSlots jobs are
-  // outstanding (each holds a slot until completed) and kSvcRing > kSlots
-  static_assert(qfec::kSvcRing > kSlots, "service ring smaller than the slots");
   const uint32_t seq = ctx->svc_seq++;
   qfec::SvcJob& j = ctx->svc_ring[seq % qfec::kSvcRing];
   j.a = a;
@@ -291,6 +304,14 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   j.recover = recover ? 1u : 0u;
   j.flag_slot = (uint32_t)slot;
   j.token = token;
+  j.tab_bytes = tb.bytes;
+  j.t_off = tb.off;
+  j.t_len = tb.len;
+  j.t_ptr = tb.ptr;
+  j.t_poff = tb.poff;
+  j.t_plen = tb.plen;
+  j.t_miss = tb.miss;
+  j.t_ooff = tb.ooff;
   const uint32_t wseq = ctx->svc_poison_next ? seq ^ 0x80000000u : seq;  // test hook
   ctx->svc_poison_next = false;
   __atomic_store_n(&j.seq, wseq, __ATOMIC_RELEASE);
@@ -1485,7 +1506,13 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     const Tab t(np, cnt, recover);
     if ((rc = finish(slot))) return rc;
     Slot& s = ctx->slots[slot];
-    uint8_t* h = s.h_in;
+    // a few groups go to the resident service worker, their index tables
+    // written INLINE into its ring entry (the worker reads entry and tables
+    // in one round trip); everything else through the slot's mapped buffer
+    bool svc = direct && ctx->svc_on && cnt <= kSvcGroups && t.total <= qfec::kSvcTab &&
+               ensure_service(ctx) == QFEC_OK;
+    qfec::SvcJob* je = svc ? svc_next_entry(ctx) : nullptr;
+    uint8_t* h = svc ? je->tab : s.h_in;
     std::memcpy(h + t.off, pkt_off + p0, np * 8);  // payloads stay where they are
     std::memcpy(h + t.len, pkt_len + p0, np * 2);
     uint32_t* h_ptr = reinterpret_cast<uint32_t*>(h + t.ptr);
@@ -1520,7 +1547,6 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       a.out = parity_out;
     }
     uint32_t token = 0;
-    bool svc = false;
     if (direct) {
       token = ++ctx->flag_token ? ctx->flag_token : ++ctx->flag_token;  // never 0
       a.done_count = ctx->d_done + slot;
@@ -1528,12 +1554,15 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       a.done_token = token;
       // a few groups: the resident service worker takes them from its ring
       // (no launch); a flag is all their completion needs
-      svc = ctx->svc_on && cnt <= kSvcGroups;
-      if (svc && svc_submit(ctx, slot, a, recover, token) != QFEC_OK) {
+      const SvcTabs tb{(uint32_t)t.total, (uint32_t)t.off, (uint32_t)t.len, (uint32_t)t.ptr,
+                       (uint32_t)t.poff, (uint32_t)t.plen, (uint32_t)t.miss, (uint32_t)t.ooff};
+      if (svc && svc_submit(ctx, slot, a, recover, token, tb) != QFEC_OK) {
         // the service could not be set up or (re)launched: off for this
-        // context, this batch launched as before (same flag and token)
+        // context, this batch launched as before (same flag and token), its
+        // tables moved from the ring entry to the slot buffer the launch reads
         ctx->svc_on = false;
         svc = false;
+        std::memcpy(s.h_in, je->tab, t.total);
       }
       if (!svc) {
         if (cnt <= kDirectGroups)

@@ -93,13 +93,21 @@ struct RaggedArgs {
 // and `consumed`, and exits after idle_ticks without work (alive = 0, then one
 // more look at pub_end: the host, after publishing, relaunches it if it
 // reads alive == 0 -- each side writes, fences, then reads the other's word).
+// Round 5: the job's index tables are written INLINE (tab, at the t_*
+// offsets, the direct path's Tab layout), so the worker copies the entry --
+// header and tables -- into LDS in one PCIe round trip.  a's table pointers
+// are not used by the worker.
+constexpr uint32_t kSvcTab = 16384 - 256;  // inline table bytes (64 groups of up to 16 packets)
 struct SvcJob {
-  RaggedArgs a;       // tables in the mapped slot buffer, as the direct path
+  RaggedArgs a;       // bytes / parity / out: the mapped payload buffers
   uint64_t start;     // the job's first group in the global group sequence
   uint32_t seq;       // job number (ring index = seq % kSvcRing)
   uint32_t recover;
   uint32_t flag_slot; // index into the context's host-mapped flags
   uint32_t token;
+  uint32_t tab_bytes; // table bytes in tab (<= kSvcTab)
+  uint32_t t_off, t_len, t_ptr, t_poff, t_plen, t_miss, t_ooff;  // offsets into tab
+  alignas(16) uint8_t tab[kSvcTab];
 };
 struct SvcShared {
   uint64_t pub_end;   // host: groups published

@@ -580,27 +580,18 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
     if constexpr (RECOVER) {
       if (((bad_lo | bad_hi) != 0u || rbad) && t == 0u) atomicOr(a.err, kErrMissingIndex);
     }
-    // INPL: the output row of group g is its own row missing[g] (the in-slot
-    // recover written in place; every read of the phase is done by the
-    // meeting, and no other workgroup reads this group).  The phase's lost
-    // indices are loaded before the meeting, all at once (one round trip
-    // under the meeting's wait instead of one per unrolled batch of stores:
-    // 0.76 vs 0.81 of 8 TB/s, profiles/round5/bench_r5b.json), and the store
-    // loops are unrolled so that they index them statically.
-    constexpr int TSI = INPL ? TS : 1;
-    uint32_t mi[TSI];
-    if constexpr (INPL) {
-#pragma unroll
-      for (int i = 0; i < TS; ++i) {
-        const uint64_t g = gidx(i);
-        mi[i] = lane_on && g < a.n_groups && i < SP ? (uint32_t)a.inplace_missing[g] : 0u;
-      }
-    }
     phase_meet(a.phase_sync, MEET2 ? 2u * p + 1u : p + 1u);
+    // INPL: the output row of group g is its own row missing[g] (the in-slot
+    // recover written in place; every read of the phase is done by now, and
+    // no other workgroup reads this group).  It runs at 0.73-0.76 of 8 TB/s
+    // against 0.80-0.82 out of place: its stores land inside the rows' own
+    // allocation, the DRAM placement DESIGN.md §4 measured slow for the
+    // one-pass kernel's parity too (prefetching the lost indices before the
+    // meeting measured no better: profiles/round5/bench_r5{b,c}.json).
     bool ibad = false;
-    auto dst = [&](uint64_t g, int i, bool& on) -> uint8_t* {
+    auto dst = [&](uint64_t g, bool& on) -> uint8_t* {
       if constexpr (INPL) {
-        const uint32_t m = mi[INPL ? i : 0];
+        const uint32_t m = a.inplace_missing[g];
         if (m >= k) {
           ibad = ibad || on;
           on = false;
@@ -610,30 +601,20 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
         return a.out + g * a.out_stride + off;
       }
     };
-    if constexpr (INPL) {
-#pragma unroll
-      for (int i = 0; i < STEPS; ++i) {
-        const uint64_t g = gidx(i);
-        bool on = lane_on && g < a.n_groups && i < NL;
-        uint8_t* d = dst(on ? g : 0, i, on);
-        if (on) st16t<true>(d, s_par[i][tid]);
-      }
-    } else {
 #pragma unroll 4
-      for (int i = 0; i < STEPS; ++i) {
-        const uint64_t g = gidx(i);
-        const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
-        bool on = lane_on && g < a.n_groups && !skip && i < NL;
-        uint8_t* d = dst(on ? g : 0, 0, on);
-        if (on) st16t<true>(d, s_par[i][tid]);
-      }
+    for (int i = 0; i < STEPS; ++i) {
+      const uint64_t g = gidx(i);
+      const uint32_t skip = RECOVER ? ((i < 32 ? bad_lo >> i : bad_hi >> (i - 32)) & 1u) : 0u;
+      bool on = lane_on && g < a.n_groups && !skip && i < NL;
+      uint8_t* d = dst(on ? g : 0, on);
+      if (on) st16t<true>(d, s_par[i][tid]);
     }
     if constexpr (RS > 0) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const uint64_t g = gidx(STEPS + j);
         bool on = ((ron[j / 32] >> (j % 32)) & 1u) != 0u;
-        uint8_t* d = dst(on ? g : 0, STEPS + j, on);
+        uint8_t* d = dst(on ? g : 0, on);
         if (on) st16t<true>(d, racc[j]);
       }
     }
@@ -1506,14 +1487,17 @@ __global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
 
 // The small-batch service worker (qfec_internal.h SvcJob / SvcShared): ONE
 // workgroup of kSvcWaves waves, resident while batches keep coming.  Thread 0
-// polls the host-mapped pub_end; every published group is then taken by one
-// wave (window_group, as the small-batch kernel); after a barrier every
-// thread's outputs are made visible system-wide and thread 0 stores each
-// finished job's token into its flag.  Host memory is read through a
-// system-scope acquire after each poll (a resident kernel gets no cache
-// invalidation from a dispatch: the tables and payloads of a reused slot
-// buffer would otherwise be read stale).  Exit: idle_ticks without work, or
-// quit.  All control stores are vector stores.
+// polls the host-mapped pub_end; for every published job the workgroup copies
+// the job's ring entry -- its header AND its index tables, which the host
+// writes inline (round 5) -- into LDS in one PCIe round trip, and each group
+// is then taken by one wave (window_group, as the small-batch kernel) with
+// its tables read from LDS: a group costs one dependent PCIe round trip (its
+// payload bytes) instead of three (group scalars -> packet table -> bytes,
+// round 4).  After a barrier every thread's outputs are made visible
+// system-wide and thread 0 stores the job's token into its flag.  Host
+// memory is read after a system-scope acquire following each poll (a
+// resident kernel gets no cache invalidation from a dispatch).  Exit:
+// idle_ticks without work, or quit.  All control stores are vector stores.
 constexpr int kSvcWaves = 8;
 
 __device__ __forceinline__ uint64_t svc_load64(const uint64_t* p) {
@@ -1523,6 +1507,15 @@ __device__ __forceinline__ uint32_t svc_load32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The ring entry's first `bytes` bytes (a multiple of 16) into LDS, every
+// thread 16 B per pass (the tables follow the header: one round trip).
+__device__ __forceinline__ void svc_copy_entry(const SvcJob* e, uint8_t* dst, uint32_t from,
+                                               uint32_t bytes) {
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(e);
+  for (uint32_t o = from + 16u * threadIdx.x; o < bytes; o += 16u * 64u * kSvcWaves)
+    *reinterpret_cast<u32x4*>(dst + o) = ld16(src + o);
+}
+
 __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShared* sh,
                                                                         const SvcJob* ring,
                                                                         uint32_t* flags,
@@ -1530,10 +1523,15 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
   __shared__ uint32_t s_par[kSvcWaves][4 * kParWin];
   __shared__ uint64_t s_head[kSvcWaves][kParWin];
   __shared__ u32x4 s_meta[kSvcWaves][64];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
   __shared__ uint32_t s_job, s_exit;
+  static_assert(sizeof(SvcJob) % 16u == 0u, "entry copied in 16-B pieces");
+  constexpr uint32_t kHead = (uint32_t)offsetof(SvcJob, tab);
+  constexpr uint32_t kFirst = 4096u;  // first pass: the header and the first tables
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+  const SvcJob& J = *reinterpret_cast<const SvcJob*>(s_ent);
   if (tid == 0) {
     // where the previous worker stopped: jobs are finished whole and in
     // order, so the next job's number is the count finished
@@ -1568,7 +1566,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
           __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
-        __builtin_amdgcn_s_sleep(16);
+        __builtin_amdgcn_s_sleep(2);
         to = svc_load64(&sh->pub_end);
       }
       s_to = to;
@@ -1576,52 +1574,60 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
     }
     __syncthreads();
     if (s_exit) break;
-    // every thread: drop cached copies of host memory (slot tables, payloads)
+    // every thread: drop cached copies of host memory (ring entries, payloads)
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    const uint64_t from = s_from, to = s_to;
-    uint32_t j = s_job;  // wave-uniform: the job holding the next group
+    const uint64_t to = s_to;
+    uint64_t gi = s_from;
+    uint32_t jj = s_job;
     bool miss = false;
-    for (uint64_t gi = from + wv; gi < to; gi += kSvcWaves) {
-      const SvcJob* jb = ring + (j % kSvcRing);
-      uint32_t hops = 0;  // bounded: a group outside every ring entry
-      while ((jb->seq != j || gi < jb->start || gi >= jb->start + jb->a.n_groups) &&
-             hops < kSvcRing) {
-        ++j;
-        ++hops;
-        jb = ring + (j % kSvcRing);
-      }
-      if (hops == kSvcRing) {  // a malformed ring: nothing of this turn is done
+    while (gi < to) {  // the published jobs, in order (pub_end moves by whole jobs)
+      const SvcJob* e = ring + (jj % kSvcRing);
+      svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
+      __syncthreads();
+      if (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab) {
+        // a malformed ring: nothing of this turn is done
         miss = true;
         break;
       }
-      const uint64_t g = gi - jb->start;
-      if (jb->recover)
-        window_group<true, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-      else
-        window_group<false, true, 16>(jb->a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+      if (kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
+        svc_copy_entry(e, s_ent, kFirst, (kHead + J.tab_bytes + 15u) & ~15u);
+        __syncthreads();
+      }
+      // the job's tables live in LDS now (generic pointers: flat loads)
+      RaggedArgs a = J.a;
+      a.pkt_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_off);
+      a.pkt_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_len);
+      a.grp_ptr = reinterpret_cast<const uint32_t*>(J.tab + J.t_ptr);
+      a.parity_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_poff);
+      if (J.recover) {
+        a.parity_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_plen);
+        a.missing = J.tab + J.t_miss;
+        a.out_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_ooff);
+      }
+      for (uint64_t g = wv; g < J.a.n_groups; g += kSvcWaves) {
+        if (J.recover)
+          window_group<true, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+        else
+          window_group<false, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+      }
+      __threadfence_system();  // every output visible before the token
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(flags + J.flag_slot, J.token, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      gi = J.start + J.a.n_groups;
+      ++jj;
+      __syncthreads();  // s_ent is the next job's
     }
-    if (miss && lane == 0u) s_exit = 1u;  // benign race: every writer stores 1
-    __threadfence_system();  // every output visible before any token
-    __syncthreads();
-    if (s_exit) {
-      // ring miss: latch the fault and leave WITHOUT a
-      // token -- the host's wait sees the stream drained and the fault word
-      // and fails the job instead of reporting stale output as finished
+    if (miss) {
+      // latch the fault and leave WITHOUT this job's token -- the host's wait
+      // sees the stream drained and the fault word and fails the job instead
+      // of reporting stale output as finished
       if (tid == 0)
         __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     if (tid == 0) {
-      // every job published below `to` is finished (a ring entry not yet
-      // rewritten for job jj still carries job jj - kSvcRing: its seq says so)
-      uint32_t jj = s_job;
-      for (;;) {
-        const SvcJob* jb = ring + (jj % kSvcRing);
-        if (jb->seq != jj || jb->start >= to) break;
-        __hip_atomic_store(flags + jb->flag_slot, jb->token, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        ++jj;
-      }
       s_job = jj;
       s_from = to;
       __hip_atomic_store(&sh->consumed, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
