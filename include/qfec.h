@@ -443,6 +443,13 @@ int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
  * measurement hook; the service is on by default.  Any failed service job
  * turns the service off for the context (small batches then launch). */
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
+/* Measurement hook of the service: on = 1 / 0 makes the worker record
+ * 100-MHz wall-clock stamps of each job it finishes (-1 leaves the
+ * setting); stamps (may be NULL, 6 entries) receives the last job's: work
+ * seen, ring entry and tables in LDS, wave 0's first group done, every group
+ * done, outputs made visible, token stored.  (Worker launched by a later
+ * job picks the setting up at its start.) */
+int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

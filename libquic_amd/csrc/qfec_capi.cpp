@@ -129,6 +129,8 @@ struct qfec_ctx {
   qfec::SvcShared* svc_sh_dev = nullptr;
   qfec::SvcJob* svc_ring = nullptr;   // host-mapped job ring
   qfec::SvcJob* svc_ring_dev = nullptr;
+  qfec::SvcDev* svc_dev = nullptr;  // the workers' device-memory words
+  uint32_t svc_epoch = 0;           // launches of the worker (its leader's tag)
   uint64_t svc_published = 0;
   uint32_t svc_seq = 0;
   uint64_t svc_launches = 0;
@@ -270,6 +272,8 @@ int ensure_service(qfec_ctx* ctx) {
   for (uint32_t i = 0; i < qfec::kSvcRing; ++i) ctx->svc_ring[i].seq = 0xFFFFFFFFu;  // none yet
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_sh_dev), ctx->svc_sh, 0));
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_ring_dev), ctx->svc_ring, 0));
+  QFEC_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->svc_dev), sizeof(qfec::SvcDev)));
+  QFEC_HIP(ctx, hipMemset(ctx->svc_dev, 0, sizeof(qfec::SvcDev)));
   QFEC_HIP(ctx, hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
   return QFEC_OK;
 }
@@ -320,8 +324,9 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
   if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) == 0u) {
     __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
-    const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_ring_dev,
-                                                     ctx->h_flag_dev, kSvcIdleTicks,
+    const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev,
+                                                     ctx->svc_ring_dev, ctx->h_flag_dev,
+                                                     kSvcIdleTicks, ++ctx->svc_epoch,
                                                      ctx->svc_stream);
     if (e != hipSuccess) {
       // no worker runs (none was alive): take the job back, so that no later
@@ -1004,6 +1009,7 @@ void qfec_destroy(qfec_ctx* ctx) {
   if (ctx->svc_stream) (void)hipStreamDestroy(ctx->svc_stream);
   if (ctx->svc_sh) (void)hipHostFree(ctx->svc_sh);
   if (ctx->svc_ring) (void)hipHostFree(ctx->svc_ring);
+  if (ctx->svc_dev) (void)hipFree(ctx->svc_dev);
   for (auto& s : ctx->slots) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -1991,6 +1997,17 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
     stats[1] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->jobs, __ATOMIC_ACQUIRE) : 0;
     stats[2] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) : 0;
   }
+  return QFEC_OK;
+}
+
+int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  int rc = ensure_service(ctx);
+  if (rc) return rc;
+  if (on >= 0) __atomic_store_n(&ctx->svc_sh->stamp_on, on ? 1u : 0u, __ATOMIC_SEQ_CST);
+  if (stamps)
+    for (int q = 0; q < 6; ++q)
+      stamps[q] = __atomic_load_n(&ctx->svc_sh->stamps[q], __ATOMIC_ACQUIRE);
   return QFEC_OK;
 }
 

@@ -118,11 +118,29 @@ struct SvcShared {
   uint64_t jobs;      // worker: jobs finished (stats)
   uint32_t fault;     // worker: a published group lay in no ring entry; it left
                       // without finishing (no token for any job of that turn)
-  uint32_t pad;
+  uint32_t stamp_on;  // host (measurement hook): the worker records stamps[] for each job
+  // 100-MHz wall-clock stamps of the last job (qfec_debug_service_stamps):
+  // [0] work seen, [1] entry in LDS, [2] wave 0's first group done, [3] every
+  // group done, [4] outputs visible (fence), [5] token stored
+  uint64_t stamps[8];
 };
 constexpr uint32_t kSvcRing = 8;
-hipError_t launch_ragged_service(SvcShared* sh, const SvcJob* ring, uint32_t* flags,
-                                 uint64_t idle_ticks, hipStream_t s);
+// Round 5: the worker is kSvcWgs workgroups.  Workgroup 0 (the leader) polls
+// the host's pub_end and runs the alive / exit protocol above; it hands each
+// turn's end to the others (followers) through SvcDev in device memory, so
+// only the leader's decisions reach the host.  A job of more groups than one
+// workgroup has waves is split over every workgroup; each adds itself to its
+// ring entry's done counter after making its outputs visible and the last one
+// stores the token.  Smaller jobs are the leader's alone.
+constexpr uint32_t kSvcWgs = 8;
+struct SvcDev {
+  uint64_t to;               // leader: the turn's published end (followers work up to it)
+  uint32_t ready;            // leader: this launch's epoch once `to` is valid
+  uint32_t exit;             // leader: this launch's epoch when the workers leave
+  uint32_t done[kSvcRing];   // workgroups finished per ring entry (kSvcWgs per split job)
+};
+hipError_t launch_ragged_service(SvcShared* sh, SvcDev* dv, const SvcJob* ring, uint32_t* flags,
+                                 uint64_t idle_ticks, uint32_t epoch, hipStream_t s);
 
 // Packet protection batch (qpp_kernels.hip): packet p's associated data (the
 // packet header) is ad_len[p] bytes at bytes + ad_off[p], its input payload

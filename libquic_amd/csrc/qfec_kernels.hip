@@ -1485,19 +1485,24 @@ __global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
   ragged_signal_done(a);
 }
 
-// The small-batch service worker (qfec_internal.h SvcJob / SvcShared): ONE
-// workgroup of kSvcWaves waves, resident while batches keep coming.  Thread 0
-// polls the host-mapped pub_end; for every published job the workgroup copies
-// the job's ring entry -- its header AND its index tables, which the host
-// writes inline (round 5) -- into LDS in one PCIe round trip, and each group
-// is then taken by one wave (window_group, as the small-batch kernel) with
-// its tables read from LDS: a group costs one dependent PCIe round trip (its
-// payload bytes) instead of three (group scalars -> packet table -> bytes,
-// round 4).  After a barrier every thread's outputs are made visible
-// system-wide and thread 0 stores the job's token into its flag.  Host
-// memory is read after a system-scope acquire following each poll (a
-// resident kernel gets no cache invalidation from a dispatch).  Exit:
-// idle_ticks without work, or quit.  All control stores are vector stores.
+// The small-batch service worker (qfec_internal.h SvcJob / SvcShared /
+// SvcDev): kSvcWgs workgroups of kSvcWaves waves, resident while batches keep
+// coming.  The leader's thread 0 polls the host-mapped pub_end and hands the
+// turn's end to the followers through device memory; for every published job
+// each workgroup copies the job's ring entry -- its header AND its index
+// tables, which the host writes inline -- into LDS in one PCIe round trip,
+// and each group is then taken by one wave (window_group, as the small-batch
+// kernel) with its tables read from LDS: a group costs one dependent PCIe
+// round trip (its payload bytes) instead of three (group scalars -> packet
+// table -> bytes, round 4).  A job of at most kSvcWaves groups is the
+// leader's alone; a larger one is spread over all kSvcWgs x kSvcWaves waves
+// (one round of groups for up to 64), each workgroup making its outputs
+// visible system-wide before it adds itself to the entry's done counter, and
+// the last one stores the token.  Host memory is read after a system-scope
+// acquire following each poll (a resident kernel gets no cache invalidation
+// from a dispatch).  Exit: idle_ticks without work, or quit (the leader
+// decides; the followers leave on its word).  All control stores are vector
+// stores.
 constexpr int kSvcWaves = 8;
 
 __device__ __forceinline__ uint64_t svc_load64(const uint64_t* p) {
@@ -1516,58 +1521,89 @@ __device__ __forceinline__ void svc_copy_entry(const SvcJob* e, uint8_t* dst, ui
     *reinterpret_cast<u32x4*>(dst + o) = ld16(src + o);
 }
 
-__global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShared* sh,
-                                                                        const SvcJob* ring,
-                                                                        uint32_t* flags,
-                                                                        uint64_t idle_ticks) {
+__global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
+    SvcShared* sh, SvcDev* dv, const SvcJob* ring, uint32_t* flags, uint64_t idle_ticks,
+    uint32_t epoch) {
   __shared__ uint32_t s_par[kSvcWaves][4 * kParWin];
   __shared__ uint64_t s_head[kSvcWaves][kParWin];
   __shared__ u32x4 s_meta[kSvcWaves][64];
   __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
-  __shared__ uint32_t s_job, s_exit;
+  __shared__ uint32_t s_job, s_exit, s_stamp;
   static_assert(sizeof(SvcJob) % 16u == 0u, "entry copied in 16-B pieces");
   constexpr uint32_t kHead = (uint32_t)offsetof(SvcJob, tab);
   constexpr uint32_t kFirst = 4096u;  // first pass: the header and the first tables
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t wg = blockIdx.x;
+  const bool lead = wg == 0u;
   const SvcJob& J = *reinterpret_cast<const SvcJob*>(s_ent);
+  uint64_t st[6];  // measurement hook (sh->stamp_on): the leader's stamps of a job
   if (tid == 0) {
-    // where the previous worker stopped: jobs are finished whole and in
-    // order, so the next job's number is the count finished
+    // where the previous worker stopped (stable: it has left): jobs are
+    // finished whole and in order, so the next job's number is the count
     s_from = svc_load64(&sh->consumed);
     s_job = (uint32_t)svc_load64(&sh->jobs);
-    // running: a worker queued behind one that cleared `alive` on its way out
-    // says so itself (the host then stops it before a phased launch)
-    __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_stamp = lead ? svc_load32(&sh->stamp_on) : 0u;
+    if (lead) {
+      __hip_atomic_store(&dv->to, s_from, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dv->ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      // running: a worker queued behind one that cleared `alive` on its way
+      // out says so itself (the host then stops it before a phased
+      // launch)
+      __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
   for (;;) {
     if (tid == 0) {
       const uint64_t from = s_from;
-      uint64_t to = svc_load64(&sh->pub_end);
-      uint64_t t0 = wall_clock64();
+      uint64_t to = from;
       uint32_t ex = 0;
-      while (to == from) {
-        if (svc_load32(&sh->quit) != 0u) {
-          ex = 1;
-          break;
-        }
-        if (wall_clock64() - t0 > idle_ticks) {
-          // leaving: say so, then look once more (the host publishes, then
-          // reads alive: one of the two sees the other's store)
-          __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-          __atomic_thread_fence(__ATOMIC_SEQ_CST);
-          to = svc_load64(&sh->pub_end);
-          if (to == from) {
+      if (lead) {
+        to = svc_load64(&sh->pub_end);
+        const uint64_t t0 = wall_clock64();
+        while (to == from) {
+          if (svc_load32(&sh->quit) != 0u) {
             ex = 1;
             break;
           }
-          __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
+          if (wall_clock64() - t0 > idle_ticks) {
+            // leaving: say so, then look once more (the host publishes, then
+            // reads alive: one of the two sees the other's store)
+            __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            to = svc_load64(&sh->pub_end);
+            if (to == from) {
+              ex = 1;
+              break;
+            }
+            __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          to = svc_load64(&sh->pub_end);
         }
-        __builtin_amdgcn_s_sleep(2);
-        to = svc_load64(&sh->pub_end);
+        if (ex)
+          __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_store(&dv->to, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        st[0] = wall_clock64();
+      } else {
+        // follower: the leader's word, from device memory (exit read first:
+        // a `to` stored before the exit is then seen and finished first)
+        for (;;) {
+          const uint32_t e = __hip_atomic_load(&dv->exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if (__hip_atomic_load(&dv->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+            to = __hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (to > from) break;
+          }
+          if (e == epoch) {
+            ex = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
       }
       s_to = to;
       s_exit = ex;
@@ -1586,36 +1622,61 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
       __syncthreads();
       if (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab) {
         // a malformed ring: nothing of this turn is done
+        // (every workgroup reads the same entry and stops here too)
         miss = true;
         break;
       }
-      if (kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
-        svc_copy_entry(e, s_ent, kFirst, (kHead + J.tab_bytes + 15u) & ~15u);
+      const uint64_t n = J.a.n_groups;
+      const bool split = n > (uint64_t)kSvcWaves;
+      if (split || lead) {
+        if (kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
+          svc_copy_entry(e, s_ent, kFirst, (kHead + J.tab_bytes + 15u) & ~15u);
+          __syncthreads();
+        }
+        if (tid == 0) st[1] = wall_clock64();
+        // the job's tables live in LDS now (generic pointers: flat loads)
+        RaggedArgs a = J.a;
+        a.pkt_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_off);
+        a.pkt_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_len);
+        a.grp_ptr = reinterpret_cast<const uint32_t*>(J.tab + J.t_ptr);
+        a.parity_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_poff);
+        if (J.recover) {
+          a.parity_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_plen);
+          a.missing = J.tab + J.t_miss;
+          a.out_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_ooff);
+        }
+        // split: group g on wave g / kSvcWgs of workgroup g % kSvcWgs (a
+        // 9..64-group job is one round, spread over the workgroups)
+        const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
+        for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
+          if (J.recover)
+            window_group<true, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+          else
+            window_group<false, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+          if (tid == 0 && g == 0) st[2] = wall_clock64();
+        }
         __syncthreads();
+        if (tid == 0) st[3] = wall_clock64();
+        __threadfence_system();  // this workgroup's outputs visible before its count
+        __syncthreads();
+        if (tid == 0) {
+          st[4] = wall_clock64();
+          bool last = true;
+          if (split)
+            last = (__hip_atomic_fetch_add(&dv->done[jj % kSvcRing], 1u, __ATOMIC_ACQ_REL,
+                                           __HIP_MEMORY_SCOPE_SYSTEM) +
+                    1u) % kSvcWgs == 0u;
+          if (last)
+            __hip_atomic_store(flags + J.flag_slot, J.token, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          if (s_stamp) {
+            st[5] = wall_clock64();
+            for (int q = 0; q < 6; ++q)
+              __hip_atomic_store(&sh->stamps[q], st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
       }
-      // the job's tables live in LDS now (generic pointers: flat loads)
-      RaggedArgs a = J.a;
-      a.pkt_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_off);
-      a.pkt_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_len);
-      a.grp_ptr = reinterpret_cast<const uint32_t*>(J.tab + J.t_ptr);
-      a.parity_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_poff);
-      if (J.recover) {
-        a.parity_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_plen);
-        a.missing = J.tab + J.t_miss;
-        a.out_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_ooff);
-      }
-      for (uint64_t g = wv; g < J.a.n_groups; g += kSvcWaves) {
-        if (J.recover)
-          window_group<true, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-        else
-          window_group<false, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-      }
-      __threadfence_system();  // every output visible before the token
-      __syncthreads();
-      if (tid == 0)
-        __hip_atomic_store(flags + J.flag_slot, J.token, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      gi = J.start + J.a.n_groups;
+      gi = J.start + n;
       ++jj;
       __syncthreads();  // s_ent is the next job's
     }
@@ -1623,15 +1684,19 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(SvcShare
       // latch the fault and leave WITHOUT this job's token -- the host's wait
       // sees the stream drained and the fault word and fails the job instead
       // of reporting stale output as finished
-      if (tid == 0)
+      if (tid == 0 && lead) {
         __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
       break;
     }
     if (tid == 0) {
       s_job = jj;
       s_from = to;
-      __hip_atomic_store(&sh->consumed, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&sh->jobs, (uint64_t)jj, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lead) {
+        __hip_atomic_store(&sh->consumed, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&sh->jobs, (uint64_t)jj, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
     __syncthreads();
   }
@@ -1976,10 +2041,10 @@ hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t 
   return hipGetLastError();
 }
 
-hipError_t launch_ragged_service(SvcShared* sh, const SvcJob* ring, uint32_t* flags,
-                                 uint64_t idle_ticks, hipStream_t s) {
-  hipLaunchKernelGGL(ragged_service_kernel, dim3(1), dim3(64 * kSvcWaves), 0, s, sh, ring, flags,
-                     idle_ticks);
+hipError_t launch_ragged_service(SvcShared* sh, SvcDev* dv, const SvcJob* ring, uint32_t* flags,
+                                 uint64_t idle_ticks, uint32_t epoch, hipStream_t s) {
+  hipLaunchKernelGGL(ragged_service_kernel, dim3(kSvcWgs), dim3(64 * kSvcWaves), 0, s, sh, dv,
+                     ring, flags, idle_ticks, epoch);
   return hipGetLastError();
 }
 

@@ -104,6 +104,7 @@ SIGNATURES = [
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_debug_service", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
+    ("qfec_debug_service_stamps", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
     ("qfec_complete_ticket", C.c_int, [_vp, C.c_uint64, C.c_int]),
@@ -444,6 +445,13 @@ class Context:
         mode = 2 if poison_next else (-1 if on is None else int(bool(on)))
         self._check(self.lib.qfec_debug_service(self.ctx, mode, st))
         return {"launches": st[0], "jobs": st[1], "alive": st[2]}
+
+    def debug_service_stamps(self, on=None):
+        """Measurement hook: the worker's wall-clock stamps (10-ns ticks) of
+        the last job: seen, entry, first group, all groups, fence, token."""
+        st = (C.c_uint64 * 6)()
+        self._check(self.lib.qfec_debug_service_stamps(self.ctx, -1 if on is None else int(bool(on)), st))
+        return list(st)
 
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""

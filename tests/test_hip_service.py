@@ -1,6 +1,8 @@
 """GPU tests of the small-batch service (round 4; qfec_capi.cpp svc_submit,
 qfec_kernels.hip ragged_service_kernel): QFEC_PTR_MAPPED ragged batches of at
-most 16 groups are taken by ONE resident worker workgroup from a job ring in
+most 64 groups (round 5; 16 in round 4) are taken by a resident worker (8
+workgroups since round 5: a leader that polls the host and followers that
+take a share of any job of more than 8 groups) from a job ring in
 host-mapped memory instead of a kernel launch each.  The worker leaves after
 100 us without work and the next batch relaunches it (the host publishes, then
 reads the worker's alive word; the worker clears it, then reads the published
@@ -46,6 +48,31 @@ def test_service_parity_across_idle_exits():
         st = ctx.debug_service()
         assert st["jobs"] >= calls, st
         assert st["launches"] >= 5, st  # idle exits (1-4 ms pauses) and relaunches
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("n", [8, 9, 17, 33, 63, 64])
+def test_service_split_jobs(n):
+    """Round 5: a job of more than 8 groups is spread over the worker's 8
+    workgroups (each adds itself to the entry's done counter after its
+    outputs are visible; the last stores the token).  Exact for every split
+    size, many times over (the counters wrap by ring entry), mixed with
+    1-group jobs the leader takes alone, across idle exits."""
+    ctx = qfec.Context(0)
+    try:
+        z, want_l = _mapped_case(n, g0=40000 + n, kmin=2, kmax=16, lmin=1, lmax=1452, seed=n)
+        z1, want_1 = _mapped_case(1, g0=41000 + n, kmin=2, kmax=16, lmin=1, lmax=1452, seed=n + 1)
+        before = ctx.debug_service()
+        for it in range(24):
+            _check(ctx, z, want_l)
+            if it % 3 == 0:
+                _check(ctx, z1, want_1)
+            if it % 8 == 7:
+                time.sleep(0.002)  # past the idle exit: a fresh worker (new epoch)
+        st = ctx.debug_service()
+        assert st["jobs"] >= before["jobs"] + 2 * 24 + 2 * 8, st
+        assert st["launches"] >= before["launches"] + 3, st
     finally:
         ctx.close()
 

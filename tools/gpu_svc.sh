@@ -7,6 +7,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_hip_service.py tests/test_hip_mapped.py tests/test_connection.py tests/test_connection_e2e.py tests/test_hip_ragged.py -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -n 40 "$OUT/pytest.log"; exit 1; }
 tail -n 2 "$OUT/pytest.log"
+timeout -k 10 240 python -u tools/svc_stamps.py > "$OUT/stamps.txt" 2>&1 || { tail -n 30 "$OUT/stamps.txt"; exit 1; }
+cat "$OUT/stamps.txt"
 timeout -k 10 600 python -u bench.py --groups 65536 --steps 2 --warmup 1 --no-ragged --no-protect --no-entropy --no-fused --no-e2e --no-ceilings --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -n 30 "$OUT/bench.err"; exit 1; }
 python3 -c "
 import json; l=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1])
