@@ -848,6 +848,9 @@ __device__ __forceinline__ Acc2 rw3_batch(Acc2 acc, uint32_t lane, uint32_t j0, 
     v[j] = rw3_ld(r, vo0);
     if constexpr (S1) w[j] = rw3_ld(r, vo1);
   }
+  // every load of the batch issued before the first XOR (the scheduler,
+  // near the register limit, interleaved them with vmcnt(0..3) waits)
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int j = 0; j < N; ++j) acc.a0 ^= v[j];
   if constexpr (S1) {
@@ -879,25 +882,28 @@ __device__ __forceinline__ Acc2 rw3_batch_n(uint32_t n, Acc2 acc, uint32_t lane,
 
 // Lane j's input (address, len): its partial last window (bytes 16*(len>>4)
 // .. len-1 at positions 0 .. len%16-1, zero above); zero when len % 16 == 0.
-__device__ __forceinline__ u32x4 rw3_partial(uint64_t base, uint32_t len) {
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  const uint32_t rem = len & 15u;
-  if (rem == 0u) return zero;
+// Issued without a branch (a per-lane branch around the load made the
+// compiler wait for it right there: a round trip per group) and finished
+// later: in place when the window starts on a 16-B boundary (cannot leave
+// the page of the input's byte there), else the 16 bytes ending at len
+// (len >= 16: the caller sends groups with an unaligned input below 16 B
+// down the exact input-by-input path).
+__device__ __forceinline__ u32x4 rw3_partial_issue(uint64_t base, uint32_t len, bool on,
+                                                   uint64_t any) {
+  // (a lane without an input loads the first input's first bytes: `any`)
   const uint64_t pa = base + (len & ~15u);
-  u32x4 v;
-  if ((pa & 15u) == 0u) {
-    // in place (aligned: cannot leave the page of the input's byte pa)
-    v = ldg16(pa);
-    v.x &= keep_dw(rem, 0);
-    v.y &= keep_dw(rem, 1);
-    v.z &= keep_dw(rem, 2);
-    v.w &= keep_dw(rem, 3);
-  } else if (len >= 16u) {
-    v = shr_bytes_bf(ldg16(base + len - 16u), 16u - rem);
-  } else {
-    v = window16_small(reinterpret_cast<const uint8_t*>(base), len, 0u);
-  }
-  return v;
+  const bool inpl = (pa & 15u) == 0u;
+  const uint64_t at = !on ? any : (inpl ? pa : base + len - 16u);
+  return ldg16(at);
+}
+__device__ __forceinline__ u32x4 rw3_partial_finish(u32x4 v, uint64_t base, uint32_t len, bool on) {
+  const uint32_t rem = len & 15u;
+  const bool inpl = ((base + (len & ~15u)) & 15u) == 0u;
+  const u32x4 sh = shr_bytes_bf(v, (16u - rem) & 15u);
+  const uint32_t k0 = keep_dw(rem, 0), k1 = keep_dw(rem, 1), k2 = keep_dw(rem, 2), k3 = keep_dw(rem, 3);
+  u32x4 r = inpl ? u32x4{v.x & k0, v.y & k1, v.z & k2, v.w & k3} : sh;
+  const uint32_t z = (on && rem != 0u) ? 0xFFFFFFFFu : 0u;
+  return u32x4{r.x & z, r.y & z, r.z & z, r.w & z};
 }
 
 // XOR the table lanes' partial windows into the row in registers (a row not
@@ -918,8 +924,36 @@ __device__ __forceinline__ void rw3_partials_regs(u32x4& a0, u32x4& a1, uint32_t
   }
 }
 
+// v4: set-1 loads (full windows 64..) only for the inputs that have one
+// (len >= 1040, ~1 in 4 of configs[3]'s): table lanes from a ballot mask,
+// at most 4 issued ahead of the set-0 batch, so a group of <= 16 inputs is
+// ONE round trip with 16-B batches of set-0 loads (v3: batches of 8, every
+// input's set-1 load, two round trips for k > 8).
+template <int N1>
+__device__ __forceinline__ void rw4_s1(u32x4 (&w)[4], uint64_t& mask1, uint32_t tlo, uint32_t thi,
+                                       uint32_t tlen, uint32_t vo1) {
+#pragma unroll
+  for (int j = 0; j < N1; ++j) {
+    const uint32_t idx = (uint32_t)__builtin_ctzll(mask1);
+    mask1 &= mask1 - 1ull;
+    const uint32_t len = rdl(tlen, idx);
+    const uint64_t b = ((uint64_t)rdl(thi, idx) << 32) | rdl(tlo, idx);
+    w[j] = rw3_ld(rw3_rsrc(b, len & ~15u), vo1);
+  }
+}
+__device__ __forceinline__ void rw4_s1_n(uint32_t n, u32x4 (&w)[4], uint64_t& mask1, uint32_t tlo,
+                                         uint32_t thi, uint32_t tlen, uint32_t vo1) {
+  switch (n) {
+    case 1: rw4_s1<1>(w, mask1, tlo, thi, tlen, vo1); break;
+    case 2: rw4_s1<2>(w, mask1, tlo, thi, tlen, vo1); break;
+    case 3: rw4_s1<3>(w, mask1, tlo, thi, tlen, vo1); break;
+    case 4: rw4_s1<4>(w, mask1, tlo, thi, tlen, vo1); break;
+    default: break;
+  }
+}
+
 // Reduce; hold = the LDS row (16-B units) the partials go to, or ~0: registers.
-template <bool RECOVER, int B>
+template <bool RECOVER, int B, bool V4 = false>
 __device__ __forceinline__ uint32_t rw3_reduce(const RaggedArgs& a, const RwS& s, uint32_t lane,
                                                uint32_t tlo, uint32_t thi, uint32_t tlen,
                                                u32x4& a0, u32x4& a1, u32x4& pw, bool& deferred) {
@@ -955,21 +989,57 @@ __device__ __forceinline__ uint32_t rw3_reduce(const RaggedArgs& a, const RwS& s
     }
     mx = max(mx, tlen);
     const uint32_t cn = min(nin - c0, 64u);
-    const bool s1 = wave_any(r < nin && tlen > 1040u);
-    // this chunk's partial windows: one load per lane
-    pw = r < nin ? rw3_partial(((uint64_t)thi << 32) | tlo, tlen) : zero;
+    const bool s1 = wave_any(r < nin && tlen >= 1040u);  // a full window 64 (bytes 1024..1039)
+    // this chunk's partial windows: one load per lane, finished after the XORs
+    const uint64_t tb = ((uint64_t)thi << 32) | tlo;
+    const bool small = wave_any(r < nin && tlen < 16u && (tlo & 15u) != 0u);
+    if (small) {
+      // an unaligned input below 16 B (rare): input by input, exact windows
+      for (uint32_t j = 0; j < cn; ++j) {
+        const uint32_t ln = rdl(tlen, j);
+        const uint8_t* bp = reinterpret_cast<const uint8_t*>(((uint64_t)rdl(thi, j) << 32) | rdl(tlo, j));
+        if (16u * lane < ln) a0 ^= packet_window<true>(bp, ln, lane);
+        if (16u * (64u + lane) < ln) a1 ^= packet_window<true>(bp, ln, 64u + lane);
+      }
+      if (nin > 64u) continue;
+      pw = zero;
+      deferred = true;
+      continue;
+    }
+    const u32x4 praw = rw3_partial_issue(tb, tlen, r < nin, ((uint64_t)rdl(thi, 0u) << 32) | rdl(tlo, 0u));
     const uint32_t nb = (cn + (uint32_t)B - 1u) / (uint32_t)B;
     const uint32_t base = cn / nb, extra = cn - base * nb;
     uint32_t j0 = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t n = base + (b < extra ? 1u : 0u);
-      Acc2 acc{a0, a1};
-      acc = s1 ? rw3_batch_n<true, B>(n, acc, lane, j0, tlo, thi, tlen)
-               : rw3_batch_n<false, B>(n, acc, lane, j0, tlo, thi, tlen);
-      a0 = acc.a0;
-      a1 = acc.a1;
-      j0 += n;
+    if constexpr (V4) {
+      const uint32_t vo1 = 16u * (64u + lane);
+      uint64_t mask1 = __ballot(r < nin && tlen >= 1040u);
+      u32x4 w[4] = {zero, zero, zero, zero};
+      rw4_s1_n(min((uint32_t)__popcll(mask1), 4u), w, mask1, tlo, thi, tlen, vo1);
+      for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t n = base + (b < extra ? 1u : 0u);
+        Acc2 acc{a0, a1};
+        acc = rw3_batch_n<false, B>(n, acc, lane, j0, tlo, thi, tlen);
+        a0 = acc.a0;
+        j0 += n;
+      }
+      a1 ^= w[0] ^ w[1] ^ w[2] ^ w[3];
+      while (mask1 != 0ull) {  // more than 4 long inputs (rare)
+        u32x4 x[4] = {zero, zero, zero, zero};
+        rw4_s1_n(min((uint32_t)__popcll(mask1), 4u), x, mask1, tlo, thi, tlen, vo1);
+        a1 ^= x[0] ^ x[1] ^ x[2] ^ x[3];
+      }
+    } else {
+      for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t n = base + (b < extra ? 1u : 0u);
+        Acc2 acc{a0, a1};
+        acc = s1 ? rw3_batch_n<true, B>(n, acc, lane, j0, tlo, thi, tlen)
+                 : rw3_batch_n<false, B>(n, acc, lane, j0, tlo, thi, tlen);
+        a0 = acc.a0;
+        a1 = acc.a1;
+        j0 += n;
+      }
     }
+    pw = rw3_partial_finish(praw, tb, tlen, r < nin);
     if (nin <= 64u) {
       deferred = true;  // the caller XORs pw into the held row, or into registers
     } else {
@@ -979,7 +1049,7 @@ __device__ __forceinline__ uint32_t rw3_reduce(const RaggedArgs& a, const RwS& s
   return RECOVER ? s.plen : rfl(wave_max11(mx));
 }
 
-template <bool RECOVER, int NW, int DIAG = 0, int B = (NW > 8 ? 8 : 16)>
+template <bool RECOVER, int NW, int DIAG = 0, int B = (NW > 8 ? 8 : 16), bool V4 = false>
 __global__ __launch_bounds__(64 * NW) void ragged_rpw3_kernel(RaggedArgs a, const uint32_t* bnd,
                                                               uint32_t nphase, uint32_t* phase_sync) {
   __shared__ u32x4 s_hold[kRwHoldW];
@@ -1020,11 +1090,13 @@ __global__ __launch_bounds__(64 * NW) void ragged_rpw3_kernel(RaggedArgs a, cons
       __builtin_amdgcn_sched_barrier(0);
       u32x4 a0, a1, pw;
       bool deferred;
-      const uint32_t plen = rw3_reduce<RECOVER, B>(a, s0, lane, tlo0, thi0, tlen0, a0, a1, pw, deferred);
+      const uint32_t plen = rw3_reduce<RECOVER, B, V4>(a, s0, lane, tlo0, thi0, tlen0, a0, a1, pw, deferred);
       if (plen != 0xFFFFFFFFu) {
         const uint32_t nw = (plen + 15u) >> 4;
         const uint32_t e = rfl(atomicAdd(&s_nent, 1u)) / 64u;
-        const uint32_t h = rfl(atomicAdd(&s_alloc, nw)) / 64u;
+        // lane 0 adds nw, the others 0: lane 0's old value is the row whatever
+        // order the LDS takes the lanes in (x64 units assumed lane 0 first)
+        const uint32_t h = rdl(atomicAdd(&s_alloc, lane == 0u ? nw : 0u), 0u);
         const uint64_t d = (uint64_t)(uintptr_t)a.out + s0.doff;
         if (e < kRwEnt && h + nw <= kRwHoldW) {
           if (lane < nw) s_hold[h + lane] = a0;
@@ -1159,14 +1231,14 @@ static void run_rpw2_n(const RaggedArgs& a, uint32_t ppc, bool bounds = true) {
                      (const uint32_t*)g_bnd, nphase, g_sync);
 }
 
-template <bool REC, int NW, int DIAG = 0>
+template <bool REC, int NW, int DIAG = 0, int B = (NW > 8 ? 8 : 16), bool V4 = false>
 static void run_rpw3_n(const RaggedArgs& a, uint32_t ppc, bool bounds = true) {
   const uint32_t nphase = (uint32_t)std::max<uint64_t>(1, (g_total_pk + (uint64_t)ppc * g_ncu - 1) / ((uint64_t)ppc * g_ncu));
   const uint32_t nseg = nphase * g_ncu;
   if (bounds)
     hipLaunchKernelGGL(qfec::rw_bounds_kernel, dim3((nseg + 256) / 256), dim3(256), 0, 0, a.grp_ptr,
                        a.n_groups, nseg, g_bnd);
-  hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<REC, NW, DIAG>), dim3(g_ncu), dim3(64 * NW), 0, 0, a,
+  hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<REC, NW, DIAG, B, V4>), dim3(g_ncu), dim3(64 * NW), 0, 0, a,
                      (const uint32_t*)g_bnd, nphase, g_sync);
 }
 
@@ -1179,13 +1251,13 @@ static void stamps_report(const RaggedArgs& a, uint32_t ppc, const char* tag) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(qfec::g_stamps), &g_stamps_d, sizeof(g_stamps_d)));
   }
   CK(hipMemset(g_stamps_d, 0, nw * 8 * 8));
-  run_rpw3_n<REC, NW, 0>(a, ppc);  // bounds
+  run_rpw3_n<REC, NW, 0, 16, true>(a, ppc);  // bounds
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, 0));
-  run_rpw3_n<REC, NW, 2>(a, ppc, false);
+  run_rpw3_n<REC, NW, 2, 16, true>(a, ppc, false);
   CK(hipEventRecord(e1, 0));
   CK(hipDeviceSynchronize());
   float ms = 0;
@@ -1329,9 +1401,9 @@ int main(int argc, char** argv) {
       std::printf("guard %s: nphase %u nseg %u bounds monotone %d, max groups per segment %zu\n",
                   rec ? "recover" : "encode", nphase, nseg, (int)mono, mx);
       if (!mono) return 4;
-      if (rec) hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<true, 16, 0>), dim3(g_ncu), dim3(1024), 0, 0, a,
+      if (rec) hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<true, 16, 0, 16, true>), dim3(g_ncu), dim3(1024), 0, 0, a,
                                   (const uint32_t*)g_bnd, nphase, g_sync);
-      else hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<false, 16, 0>), dim3(g_ncu), dim3(1024), 0, 0, a,
+      else hipLaunchKernelGGL((qfec::ragged_rpw3_kernel<false, 16, 0, 16, true>), dim3(g_ncu), dim3(1024), 0, 0, a,
                               (const uint32_t*)g_bnd, nphase, g_sync);
       CK(hipGetLastError());
       CK(hipDeviceSynchronize());
@@ -1353,15 +1425,16 @@ int main(int argc, char** argv) {
   }
   std::vector<V> vs;
   vs.push_back({"product block encode", false, BLK(false)});
-  vs.push_back({"rpw3 NW8 P1000 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 8>(a, 1000); }});
   vs.push_back({"rpw3 NW16 P1000 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 16>(a, 1000); }});
-  vs.push_back({"rpw3 NW16 P1150 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 16>(a, 1150); }});
+  vs.push_back({"rpw4 NW16 B16 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 16, 0, 16, true>(a, 1000); }});
+  vs.push_back({"rpw4 NW12 B16 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 12, 0, 16, true>(a, 1000); }});
+  vs.push_back({"rpw4 NW16 B8 encode", false, [](const RaggedArgs& a) { run_rpw3_n<false, 16, 0, 8, true>(a, 1000); }});
   vs.push_back({"product block recover", true, BLK(true)});
-  vs.push_back({"rpw3 NW8 P1000 recover", true, [](const RaggedArgs& a) { run_rpw3_n<true, 8>(a, 1000); }});
-  vs.push_back({"rpw3 NW16 P1000 recover", true, [](const RaggedArgs& a) { run_rpw3_n<true, 16>(a, 1000); }});
+  vs.push_back({"rpw4 NW16 B16 recover", true, [](const RaggedArgs& a) { run_rpw3_n<true, 16, 0, 16, true>(a, 1000); }});
+  vs.push_back({"rpw4 NW12 B16 recover", true, [](const RaggedArgs& a) { run_rpw3_n<true, 12, 0, 16, true>(a, 1000); }});
   std::vector<V> diag;
-  diag.push_back({"rpw3 NW16 P1000 enc, no stores", false,
-                  [](const RaggedArgs& a) { run_rpw3_n<false, 16, 1>(a, 1000); }});
+  diag.push_back({"rpw4 NW16 B16 enc, no stores", false,
+                  [](const RaggedArgs& a) { run_rpw3_n<false, 16, 1, 16, true>(a, 1000); }});
   std::vector<uint8_t> h_ref(OB), h_v(OB);
   std::vector<uint16_t> hp_ref(G), hp_v(G);
   CK(hipMemcpy(hp_ref.data(), plen_ref, G * 2, hipMemcpyDeviceToHost));
