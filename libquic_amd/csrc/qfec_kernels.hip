@@ -1504,6 +1504,11 @@ __global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
 // decides; the followers leave on its word).  All control stores are vector
 // stores.
 constexpr int kSvcWaves = 8;
+// Load slots per trip of a group's bytes: 24 = every window of a group of up
+// to 12 packets longer than 1024 B in ONE PCIe round trip (16 made a
+// 10 x 1350 B group two trips: 20 slots; 238 VGPRs at 2 waves/SIMD; 32
+// spilled)
+constexpr int kSvcPB = 24;
 
 __device__ __forceinline__ uint64_t svc_load64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1650,9 +1655,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
         for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
           if (J.recover)
-            window_group<true, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+            window_group<true, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
           else
-            window_group<false, true, 16>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+            window_group<false, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
           if (tid == 0 && g == 0) st[2] = wall_clock64();
         }
         __syncthreads();
