@@ -1129,8 +1129,28 @@ def _issue_bound(kernel_pred, n, ms):
             for u in ("valu", "lds", "salu"):
                 if f"{u}_busy" in kd:
                     r[f"{u}_busy"] = round(kd[f"{u}_busy"], 4)
+            r.update(_stall_picture(name))
             return r
     return None
+
+
+def _stall_picture(name):
+    """the kernel's issue fractions against the CU's issue
+    ceilings (SIMD-32: a wave64 VALU instruction issues in 2 cycles, 2 per CU
+    per cycle; a 64-lane ds_read_b32 moves 256 B at 128 B per CU per cycle,
+    0.5 per CU per cycle) and where its waves' cycles go (PMC:
+    tools/pmc_aead_stall.sh -> profiles/round5/aead_stall.json)."""
+    path = os.path.join(ROOT, "profiles", "round5", "aead_stall.json")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        kd = json.load(f).get("kernels", {}).get(name)
+    if not kd:
+        return {}
+    keys = ("valu_issue_frac", "lds_issue_frac", "waves_per_simd", "active_any_frac",
+            "wait_any_frac", "wait_inst_any_frac", "wait_lds_frac")
+    return {"stall": {k: round(kd[k], 3) for k in keys if k in kd} |
+            {"source": "profiles/round5/aead_stall.json"}}
 
 
 def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
