@@ -20,7 +20,8 @@ class Params(C.Structure):
                 ("drop_every", C.c_int32), ("stream_len", C.c_uint64), ("batched", C.c_int32),
                 ("max_turns", C.c_int32), ("fail_encode", C.c_int32),
                 ("require_gpu", C.c_int32), ("no_end_flush", C.c_int32), ("reorder", C.c_int32),
-                ("inject_unencrypted_fec", C.c_int32), ("close_mid_batch", C.c_int32)]
+                ("inject_unencrypted_fec", C.c_int32), ("close_mid_batch", C.c_int32),
+                ("fec_option", C.c_int32)]
 
 
 _U64 = ("data_packets_sent fec_packets_sent dropped revived groups_one_loss fec_groups_skipped "
@@ -63,7 +64,8 @@ def lib(cpu_stub=False):
 
 def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True,
         max_turns=20_000, fail_encode=False, require_gpu=False, version=31,
-        end_flush=True, reorder=0, inject_unencrypted_fec=False, close_mid_batch=0, cpu_stub=False) -> dict:
+        end_flush=True, reorder=0, inject_unencrypted_fec=False, close_mid_batch=0, cpu_stub=False,
+        fec_option=0) -> dict:
     """One simulated run; returns the result fields as a dict.  cpu_stub: the
     build whose qfec entry points are the CPU test stub (no GPU needed)."""
     p = Params(version=version, n_pairs=n_pairs, group_size=group_size, drop_every=drop_every,
@@ -71,7 +73,7 @@ def run(n_pairs=1, group_size=10, drop_every=2, stream_len=100_000, batched=True
                fail_encode=int(fail_encode), require_gpu=int(require_gpu),
                no_end_flush=int(not end_flush), reorder=reorder,
                inject_unencrypted_fec=int(inject_unencrypted_fec),
-               close_mid_batch=close_mid_batch)
+               close_mid_batch=close_mid_batch, fec_option=fec_option)
     r = Result()
     lib(cpu_stub).fec_conn_run(C.byref(p), C.byref(r))
     out = {n: getattr(r, n) for n, _ in Result._fields_}

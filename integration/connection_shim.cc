@@ -52,6 +52,8 @@
 #include "net/quic/core/quic_alarm_factory.h"
 #include "net/quic/core/quic_clock.h"
 #include "net/quic/core/quic_connection.h"
+#include "net/quic/core/crypto/crypto_handshake_message.h"
+#include "net/quic/core/quic_config.h"
 #include "net/quic/core/quic_fec_connection.h"
 #include "net/quic/core/quic_flags.h"
 #include "net/quic/core/quic_framer.h"
@@ -77,6 +79,9 @@ struct fec_conn_params {
   int32_t inject_unencrypted_fec;  // 1: client 0 also sends an FEC packet at ENCRYPTION_NONE
   int32_t close_mid_batch;  // T > 0: from turn T, client 0 closes its connection while
                             // one of its FEC packets is pending in the batcher
+  int32_t fec_option;       // 1 / 2: the client sends FEC connection option kFSTR / kFHDR
+                            // (the session's FEC policy; negotiated through QuicConfig and
+                            // applied by SetFromConfig at both ends -- no EnableFecSending)
 };
 
 struct fec_conn_result {
@@ -529,7 +534,7 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
   // the groups go without FEC and the reference's loss recovery delivers the
   // stream — the GPU-failure path, runnable on the CPU.  fail_encode forces
   // that path on a GPU (qfec_debug_fail_launches on the batcher's context).
-  qfec_ctx* ctx = params->group_size > 0 ? qfec_create(0) : nullptr;
+  qfec_ctx* ctx = (params->group_size > 0 || params->fec_option) ? qfec_create(0) : nullptr;
   if (!ctx && params->require_gpu) {
     std::snprintf(r->detail, sizeof(r->detail), "qfec_create: %s", qfec_last_error(nullptr));
     return r->status = 3;
@@ -597,6 +602,25 @@ SHIM_API int fec_conn_run(const fec_conn_params* params, fec_conn_result* r) {
     cc[i]->set_debug_visitor(cwatch[i].get());
     ce[i]->conn = cc[i].get();
     se[i]->conn = sc[i].get();
+    if (params->fec_option) {
+      // the session's FEC policy as a client connection option: the client's
+      // QuicConfig sends it in its CHLO, the server's QuicConfig processes that
+      // hello, and each connection gets its negotiated config as
+      // QuicSession::OnConfigNegotiated hands it over (SetFromConfig)
+      QuicConfig ccfg, scfg;
+      QuicTagVector opts;
+      opts.push_back(params->fec_option == 2 ? kFHDR : kFSTR);
+      ccfg.SetConnectionOptionsToSend(opts);
+      CryptoHandshakeMessage chlo;
+      ccfg.ToHandshakeMessage(&chlo);
+      std::string details;
+      if (scfg.ProcessPeerHello(chlo, CLIENT, &details) != QUIC_NO_ERROR) {
+        std::snprintf(r->detail, sizeof(r->detail), "server config: %s", details.c_str());
+        return r->status = 6;
+      }
+      cc[i]->SetFromConfig(ccfg);
+      sc[i]->SetFromConfig(scfg);
+    }
     if (params->group_size > 0) cc[i]->EnableFecSending(params->group_size);
   }
   if (params->inject_unencrypted_fec && n > 0) {
