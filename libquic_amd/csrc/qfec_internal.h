@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace qfec {
@@ -107,8 +108,35 @@ struct SvcJob {
   uint32_t token;
   uint32_t tab_bytes; // table bytes in tab (<= kSvcTab)
   uint32_t t_off, t_len, t_ptr, t_poff, t_plen, t_miss, t_ooff;  // offsets into tab
+  // Round 5: a job whose header and tables fit the first kSvcHead bytes
+  // carries svc_head_hash of them (this word excluded), stored by the host
+  // LAST; the leader reads those bytes in every poll of the ring, so a job it
+  // finds whole there (hash, seq and start agree) needs no second PCIe round
+  // trip for its entry.  0 for a larger job (then never taken from a poll).
+  uint64_t head_sum;
   alignas(16) uint8_t tab[kSvcTab];
 };
+constexpr uint32_t kSvcHead = 1024;  // bytes of the entry read with every poll (64 x 16 B)
+constexpr uint32_t kSvcHeadSumWord = (uint32_t)(offsetof(SvcJob, head_sum) / 8u);
+static_assert(offsetof(SvcJob, head_sum) % 8u == 0u, "head_sum on a word");
+static_assert(offsetof(SvcJob, tab) < kSvcHead, "the header fits the polled bytes");
+// Order-free sum over the 8-byte words [0, nbytes / 8) of the entry but
+// head_sum's own: each word mixed with its index (splitmix64 finalizer), so a
+// torn read -- some 16-B pieces from before the host's writes -- does not sum
+// to the stored value (host and device compute the same function).
+__host__ __device__ inline uint64_t svc_head_word(uint64_t w, uint32_t i) {
+  uint64_t z = w ^ (0x9E3779B97F4A7C15ull * (uint64_t)(i + 1u));
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline uint64_t svc_head_hash(const SvcJob& j, uint32_t nbytes) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(&j);
+  uint64_t h = 0;
+  for (uint32_t i = 0; i < nbytes / 8u; ++i)
+    if (i != kSvcHeadSumWord) h += svc_head_word(w[i], i);
+  return h | 1ull;  // never 0 (0 = no hash)
+}
 struct SvcShared {
   uint64_t pub_end;   // host: groups published
   uint64_t consumed;  // worker: groups finished (a new worker starts here)

@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   __shared__ u32x4 s_meta[kSvcWaves][64];
   __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
-  __shared__ uint32_t s_job, s_exit, s_stamp;
+  __shared__ uint32_t s_job, s_exit, s_stamp, s_pref;
   static_assert(sizeof(SvcJob) % 16u == 0u, "entry copied in 16-B pieces");
   constexpr uint32_t kHead = (uint32_t)offsetof(SvcJob, tab);
   constexpr uint32_t kFirst = 4096u;  // first pass: the header and the first tables
@@ -1561,57 +1561,95 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   }
   __syncthreads();
   for (;;) {
-    if (tid == 0) {
+    if (lead && wv == 0u) {
+      // The leader's wave 0 polls.  Every look reads pub_end AND the next
+      // job's first kSvcHead bytes (16 per lane, relaxed system-scope loads,
+      // all in flight together: one PCIe round trip); when the look that sees
+      // the job holds it whole -- its head hash, seq and start agree -- the
+      // entry copy below is skipped (round 5: one round trip less per job).
       const uint64_t from = s_from;
-      uint64_t to = from;
+      const uint32_t job0 = s_job;
+      const uint64_t* hp = reinterpret_cast<const uint64_t*>(ring + (job0 % kSvcRing)) + 2u * lane;
+      uint64_t h0 = 0, h1 = 0;
+      auto look = [&]() -> uint64_t {
+        const uint64_t t = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        h0 = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        h1 = __hip_atomic_load(hp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return t;
+      };
+      uint64_t to = look();
       uint32_t ex = 0;
-      if (lead) {
-        to = svc_load64(&sh->pub_end);
-        const uint64_t t0 = wall_clock64();
-        while (to == from) {
-          if (svc_load32(&sh->quit) != 0u) {
+      const uint64_t t0 = wall_clock64();
+      while (to == from) {
+        if (svc_load32(&sh->quit) != 0u) {
+          ex = 1;
+          break;
+        }
+        if (wall_clock64() - t0 > idle_ticks) {
+          // leaving: say so, then look once more (the host publishes, then
+          // reads alive: one of the two sees the other's store)
+          __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+          __atomic_thread_fence(__ATOMIC_SEQ_CST);
+          to = look();
+          if (to == from) {
             ex = 1;
             break;
           }
-          if (wall_clock64() - t0 > idle_ticks) {
-            // leaving: say so, then look once more (the host publishes, then
-            // reads alive: one of the two sees the other's store)
-            __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-            __atomic_thread_fence(__ATOMIC_SEQ_CST);
-            to = svc_load64(&sh->pub_end);
-            if (to == from) {
-              ex = 1;
-              break;
-            }
-            __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-          to = svc_load64(&sh->pub_end);
+          __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
         }
+        __builtin_amdgcn_s_sleep(2);
+        to = look();
+      }
+      if (lane == 0u) {
         if (ex)
           __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         else
           __hip_atomic_store(&dv->to, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t pref = 0;
+      if (!ex) {
+        uint64_t* sw = reinterpret_cast<uint64_t*>(s_ent);
+        sw[2u * lane] = h0;
+        sw[2u * lane + 1u] = h1;
+        wave_lds_order();
+        const uint32_t tbb = J.tab_bytes;
+        const uint32_t nb = kHead + tbb <= kSvcHead ? ((kHead + tbb + 15u) & ~15u) : 0u;
+        uint64_t part = 0;
+        if (2u * lane < nb / 8u && 2u * lane != kSvcHeadSumWord) part += svc_head_word(h0, 2u * lane);
+        if (2u * lane + 1u < nb / 8u && 2u * lane + 1u != kSvcHeadSumWord)
+          part += svc_head_word(h1, 2u * lane + 1u);
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) part += (uint64_t)__shfl_xor((unsigned long long)part, d, 64);
+        pref = (nb != 0u && (part | 1ull) == J.head_sum && J.seq == job0 && J.start == from) ? 1u : 0u;
+      }
+      if (lane == 0u) {
         st[0] = wall_clock64();
-      } else {
-        // follower: the leader's word, from device memory (exit read first:
-        // a `to` stored before the exit is then seen and finished first)
-        for (;;) {
-          const uint32_t e = __hip_atomic_load(&dv->exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          if (__hip_atomic_load(&dv->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
-            to = __hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (to > from) break;
-          }
-          if (e == epoch) {
-            ex = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+        s_to = to;
+        s_exit = ex;
+        s_pref = pref;
+      }
+    } else if (!lead && tid == 0) {
+      // follower: the leader's word, from device memory (exit read first:
+      // a `to` stored before the exit is then seen and finished first)
+      const uint64_t from = s_from;
+      uint64_t to = from;
+      uint32_t ex = 0;
+      for (;;) {
+        const uint32_t e = __hip_atomic_load(&dv->exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_load(&dv->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+          to = __hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if (to > from) break;
         }
+        if (e == epoch) {
+          ex = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
       s_to = to;
       s_exit = ex;
+      s_pref = 0u;
     }
     __syncthreads();
     if (s_exit) break;
@@ -1623,7 +1661,8 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
     bool miss = false;
     while (gi < to) {  // the published jobs, in order (pub_end moves by whole jobs)
       const SvcJob* e = ring + (jj % kSvcRing);
-      svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
+      // (the turn's first job may already be in LDS from the leader's poll)
+      if (!(s_pref != 0u && jj == s_job)) svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
       __syncthreads();
       if (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab) {
         // a malformed ring: nothing of this turn is done
