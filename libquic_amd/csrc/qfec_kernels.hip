@@ -36,6 +36,7 @@
 #include "qfec_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace qfec {
@@ -1375,21 +1376,33 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
 // windows: profiles/round1/sq_stalls_fec_pq.txt, parked 68-78% of cycles).
 // Groups outside the form (more than 64 received packets, a packet < 16 B,
 // any invalid field) run the exact per-group body (ragged_group).
+// a value every lane holds alike, moved to an SGPR
+__device__ __forceinline__ uint32_t uni32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
+}
+
 template <bool RECOVER, bool NT, int PB>
 __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
                                              uint32_t* s_par, uint64_t* s_head, u32x4* s_meta) {
-  // trip 1: the group's scalars (s_load)
-  const uint32_t p0 = a.grp_ptr[g];
-  const uint32_t k = a.grp_ptr[g + 1] - p0;
+  // trip 1: the group's scalars (s_load; the service's tables sit in LDS
+  // behind generic pointers: flat loads into VGPRs, which the compiler takes
+  // for per-lane values -- every slot below then became a waterfall loop
+  // around its load, ~3 us of issue for one group -- so the scalars are
+  // moved to SGPRs explicitly)
+  const uint32_t p0 = uni32(a.grp_ptr[g]);
+  const uint32_t k = uni32(a.grp_ptr[g + 1]) - p0;
   uint32_t m = 0xFFFFFFFFu, plen = 0;
   uint64_t dst_off, par_off = 0;
   if constexpr (RECOVER) {
-    m = a.missing[g];
-    plen = a.parity_len[g];
-    dst_off = a.out_off[g];
-    par_off = a.parity_off[g];
+    m = uni32(a.missing[g]);
+    plen = uni32(a.parity_len[g]);
+    dst_off = uni64(a.out_off[g]);
+    par_off = uni64(a.parity_off[g]);
   } else {
-    dst_off = a.parity_off[g];
+    dst_off = uni64(a.parity_off[g]);
   }
   const uint32_t kr = RECOVER ? k - 1u : k;  // received packets
   const bool form = k >= 1u && k <= 255u && kr <= 64u &&
@@ -1431,50 +1444,100 @@ __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, ui
   // longer than that reach one
   const uint64_t longm = plen > 1024u ? __ballot(lane < kr && len > min(1024u, plen - 16u)) : 0ull;
   const uint32_t ns = kr + (uint32_t)__popcll(longm);
+  // slot tables, lane t describing slots t and t + 64: slot j < kr is packet
+  // j's first window, slot kr + n the second window of the n-th long packet
+  // (the n-th set bit of longm, found by halving), a slot at or past ns none
+  // (length 0).  A slot's load then costs three readlanes and its descriptor.
+  // (One wave issues an instruction every few cycles: the per-slot search
+  // for the next long packet, ~35 instructions a slot, spread a group's 20
+  // loads over ~1.5 us of the service's one-group latency.)
+  auto slot_packet = [&](uint32_t j) -> uint32_t {
+    uint32_t n = j - kr, pos = 0u, w = (uint32_t)longm;
+    const uint32_t clo = (uint32_t)__popc((uint32_t)longm);
+    const bool up = n >= clo;
+    n = up ? n - clo : n;
+    pos = up ? 32u : 0u;
+    w = up ? (uint32_t)(longm >> 32) : w;
+#pragma unroll
+    for (uint32_t b = 16u; b >= 1u; b >>= 1) {
+      const uint32_t c = (uint32_t)__popc(w & ((1u << b) - 1u));
+      const bool ge = n >= c;
+      n = ge ? n - c : n;
+      pos = ge ? pos + b : pos;
+      w = ge ? w >> b : w;
+    }
+    return j < kr ? j : pos;  // (pos <= 63 for any j: a valid shuffle lane)
+  };
+  const uint32_t rA = slot_packet(lane), rB = slot_packet(lane + 64u);
+  // (every shuffle with the whole wave active: a lane that reads an inactive
+  // lane's value gets 0, so none sits under the `< ns` condition)
+  const uint32_t shA = (uint32_t)__shfl((int)len, (int)rA, 64);
+  const uint32_t shB = (uint32_t)__shfl((int)len, (int)rB, 64);
+  const uint32_t lenA = lane < ns ? shA : 0u;
+  const uint32_t lenB = lane + 64u < ns ? shB : 0u;
+  const uint32_t olA = (uint32_t)__shfl((int)offlo, (int)rA, 64);
+  const uint32_t ohA = (uint32_t)__shfl((int)offhi, (int)rA, 64);
+  const uint32_t olB = (uint32_t)__shfl((int)offlo, (int)rB, 64);
+  const uint32_t ohB = (uint32_t)__shfl((int)offhi, (int)rB, 64);
   // trip 3: every slot's bytes, PB loads in flight per lane.  Branch-free: a
-  // slot past the end loads through a descriptor of 0 bytes (the bounds check
-  // returns zeros, no memory access), so no load sits in a branch and the
-  // wait counts stay exact (branches made the compiler drain vmcnt before
-  // every load).
-  uint64_t lm = longm;
-  for (uint32_t s = 0; s < ns; s += PB) {
+  // slot past the end loads through a descriptor of 0 bytes (its length: the
+  // bounds check returns zeros, no memory access; a real slot's load ends
+  // inside its packet), so no load sits in a branch and the wait counts stay
+  // exact (branches made the compiler drain vmcnt before every load).  A
+  // chunk reads ONE table (slots base .. base + 63; slots at or past lim
+  // none): choosing the table per slot by a select was miscompiled (the
+  // select hoisted out of the unrolled slots).  The first PB slots (every
+  // group of up to 12 full-size packets) with constant slot numbers.
+  auto chunk = [&](uint32_t s, uint32_t base, uint32_t lim, uint32_t lenT, uint32_t olT, uint32_t ohT,
+                   auto first) __attribute__((always_inline)) {
     u32x4 v[PB];
     uint32_t li[PB];
-    bool second[PB];
 #pragma unroll
     for (int u = 0; u < PB; ++u) {
       const uint32_t j = s + (uint32_t)u;
-      const bool valid = j < ns;
-      second[u] = j >= kr;
-      const uint32_t r = second[u] ? (uint32_t)__builtin_ctzll(lm | (1ull << 63)) : min(j, 63u);
-      lm = valid && second[u] ? lm & (lm - 1ull) : lm;
-      li[u] = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)r);
-      const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)offhi, (int)r) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)offlo, (int)r);
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.bytes + o), 0, valid ? 0x7FFFFFFF : 0, 0x00020000);
-      const uint32_t w = second[u] ? w1 : w0;
+      const int t = (int)min(j - base, 63u);  // (slots past the table: li = 0)
+      li[u] = (uint32_t)__builtin_amdgcn_readlane((int)lenT, t);
+      // (the first chunk's slots are below 64, where the table is 0 past ns)
+      if constexpr (!decltype(first)::value) li[u] = j < lim ? li[u] : 0u;
+      const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ohT, t) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)olT, t);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.bytes + o), 0, (int)li[u], 0x00020000);
+      const uint32_t w = j >= kr ? w1 : w0;
       v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)min(w, li[u] - 16u), 0, NT ? 2 : 0);
+      // the first chunk in source order: each slot's descriptor right before
+      // its load (hoisting them all holds 4 SGPRs a slot: spills) and every
+      // load before any use (the scheduler otherwise interleaves the uses and
+      // waits on the first loads before issuing the last)
+      if constexpr (decltype(first)::value) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int u = 0; u < PB; ++u) {
-      const uint32_t w = second[u] ? w1 : w0;
+      const bool second = s + (uint32_t)u >= kr;
+      const uint32_t w = second ? w1 : w0;
       const uint32_t keep = w < li[u] ? 0xFFFFFFFFu : 0u;
       const uint32_t sh = w + 16u > li[u] ? min(w + 16u - li[u], 15u) : 0u;
       const u32x4 x = shr_bytes_bf(v[u], sh) & keep;
       const u32x4 zero = {0u, 0u, 0u, 0u};
-      acc0 ^= second[u] ? zero : x;
-      acc1 ^= second[u] ? x : zero;
+      acc0 ^= second ? zero : x;
+      acc1 ^= second ? x : zero;
     }
-  }
+  };
+  const uint32_t limA = min(ns, 64u);
+  chunk(0u, 0u, limA, lenA, olA, ohA, std::true_type{});
+  for (uint32_t s = PB; s < limA; s += PB) chunk(s, 0u, limA, lenA, olA, ohA, std::false_type{});
+  for (uint32_t s = 64u; s < ns; s += PB) chunk(s, 64u, ns, lenB, olB, ohB, std::false_type{});
   uint8_t* dst = a.out + dst_off;
   const uint32_t nwin = (plen + 15u) >> 4;
   if (lane < nwin) st16t<NT>(dst + w0, acc0);
   if (lane + 64u < nwin) st16t<NT>(dst + w1, acc1);
 }
 
+// (one workgroup per 4 groups of a small batch: occupancy is no object; the
+// default 4-waves-per-SIMD target left the recover body 128 VGPRs and spilled)
 template <bool RECOVER, bool NT, int PB>
-__global__ __launch_bounds__(kBlock) void ragged_window_kernel(RaggedArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void ragged_window_kernel(
+    RaggedArgs a) {
   __shared__ uint32_t s_par[kFlatWaves][4 * kParWin];
   __shared__ uint64_t s_head[kFlatWaves][kParWin];
   __shared__ u32x4 s_meta[kFlatWaves][64];
@@ -1543,7 +1606,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   const uint32_t wg = blockIdx.x;
   const bool lead = wg == 0u;
   const SvcJob& J = *reinterpret_cast<const SvcJob*>(s_ent);
-  uint64_t st[6];  // measurement hook (sh->stamp_on): the leader's stamps of a job
+  __shared__ uint64_t st[6];  // measurement hook (sh->stamp_on): the leader's stamps of a job (thread 0; LDS, not 12 VGPRs live through the job)
   if (tid == 0) {
     // where the previous worker stopped (stable: it has left): jobs are
     // finished whole and in order, so the next job's number is the count
