@@ -1762,11 +1762,14 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
             window_group<false, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
           if (tid == 0 && g == 0) st[2] = wall_clock64();
         }
-        __syncthreads();
-        if (tid == 0) st[3] = wall_clock64();
-        __threadfence_system();  // this workgroup's outputs visible before its count
+        // every wave's output stores acknowledged, then ONE system-scope
+        // release (thread 0's: its L2 write-back covers the workgroup) before
+        // the count / token -- not one per thread
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
+          st[3] = wall_clock64();
+          __threadfence_system();  // this workgroup's outputs visible before its count
           st[4] = wall_clock64();
           bool last = true;
           if (split)
