@@ -1384,9 +1384,26 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
 }
 
-template <bool RECOVER, bool NT, int PB>
-__device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
-                                             uint32_t* s_par, uint64_t* s_head, u32x4* s_meta) {
+// NP > 1: one group on NP waves (the service's one-group job).  Wave `part`
+// takes every NP-th slot and leaves its partial windows in red0 / red1
+// [part * 64 + lane]; the caller XORs the NP partials after a barrier and
+// stores them where the returned WinOut says (red); a group out of the fast
+// form is finished by part 0 alone (!red).  Only part 0 stores the encode length and
+// folds in the recover parity.
+struct WinOut {
+  uint8_t* dst;
+  uint32_t w0, w1, nwin;
+  bool red;  // partials left in red0 / red1 (false: finished, or NP == 1)
+};
+
+template <bool RECOVER, bool NT, int PB, int NP = 1>
+__device__ __forceinline__ WinOut window_group(const RaggedArgs& a, uint64_t g, uint32_t lane,
+                                               uint32_t* s_par, uint64_t* s_head, u32x4* s_meta,
+                                               uint32_t part = 0, u32x4* red0 = nullptr,
+                                               u32x4* red1 = nullptr) {
+  static_assert(PB % NP == 0, "slots split evenly over the waves");
+  constexpr int PW = PB / NP;                     // loads per wave per chunk
+  const uint32_t pt = NP == 1 ? 0u : part;        // (NP == 1: constant slot numbers)
   // trip 1: the group's scalars (s_load; the service's tables sit in LDS
   // behind generic pointers: flat loads into VGPRs, which the compiler takes
   // for per-lane values -- every slot below then became a waterfall loop
@@ -1422,21 +1439,25 @@ __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, ui
   if (RECOVER && form) {
     w0 = min(16u * lane, plen - 16u);
     w1 = min(16u * (lane + 64u), plen - 16u);
-    const uint8_t* prow = a.parity + par_off;
-    acc0 = ld16t<NT>(prow + w0);
-    if (plen > 1024u) acc1 = ld16t<NT>(prow + w1);
+    if (pt == 0u) {
+      const uint8_t* prow = a.parity + par_off;
+      acc0 = ld16t<NT>(prow + w0);
+      if (plen > 1024u) acc1 = ld16t<NT>(prow + w1);
+    }
   }
   const uint32_t lim = RECOVER ? plen : kMaxPacket;
   if (!form || wave_any(lane < kr && (len < 16u || len > lim))) {
-    GroupPrefetch f;
-    group_scalars<RECOVER>(a, g, f);
-    group_vectors<RECOVER, NT>(a, g, lane, f);
-    ragged_group<RECOVER, NT, 2, 1>(a, g, lane, f, s_par, s_head, s_meta);
-    return;
+    if (pt == 0u) {
+      GroupPrefetch f;
+      group_scalars<RECOVER>(a, g, f);
+      group_vectors<RECOVER, NT>(a, g, lane, f);
+      ragged_group<RECOVER, NT, 2, 1>(a, g, lane, f, s_par, s_head, s_meta);
+    }
+    return WinOut{nullptr, 0u, 0u, 0u, false};
   }
   if constexpr (!RECOVER) {
     plen = wave_max11(len);
-    if (lane == 0) a.parity_len_out[g] = (uint16_t)plen;
+    if (lane == 0 && pt == 0u) a.parity_len_out[g] = (uint16_t)plen;
     w0 = min(16u * lane, plen - 16u);
     w1 = min(16u * (lane + 64u), plen - 16u);
   }
@@ -1484,17 +1505,17 @@ __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, ui
   // bounds check returns zeros, no memory access; a real slot's load ends
   // inside its packet), so no load sits in a branch and the wait counts stay
   // exact (branches made the compiler drain vmcnt before every load).  A
-  // chunk reads ONE table (slots base .. base + 63; slots at or past lim
-  // none): choosing the table per slot by a select was miscompiled (the
-  // select hoisted out of the unrolled slots).  The first PB slots (every
-  // group of up to 12 full-size packets) with constant slot numbers.
+  // chunk of PB slots reads ONE table (slots base .. base + 63; slots at or
+  // past lim none), this wave's PW of them (slot s + pt + NP u).  The first
+  // PB slots (every group of up to 12 full-size packets) with the loads
+  // issued before any use.
   auto chunk = [&](uint32_t s, uint32_t base, uint32_t lim, uint32_t lenT, uint32_t olT, uint32_t ohT,
                    auto first) __attribute__((always_inline)) {
-    u32x4 v[PB];
-    uint32_t li[PB];
+    u32x4 v[PW];
+    uint32_t li[PW];
 #pragma unroll
-    for (int u = 0; u < PB; ++u) {
-      const uint32_t j = s + (uint32_t)u;
+    for (int u = 0; u < PW; ++u) {
+      const uint32_t j = s + pt + (uint32_t)(NP * u);
       const int t = (int)min(j - base, 63u);  // (slots past the table: li = 0)
       li[u] = (uint32_t)__builtin_amdgcn_readlane((int)lenT, t);
       // (the first chunk's slots are below 64, where the table is 0 past ns)
@@ -1512,8 +1533,8 @@ __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, ui
       if constexpr (decltype(first)::value) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int u = 0; u < PB; ++u) {
-      const bool second = s + (uint32_t)u >= kr;
+    for (int u = 0; u < PW; ++u) {
+      const bool second = s + pt + (uint32_t)(NP * u) >= kr;
       const uint32_t w = second ? w1 : w0;
       const uint32_t keep = w < li[u] ? 0xFFFFFFFFu : 0u;
       const uint32_t sh = w + 16u > li[u] ? min(w + 16u - li[u], 15u) : 0u;
@@ -1529,8 +1550,14 @@ __device__ __forceinline__ void window_group(const RaggedArgs& a, uint64_t g, ui
   for (uint32_t s = 64u; s < ns; s += PB) chunk(s, 64u, ns, lenB, olB, ohB, std::false_type{});
   uint8_t* dst = a.out + dst_off;
   const uint32_t nwin = (plen + 15u) >> 4;
+  if constexpr (NP > 1) {
+    red0[pt * 64u + lane] = acc0;
+    red1[pt * 64u + lane] = acc1;
+    return WinOut{dst, w0, w1, nwin, true};
+  }
   if (lane < nwin) st16t<NT>(dst + w0, acc0);
   if (lane + 64u < nwin) st16t<NT>(dst + w1, acc1);
+  return WinOut{nullptr, 0u, 0u, 0u, false};
 }
 
 // (one workgroup per 4 groups of a small batch: occupancy is no object; the
@@ -1595,6 +1622,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   __shared__ uint32_t s_par[kSvcWaves][4 * kParWin];
   __shared__ uint64_t s_head[kSvcWaves][kParWin];
   __shared__ u32x4 s_meta[kSvcWaves][64];
+  __shared__ u32x4 s_red[2][kSvcWaves * 64];  // a one-group job's partial windows
   __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
   __shared__ uint32_t s_job, s_exit, s_stamp, s_pref;
@@ -1755,12 +1783,33 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         // split: group g on wave g / kSvcWgs of workgroup g % kSvcWgs (a
         // 9..64-group job is one round, spread over the workgroups)
         const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
-        for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
-          if (J.recover)
-            window_group<true, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-          else
-            window_group<false, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-          if (tid == 0 && g == 0) st[2] = wall_clock64();
+        if (n == 1u) {
+          // one group: every wave of the leader on it (its slots dealt round
+          // the waves: a wave issues an instruction every few cycles, and one
+          // wave alone spent ~1 us issuing a group's loads and shifting its
+          // windows), the partial windows XORed out of LDS by two waves
+          const WinOut o =
+              J.recover ? window_group<true, true, kSvcPB, kSvcWaves>(
+                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1])
+                        : window_group<false, true, kSvcPB, kSvcWaves>(
+                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1]);
+          __syncthreads();
+          if (o.red && wv < 2u) {
+            const u32x4* r = s_red[wv];
+            u32x4 x = r[lane];
+#pragma unroll
+            for (int q = 1; q < kSvcWaves; ++q) x ^= r[q * 64 + lane];
+            if (lane + 64u * wv < o.nwin) st16t<true>(o.dst + (wv == 0u ? o.w0 : o.w1), x);
+          }
+          if (tid == 0) st[2] = wall_clock64();
+        } else {
+          for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
+            if (J.recover)
+              window_group<true, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+            else
+              window_group<false, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+            if (tid == 0 && g == 0) st[2] = wall_clock64();
+          }
         }
         // every wave's output stores acknowledged, then ONE system-scope
         // release (thread 0's: its L2 write-back covers the workgroup) before
