@@ -320,12 +320,15 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   ctx->svc_poison_next = false;
   __atomic_store_n(&j.head_sum, 0ull, __ATOMIC_RELAXED);
   __atomic_store_n(&j.seq, wseq, __ATOMIC_RELEASE);
-  // a job that fits the polled head: its hash last (the worker's poll takes
-  // the job from the bytes it already read when they sum to it)
+  // the hash of the polled head (the entry's first kSvcHead bytes at most)
+  // last: the worker's poll takes a job that fits its head from the bytes it
+  // already read when they sum to it, and a larger one's size (every
+  // workgroup then copies the entry in one pass)
   constexpr uint32_t kHead = (uint32_t)offsetof(qfec::SvcJob, tab);
-  if (kHead + tb.bytes <= qfec::kSvcHead)
-    __atomic_store_n(&j.head_sum, qfec::svc_head_hash(j, (kHead + tb.bytes + 15u) & ~15u),
-                     __ATOMIC_RELEASE);
+  __atomic_store_n(&j.head_sum,
+                   qfec::svc_head_hash(j, std::min<uint32_t>((kHead + tb.bytes + 15u) & ~15u,
+                                                             qfec::kSvcHead)),
+                   __ATOMIC_RELEASE);
   ctx->svc_published += a.n_groups;
   __atomic_store_n(&sh->pub_end, ctx->svc_published, __ATOMIC_RELEASE);
   __atomic_thread_fence(__ATOMIC_SEQ_CST);

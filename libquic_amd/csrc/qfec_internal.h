@@ -166,6 +166,11 @@ struct SvcDev {
   uint32_t ready;            // leader: this launch's epoch once `to` is valid
   uint32_t exit;             // leader: this launch's epoch when the workers leave
   uint32_t done[kSvcRing];   // workgroups finished per ring entry (kSvcWgs per split job)
+  // leader, just after `to`: the turn's first job's entry size when its poll
+  // found the head whole (the followers copy the entry in one pass), one
+  // word as a leader that runs ahead rewrites it: (uint32_t)to << 32 | (job &
+  // 0xFFFF) << 16 | bytes / 16 (0: size unknown)
+  uint64_t ent;
 };
 hipError_t launch_ragged_service(SvcShared* sh, SvcDev* dv, const SvcJob* ring, uint32_t* flags,
                                  uint64_t idle_ticks, uint32_t epoch, hipStream_t s);

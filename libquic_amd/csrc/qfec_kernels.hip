@@ -1594,11 +1594,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 // decides; the followers leave on its word).  All control stores are vector
 // stores.
 constexpr int kSvcWaves = 8;
-// Load slots per trip of a group's bytes: 24 = every window of a group of up
-// to 12 packets longer than 1024 B in ONE PCIe round trip (16 made a
-// 10 x 1350 B group two trips: 20 slots; 238 VGPRs at 2 waves/SIMD; 32
-// spilled)
+// Load slots per trip of a group's bytes.  A one-group job (all eight waves,
+// three slots each): 24 = every window of a group of up to 12 packets longer
+// than 1024 B in ONE PCIe round trip.  A job of several groups (a wave per
+// group): 20 = the 10 x 1350 B group (kDefaultMaxPacketsPerFecGroup) in one
+// trip (16 made it two; 24 beside the one-group form spilled at 2 waves/SIMD)
 constexpr int kSvcPB = 24;
+constexpr int kSvcPBw = 20;
 
 __device__ __forceinline__ uint64_t svc_load64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1625,7 +1627,10 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   __shared__ u32x4 s_red[2][kSvcWaves * 64];  // a one-group job's partial windows
   __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
-  __shared__ uint32_t s_job, s_exit, s_stamp, s_pref;
+  __shared__ uint32_t s_job, s_exit, s_stamp;
+  // the job whose entry size is known (s_need bytes; the leader: s_have of
+  // them already in LDS from its poll), else no job
+  __shared__ uint32_t s_entjob, s_have, s_need;
   static_assert(sizeof(SvcJob) % 16u == 0u, "entry copied in 16-B pieces");
   constexpr uint32_t kHead = (uint32_t)offsetof(SvcJob, tab);
   constexpr uint32_t kFirst = 4096u;  // first pass: the header and the first tables
@@ -1692,33 +1697,43 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         __builtin_amdgcn_s_sleep(2);
         to = look();
       }
+      // the head found whole (its hash, seq and start agree): the entry's
+      // size is known -- a small job is all in LDS already, a larger one is
+      // copied in one pass by every workgroup (the followers learn the size
+      // with `to`) instead of a header pass and a table pass
       if (lane == 0u) {
         if (ex)
           __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         else
           __hip_atomic_store(&dv->to, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
-      uint32_t pref = 0;
+      uint32_t have = 0, need = 0;
       if (!ex) {
         uint64_t* sw = reinterpret_cast<uint64_t*>(s_ent);
         sw[2u * lane] = h0;
         sw[2u * lane + 1u] = h1;
         wave_lds_order();
         const uint32_t tbb = J.tab_bytes;
-        const uint32_t nb = kHead + tbb <= kSvcHead ? ((kHead + tbb + 15u) & ~15u) : 0u;
+        const uint32_t full = min((kHead + min(tbb, kSvcTab) + 15u) & ~15u, (uint32_t)sizeof(SvcJob));
+        const uint32_t nb = min(full, kSvcHead);
         uint64_t part = 0;
         if (2u * lane < nb / 8u && 2u * lane != kSvcHeadSumWord) part += svc_head_word(h0, 2u * lane);
         if (2u * lane + 1u < nb / 8u && 2u * lane + 1u != kSvcHeadSumWord)
           part += svc_head_word(h1, 2u * lane + 1u);
 #pragma unroll
         for (int d = 32; d > 0; d >>= 1) part += (uint64_t)__shfl_xor((unsigned long long)part, d, 64);
-        pref = (nb != 0u && (part | 1ull) == J.head_sum && J.seq == job0 && J.start == from) ? 1u : 0u;
+        const bool whole = (part | 1ull) == J.head_sum && J.seq == job0 && J.start == from &&
+                           tbb <= kSvcTab;
+        have = whole ? nb : 0u;
+        need = whole ? full : 0u;
       }
       if (lane == 0u) {
         st[0] = wall_clock64();
         s_to = to;
         s_exit = ex;
-        s_pref = pref;
+        s_entjob = need != 0u ? job0 : 0xFFFFFFFFu;
+        s_have = have;
+        s_need = need;
       }
     } else if (!lead && tid == 0) {
       // follower: the leader's word, from device memory (exit read first:
@@ -1740,20 +1755,47 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
       }
       s_to = to;
       s_exit = ex;
-      s_pref = 0u;
+      s_have = 0u;
+      s_entjob = 0xFFFFFFFFu;
+      s_need = 0u;
+      while (!ex) {
+        // the leader's word on this turn's first entry (stored a moment after
+        // `to`); a leader gone on to a later turn: size unknown
+        const uint64_t ent = __hip_atomic_load(&dv->ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(ent >> 32) == (uint32_t)to) {
+          s_need = (uint32_t)(ent & 0xFFFFu) << 4;
+          s_entjob = s_job + ((((uint32_t)(ent >> 16) & 0xFFFFu) - s_job) & 0xFFFFu);
+          break;
+        }
+        if (__hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != to) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
     __syncthreads();
     if (s_exit) break;
     // every thread: drop cached copies of host memory (ring entries, payloads)
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    // the leader's word for the followers: after its fence, so the store's
+    // completion does not hold up the leader's own acquire
+    if (lead && tid == 0)
+      __hip_atomic_store(&dv->ent,
+                         ((uint64_t)(uint32_t)s_to << 32) | ((uint64_t)(s_entjob & 0xFFFFu) << 16) |
+                             (s_need >> 4),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t to = s_to;
     uint64_t gi = s_from;
     uint32_t jj = s_job;
     bool miss = false;
     while (gi < to) {  // the published jobs, in order (pub_end moves by whole jobs)
       const SvcJob* e = ring + (jj % kSvcRing);
-      // (the turn's first job may already be in LDS from the leader's poll)
-      if (!(s_pref != 0u && jj == s_job)) svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
+      // a job of known size in one pass (the leader's poll may hold some or
+      // all of it already), else the header and first tables, then the rest
+      const uint32_t have = jj == s_entjob ? s_have : 0u;
+      const uint32_t need = jj == s_entjob ? s_need : 0u;
+      if (need == 0u)
+        svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
+      else if (have < need)
+        svc_copy_entry(e, s_ent, have, need);
       __syncthreads();
       if (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab) {
         // a malformed ring: nothing of this turn is done
@@ -1764,7 +1806,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
       const uint64_t n = J.a.n_groups;
       const bool split = n > (uint64_t)kSvcWaves;
       if (split || lead) {
-        if (kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
+        if (need == 0u && kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
           svc_copy_entry(e, s_ent, kFirst, (kHead + J.tab_bytes + 15u) & ~15u);
           __syncthreads();
         }
@@ -1805,9 +1847,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         } else {
           for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
             if (J.recover)
-              window_group<true, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+              window_group<true, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
             else
-              window_group<false, true, kSvcPB>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+              window_group<false, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
             if (tid == 0 && g == 0) st[2] = wall_clock64();
           }
         }
