@@ -52,6 +52,28 @@ def test_service_parity_across_idle_exits():
         ctx.close()
 
 
+@pytest.mark.parametrize("k", [1, 2, 10, 12, 13, 24, 33, 40, 64, 65])
+@pytest.mark.parametrize("shape", ["full", "wide", "short"])
+def test_service_one_group_on_all_waves(k, shape):
+    """Round 5: a one-group job runs on all 8 waves of the leader (its slots
+    dealt round the waves, partial windows XORed out of LDS; a group out of
+    the fast form -- more than 64 received packets, a packet under 16 B --
+    by wave 0 alone).  k = 13 and up needs a second chunk of slots, k = 33
+    and up (full packets) the second slot table (slots 64-127); exact,
+    encode and recover (one drop index per group), over repeated jobs."""
+    kw = {"full": dict(lmin=1452, lmax=1452), "wide": dict(lmin=16, lmax=1452),
+          "short": dict(lmin=1, lmax=40)}[shape]
+    ctx = qfec.Context(0)
+    try:
+        for rep in range(3):
+            z, want_l = _mapped_case(1, g0=45000 + 7 * k + rep, kmin=k, kmax=k, seed=100 * k + rep,
+                                     **kw)
+            _check(ctx, z, want_l)
+        assert ctx.debug_service()["jobs"] >= 6
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("n", [8, 9, 17, 33, 63, 64])
 def test_service_split_jobs(n):
     """Round 5: a job of more than 8 groups is spread over the worker's 8
