@@ -138,19 +138,23 @@ inline uint64_t svc_head_hash(const SvcJob& j, uint32_t nbytes) {
   return h | 1ull;  // never 0 (0 = no hash)
 }
 struct SvcShared {
-  uint64_t pub_end;   // host: groups published
-  uint64_t consumed;  // worker: groups finished (a new worker starts here)
+  // the host's words (the worker reads them) on a cache line of their own:
+  // the worker's per-turn stores below would otherwise take the line from
+  // the host's cache before every publish
+  alignas(64) uint64_t pub_end;  // host: groups published
   uint32_t alive;     // host: 1 when it launches a worker; worker: 1 when it starts,
                       // 0 on its way out
   uint32_t quit;      // host: exit now (context destroyed)
+  uint32_t stamp_on;  // host (measurement hook): the worker records stamps[] for each job
+  // the worker's words, stored every turn
+  alignas(64) uint64_t consumed;  // worker: groups finished (a new worker starts here)
   uint64_t jobs;      // worker: jobs finished (stats)
   uint32_t fault;     // worker: a published group lay in no ring entry; it left
                       // without finishing (no token for any job of that turn)
-  uint32_t stamp_on;  // host (measurement hook): the worker records stamps[] for each job
   // 100-MHz wall-clock stamps of the last job (qfec_debug_service_stamps):
   // [0] work seen, [1] entry in LDS, [2] wave 0's first group done, [3] every
   // group done, [4] outputs visible (fence), [5] token stored
-  uint64_t stamps[8];
+  alignas(64) uint64_t stamps[8];
 };
 constexpr uint32_t kSvcRing = 8;
 // Round 5: the worker is kSvcWgs workgroups.  Workgroup 0 (the leader) polls
