@@ -30,6 +30,12 @@ thread_local char g_tls_error[512] = "";
 constexpr int kSlots = 3;                         // host path pipeline depth
 constexpr size_t kStageBytes = 64ull << 20;       // per-slot input staging
 constexpr uint64_t kDirectGroups = 256;  // mapped batches up to this size: no staging copies
+// A slot's completion word sits on a 64-B line of its own (h_flag[slot *
+// kFlagStride]), followed by the encode lengths of a direct batch of up to
+// kFlagPlens groups: the completion reads the token and the lengths in one
+// cache-line transfer instead of two (the lengths otherwise land in h_out)
+constexpr uint32_t kFlagStride = 16;
+constexpr uint64_t kFlagPlens = 30;
 // Device error words (kernel-latched error bits), one per kind of work so
 // that collecting one never reads or clears another's: the
 // context stream's device-pointer calls, each staging slot's QFEC_ASYNC op,
@@ -243,9 +249,9 @@ int ensure_staging(qfec_ctx* ctx) {
   }
   QFEC_HIP(ctx, hipMalloc(&ctx->d_done, kSlots * sizeof(uint32_t)));
   QFEC_HIP(ctx, hipMemset(ctx->d_done, 0, kSlots * sizeof(uint32_t)));
-  QFEC_HIP(ctx, hipHostMalloc(&ctx->h_flag, kSlots * sizeof(uint32_t),
+  QFEC_HIP(ctx, hipHostMalloc(&ctx->h_flag, kSlots * kFlagStride * sizeof(uint32_t),
                               hipHostMallocMapped | hipHostMallocPortable));
-  std::memset(ctx->h_flag, 0, kSlots * sizeof(uint32_t));
+  std::memset(ctx->h_flag, 0, kSlots * kFlagStride * sizeof(uint32_t));
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->h_flag_dev), ctx->h_flag, 0));
   ctx->staging_ready = true;
   return QFEC_OK;
@@ -306,7 +312,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   j.a.done_flag = nullptr;
   j.start = ctx->svc_published;
   j.recover = recover ? 1u : 0u;
-  j.flag_slot = (uint32_t)slot;
+  j.flag_slot = (uint32_t)slot * kFlagStride;
   j.token = token;
   j.tab_bytes = tb.bytes;
   j.t_off = tb.off;
@@ -357,7 +363,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
 // so a worker that faulted or left without the job ends in an error, not a
 // hang.
 int wait_flag_svc(qfec_ctx* ctx, int si, uint32_t token) {
-  const uint32_t* f = ctx->h_flag + si;
+  const uint32_t* f = ctx->h_flag + si * kFlagStride;
   for (uint32_t spins = 1;; ++spins) {
     if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
     if ((spins & 4095u) == 0) {
@@ -406,7 +412,7 @@ void svc_abandon(qfec_ctx* ctx) {
 // event, recorded after the launch, is polled now and then so that a flag
 // that never comes ends in an error instead of a hang.
 int wait_flag(qfec_ctx* ctx, int si, uint32_t token) {
-  const uint32_t* f = ctx->h_flag + si;
+  const uint32_t* f = ctx->h_flag + si * kFlagStride;
   for (uint32_t spins = 1;; ++spins) {
     if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == token) return QFEC_OK;
     if ((spins & 1023u) == 0) {
@@ -431,7 +437,7 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   if (!op.live) return QFEC_OK;
   Slot& s = ctx->slots[si];
   if (op.svc) {
-    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
+    if (!wait && __atomic_load_n(ctx->h_flag + si * kFlagStride, __ATOMIC_ACQUIRE) != op.token) {
       // a worker that is gone without the token (fault, ring miss, exit)
       // must end in an error, not QFEC_PENDING forever
       const hipError_t q = hipStreamQuery(ctx->svc_stream);
@@ -452,7 +458,7 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
       return wrc;
     }
   } else if (op.direct) {
-    if (!wait && __atomic_load_n(ctx->h_flag + si, __ATOMIC_ACQUIRE) != op.token) {
+    if (!wait && __atomic_load_n(ctx->h_flag + si * kFlagStride, __ATOMIC_ACQUIRE) != op.token) {
       const hipError_t q = hipEventQuery(s.done);
       if (q == hipErrorNotReady) return QFEC_PENDING;
       if (q != hipSuccess) {
@@ -472,7 +478,11 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
     QFEC_HIP(ctx, hipEventSynchronize(s.done));
   }
   if (!op.recover && op.parity_len_out)
-    std::memcpy(op.parity_len_out, s.h_out, op.cnt * sizeof(uint16_t));
+    std::memcpy(op.parity_len_out,
+                op.direct && op.cnt <= kFlagPlens
+                    ? static_cast<const void*>(ctx->h_flag + si * kFlagStride + 1)
+                    : static_cast<const void*>(s.h_out),
+                op.cnt * sizeof(uint16_t));
   return op.direct ? QFEC_OK : collect_error(ctx, s.stream, kErrSlot0 + si);
 }
 
@@ -1483,7 +1493,11 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       QFEC_HIP(ctx, hipEventSynchronize(ctx->slots[si].done));
     }
     if (!recover)
-      std::memcpy(parity_len_out + c.g0, ctx->slots[si].h_out, c.cnt * sizeof(uint16_t));
+      std::memcpy(parity_len_out + c.g0,
+                  c.token != 0u && c.cnt <= kFlagPlens  // (a direct batch: token set)
+                      ? static_cast<const void*>(ctx->h_flag + si * kFlagStride + 1)
+                      : static_cast<const void*>(ctx->slots[si].h_out),
+                  c.cnt * sizeof(uint16_t));
     c.live = false;
     return QFEC_OK;
   };
@@ -1559,14 +1573,17 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       a.out_off = reinterpret_cast<const uint64_t*>(tab + t.ooff);
       a.out = out;
     } else {
-      a.parity_len_out = reinterpret_cast<uint16_t*>(direct ? s.h_out_dev : s.d_out);
+      a.parity_len_out = reinterpret_cast<uint16_t*>(
+          !direct ? s.d_out
+                  : cnt <= kFlagPlens ? reinterpret_cast<uint8_t*>(ctx->h_flag_dev + slot * kFlagStride + 1)
+                                      : s.h_out_dev);
       a.out = parity_out;
     }
     uint32_t token = 0;
     if (direct) {
       token = ++ctx->flag_token ? ctx->flag_token : ++ctx->flag_token;  // never 0
       a.done_count = ctx->d_done + slot;
-      a.done_flag = ctx->h_flag_dev + slot;
+      a.done_flag = ctx->h_flag_dev + slot * kFlagStride;
       a.done_token = token;
       // a few groups: the resident service worker takes them from its ring
       // (no launch); a flag is all their completion needs
