@@ -1370,6 +1370,9 @@ def bench_connection(cpu=True):
                    "revived views (wall, median); up to 256 groups the index tables are read in "
                    "place too and the host spins on a completion flag the kernel's last "
                    "workgroup stores (latency path), above that they are staged to the device; "
+                   "batches of up to 64 groups go to the resident small-batch service, which each "
+                   "rep's turn start warms (qfec_service_warm) before the batch is assembled "
+                   "(encode_build_us), as an event loop does; "
                    "cpu_1core = the oracle's per-group XorBuffers accumulate (the reference's "
                    "connection-thread path), one core"
                    + ("" if cpu else "; cpu legs requested off but always run"))

@@ -155,6 +155,15 @@ uint64_t qfec_async_ticket(const qfec_ctx* ctx);
  * QFEC_ERR_INTERNAL for an unknown or already completed ticket.
  * qfec_complete still finishes every op and claims every kept code. */
 int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait);
+/* Small-batch service hint (round 5; no counterpart in the reference): make
+ * sure the context's resident worker runs.  An event loop that calls it when
+ * a turn starts collecting groups finds the worker resident at the turn's
+ * flush instead of relaunching it there (the worker leaves after 100 us
+ * without work; a relaunch costs the calling thread 3-5 us and the flush
+ * ~20 us).  One load when the worker runs; a no-op with the service off.
+ * Returns a qfec_* code (a failed launch turns the service off for the
+ * context, as a failed relaunch in a batch call does). */
+int qfec_service_warm(qfec_ctx* ctx);
 const char* qfec_strerror(int code);
 /* Pinned, device-mapped host memory for QFEC_PTR_MAPPED payloads (the
  * registered receive / send buffers of a QUIC server: the GPU reads packets

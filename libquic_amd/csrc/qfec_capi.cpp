@@ -2003,6 +2003,28 @@ int qfec_phase_backoff(qfec_ctx* ctx) { return ctx ? (int)ctx->phase_backoff : -
 
 int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_phased : -1; }
 
+int qfec_service_warm(qfec_ctx* ctx) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!ctx->svc_on) return QFEC_OK;
+  if ((rc = ensure_staging(ctx)) || (rc = ensure_service(ctx))) return rc;
+  qfec::SvcShared* sh = ctx->svc_sh;
+  if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) != 0u) return QFEC_OK;
+  // nothing is published here, so a worker that is leaving needs no second
+  // look: a spare one queued behind it on the stream idles out in turn
+  __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
+  const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev, ctx->svc_ring_dev,
+                                                   ctx->h_flag_dev, kSvcIdleTicks, ++ctx->svc_epoch,
+                                                   ctx->svc_stream);
+  if (e != hipSuccess) {
+    __atomic_store_n(&sh->alive, 0u, __ATOMIC_SEQ_CST);
+    ctx->svc_on = false;
+    return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
+  }
+  ++ctx->svc_launches;
+  return QFEC_OK;
+}
+
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
   if (on == 2) {

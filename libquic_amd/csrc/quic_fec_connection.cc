@@ -305,12 +305,17 @@ QuicFecBatcher::~QuicFecBatcher() {
   QuicFecGroup::Finish(&rev_pending_, true);
 }
 
+// The turn's first group warms the small-batch service (qfec_service_warm):
+// the worker is then resident by the turn's Launch instead of relaunched
+// there.  Best effort: a failure shows at Launch as before.
 void QuicFecBatcher::AddClosedGroup(Visitor* v, const QuicPacketHeader& fec_header,
                                     std::unique_ptr<QuicFecGroup> group) {
+  if (ctx_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
   enc_.push_back(EncodeItem{v, fec_header, std::move(group)});
 }
 
 void QuicFecBatcher::AddRevivable(Visitor* v, std::unique_ptr<QuicFecGroup> group) {
+  if (ctx_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
   rev_.push_back(ReviveItem{v, std::move(group)});
 }
 

@@ -108,6 +108,7 @@ SIGNATURES = [
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
     ("qfec_complete_ticket", C.c_int, [_vp, C.c_uint64, C.c_int]),
+    ("qfec_service_warm", C.c_int, [_vp]),
     ("qfec_synth_fixed", C.c_int,
      [_vp, _u8p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
       C.c_uint64]),
@@ -436,6 +437,11 @@ class Context:
         raises its own error only."""
         rc = self.lib.qfec_complete_ticket(self.ctx, ticket, 1 if wait else 0)
         return rc if rc == 1 else self._check(rc)
+
+    def service_warm(self):
+        """qfec_service_warm: make sure the small-batch service's worker runs
+        (an event loop's turn start); a no-op with the service off."""
+        self._check(self.lib.qfec_service_warm(self.ctx))
 
     def debug_service(self, on=None, poison_next=False):
         """Small-batch service hook: on True / False enables / disables the

@@ -56,6 +56,12 @@ int qfec_complete(qfec_ctx* ctx, int wait) {
   return QFEC_OK;
 }
 
+/* No resident worker on the CPU: nothing to warm. */
+int qfec_service_warm(qfec_ctx* ctx) {
+  (void)ctx;
+  return QFEC_OK;
+}
+
 /* Work completes inside the call: nothing is ever queued. */
 uint64_t qfec_async_ticket(const qfec_ctx* ctx) {
   (void)ctx;

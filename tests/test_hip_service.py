@@ -52,6 +52,27 @@ def test_service_parity_across_idle_exits():
         ctx.close()
 
 
+def test_service_warm():
+    """qfec_service_warm (an event loop's turn start): the worker runs after
+    it, a second call while it runs launches nothing, batches stay exact, and
+    with the service off it is a no-op."""
+    z, want_l = _mapped_case(2, g0=46000, kmin=10, kmax=10, lmin=1350, lmax=1350, seed=3)
+    ctx = qfec.Context(0)
+    try:
+        ctx.service_warm()
+        st = ctx.debug_service()
+        assert st["alive"] == 1 and st["launches"] >= 1, st
+        ctx.service_warm()
+        assert ctx.debug_service()["launches"] == st["launches"]
+        _check(ctx, z, want_l)
+        ctx.debug_service(on=False)
+        ctx.service_warm()
+        assert ctx.debug_service()["alive"] == 0
+        _check(ctx, z, want_l)
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("k", [1, 2, 10, 12, 13, 24, 33, 40, 64, 65])
 @pytest.mark.parametrize("shape", ["full", "wide", "short"])
 def test_service_one_group_on_all_waves(k, shape):
