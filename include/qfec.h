@@ -152,8 +152,9 @@ uint64_t qfec_async_ticket(const qfec_ctx* ctx);
 /* Finish ONE queued op: wait blocks, otherwise QFEC_PENDING while it runs.
  * Returns that op's own code only (an op finished early by another call --
  * its staging slot reused, a synchronous call -- keeps its code for this);
- * QFEC_ERR_INTERNAL for an unknown or already completed ticket.
- * qfec_complete still finishes every op and claims every kept code. */
+ * QFEC_ERR_INTERNAL for an unknown or already claimed ticket.  The codes of
+ * the last 4096 tickets stay claimable once each, also after qfec_complete
+ * finished their ops (which reports an op's error once, to one of the two). */
 int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait);
 /* Small-batch service hint (round 5; no counterpart in the reference): make
  * sure the context's resident worker runs.  An event loop that calls it when
@@ -419,6 +420,10 @@ int qfec_phase_backoff(qfec_ctx* ctx);
  * The measurement names its roofline kernel from this, not from a copy of
  * the library's size rule. */
 int qfec_last_fixed_phased(const qfec_ctx* ctx);
+/* Test hook: the workgroup count of the last device fixed-shape launch if it
+ * ran phased (one per CU, less the CUs other contexts' resident small-batch
+ * workers hold), else 0. */
+uint32_t qfec_debug_last_phase_grid(const qfec_ctx* ctx);
 /* Test hook: launch `extra` workgroups beyond one per CU in phased launches
  * (0..64; they cannot all be resident, so the first meeting times out — the
  * abandon path; the backoff does not apply while extra > 0), and with
@@ -434,6 +439,10 @@ int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases);
  * (40 LDS steps per phase only, more phases); 1 restores the default.  For
  * the per-group-size A/B; results are identical. */
 int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on);
+/* Test hook: the load batch of the runtime-k phased body (group sizes above
+ * 16): 16 (round 5's) or 32 (the default; 0 restores it).  For the
+ * per-group-size A/B; results are identical. */
+int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch);
 /* Test hook: fail != 0 makes every ragged call on this context fail with
  * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
  * connection integration: groups go without FEC). */
@@ -459,6 +468,10 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
  * done, outputs made visible, token stored.  (Worker launched by a later
  * job picks the setting up at its start.) */
 int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps);
+/* Test hook: hold != 0 keeps the service's follower workgroups waiting at
+ * their start (as if dispatched late behind another kernel) until it is
+ * cleared; the leader runs on.  A split job's token then waits for them. */
+int qfec_debug_service_hold(qfec_ctx* ctx, int hold);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

@@ -10,7 +10,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <map>
 #include <mutex>
 #include <cstdarg>
 #include <cstdio>
@@ -95,10 +94,12 @@ struct qfec_ctx {
   uint32_t phase_seen = 0;
   uint32_t phase_backoff = 0;
   int last_fixed_phased = -1;  // the last device fixed-shape launch: 1 phased, 0 one-pass
+  uint32_t last_phase_grid = 0;  // ... its phased grid (workgroups), 0 one-pass
   uint32_t ncu = 0;          // CU count, queried once
   uint32_t phase_extra = 0;  // test hook (qfec_debug_phase)
   uint32_t phase_min = 0;    // test hook (qfec_debug_phase_min)
   uint32_t no_regsteps = 0;  // test hook (qfec_debug_phase_regsteps)
+  uint32_t rt_batch = 0;     // test hook (qfec_debug_phase_rtbatch)
   bool debug_fail = false;   // test hook (qfec_debug_fail_launches)
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
@@ -120,13 +121,19 @@ struct qfec_ctx {
   uint64_t last_ticket = 0;  // of the last ragged mapped call, 0 if it ran synchronously
   // results of async ops finished by a call other than their owner's (a slot
   // reused, a synchronous call draining the slots, qfec_complete), kept for
-  // qfec_complete_ticket: each op's code reaches its own ticket's caller;
-  // `reported` once qfec_complete has returned it (it reports each code once)
+  // qfec_complete_ticket: each op's code reaches its own ticket's caller.
+  // A ring indexed by ticket (a std::map of every op's code, OK
+  // ones included, was walked by every qfec_complete -- thousands of node
+  // hops per call at the 4096 cap): insert, claim and overwrite are O(1) and
+  // allocate nothing; a ticket 4096 newer takes the oldest's place.
+  static constexpr uint32_t kKept = 4096;
   struct Kept {
+    uint64_t ticket = 0;  // 0: empty / claimed
     int code = QFEC_OK;
-    bool reported = false;
-  };
-  std::map<uint64_t, Kept> finished;
+  } kept[kKept];
+  // the first code of an op finished by another call that qfec_complete has
+  // not reported yet (it reports each such code once; OK codes need none)
+  int unreported = QFEC_OK;
   // small-batch service (qfec_internal.h SvcJob): a resident worker on a
   // stream of its own takes mapped async batches of <= kSvcGroups groups from
   // a ring in host-mapped memory -- no kernel launch per batch
@@ -267,6 +274,29 @@ constexpr uint64_t kSvcGroups = 64;
 // within it finds the worker resident
 constexpr uint64_t kSvcIdleTicks = 10000;
 
+// Process-wide registry of the contexts that run a small-batch service
+// (VERDICT r5 item 3): a phased launch on one context counts the workers of
+// the OTHERS on its device that are resident (or queued) and leaves their CUs
+// out of its grid.  A worker is kSvcWgs workgroups of 512 lanes at 252 VGPRs
+// and 57 KiB of LDS: each holds a CU whose LDS a phased workgroup (160 KiB)
+// can no longer get, so a full one-per-CU grid would not be resident and its
+// meetings would time out (round 5: 0.6-0.7x, abandoned).  The model is the
+// reference's: one connection thread per QuicConnection
+// (quic_connection.h:14), here one context per thread, several per process.
+std::mutex g_svc_mu;
+std::vector<qfec_ctx*> g_svc_ctxs;
+
+uint32_t other_service_cus(const qfec_ctx* ctx) {
+  std::lock_guard<std::mutex> lock(g_svc_mu);
+  uint32_t n = 0;
+  for (const qfec_ctx* c : g_svc_ctxs)
+    if (c != ctx && c->device == ctx->device && c->svc_sh &&
+        (__atomic_load_n(&c->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ||
+         hipStreamQuery(c->svc_stream) == hipErrorNotReady))
+      n += qfec::kSvcWgs;
+  return n;
+}
+
 int ensure_service(qfec_ctx* ctx) {
   if (ctx->svc_stream) return QFEC_OK;
   const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
@@ -279,8 +309,15 @@ int ensure_service(qfec_ctx* ctx) {
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_sh_dev), ctx->svc_sh, 0));
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_ring_dev), ctx->svc_ring, 0));
   QFEC_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->svc_dev), sizeof(qfec::SvcDev)));
-  QFEC_HIP(ctx, hipMemset(ctx->svc_dev, 0, sizeof(qfec::SvcDev)));
   QFEC_HIP(ctx, hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
+  // zeroed on the worker's own stream (a non-blocking stream is not ordered
+  // after the null stream's memset)
+  QFEC_HIP(ctx, hipMemsetAsync(ctx->svc_dev, 0, sizeof(qfec::SvcDev), ctx->svc_stream));
+  QFEC_HIP(ctx, hipStreamSynchronize(ctx->svc_stream));
+  {
+    std::lock_guard<std::mutex> lock(g_svc_mu);
+    g_svc_ctxs.push_back(ctx);
+  }
   return QFEC_OK;
 }
 
@@ -404,6 +441,13 @@ void svc_abandon(qfec_ctx* ctx) {
   ctx->svc_seq = (uint32_t)__atomic_load_n(&ctx->svc_sh->jobs, __ATOMIC_ACQUIRE);
   __atomic_store_n(&ctx->svc_sh->pub_end, consumed, __ATOMIC_RELEASE);
   __atomic_store_n(&ctx->svc_sh->fault, 0u, __ATOMIC_RELEASE);
+  // the workers' device words afresh (a split job's done count
+  // left part-way would misalign every later one of its ring entry, and a
+  // follower's announcement count must match the leader's); every worker has
+  // left (stop_service synchronised the stream)
+  if (ctx->svc_dev &&
+      hipMemsetAsync(ctx->svc_dev, 0, sizeof(qfec::SvcDev), ctx->svc_stream) == hipSuccess)
+    (void)hipStreamSynchronize(ctx->svc_stream);
   __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
 }
 
@@ -486,11 +530,12 @@ int complete_async_op(qfec_ctx* ctx, int si, bool wait) {
   return op.direct ? QFEC_OK : collect_error(ctx, s.stream, kErrSlot0 + si);
 }
 
-// Keep op `t`'s code for its ticket's qfec_complete_ticket (at most 4096
-// unclaimed codes; the oldest goes first).
+// Keep op `t`'s code for its ticket's qfec_complete_ticket (the last 4096
+// tickets' codes; a newer ticket overwrites the one 4096 before it).  A
+// non-OK code not yet reported by qfec_complete is remembered for it.
 void keep_code(qfec_ctx* ctx, uint64_t t, int rc, bool reported) {
-  if (ctx->finished.size() >= 4096) ctx->finished.erase(ctx->finished.begin());
-  ctx->finished[t] = qfec_ctx::Kept{rc, reported};
+  ctx->kept[t % qfec_ctx::kKept] = qfec_ctx::Kept{t, rc};
+  if (!reported && rc != QFEC_OK && ctx->unreported == QFEC_OK) ctx->unreported = rc;
 }
 
 // Finish the op of slot `si` (if live) for a caller that does not own it: its
@@ -516,10 +561,8 @@ int complete_async(qfec_ctx* ctx, bool wait) {
   // ops retired by other calls report here too, once; their codes stay
   // claimable by their tickets (QuicFecGroup::Finish on a context
   // another caller completed)
-  for (auto& f : ctx->finished) {
-    if (f.second.code && !f.second.reported && !first) first = f.second.code;
-    f.second.reported = true;
-  }
+  first = ctx->unreported;
+  ctx->unreported = QFEC_OK;
   for (;;) {
     int si = -1;
     for (int i = 0; i < kSlots; ++i)
@@ -798,9 +841,17 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
   a.phase_extra = ctx->phase_extra;
   a.phase_min = ctx->phase_min;
   a.no_regsteps = ctx->no_regsteps;
+  a.rt_batch = ctx->rt_batch;
   a.phase_host = ctx->h_phase_dev;
   a.phase_sync = (flags & QFEC_ONE_PASS) ? nullptr : ctx->d_phase;
-  if (a.phase_sync && qfec::fixed_uses_phases(a, nt)) {
+  uint32_t grid = 0;
+  bool phased = a.phase_sync && qfec::fixed_uses_phases(a, nt);
+  if (phased) {
+    // (the registry only for a batch that would phase at all)
+    a.svc_cus = other_service_cus(ctx);
+    phased = qfec::fixed_uses_phases(a, nt, &grid);
+  }
+  if (phased) {
     const uint32_t seen = __atomic_load_n(ctx->h_phase, __ATOMIC_ACQUIRE);
     if (seen != ctx->phase_seen) {
       ctx->phase_seen = seen;
@@ -828,11 +879,14 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
       ctx->phase_stream = ctx->stream;
       ctx->phase_recorded = true;
       ctx->last_fixed_phased = 1;
+      ctx->last_phase_grid = grid;
       return QFEC_OK;
     }
   }
+  a.phase_sync = nullptr;  // (a phased plan refused above: one-pass)
   QFEC_HIP(ctx, qfec::launch_fixed(a, nt, ctx->stream));
   ctx->last_fixed_phased = 0;
+  ctx->last_phase_grid = 0;
   return QFEC_OK;
 }
 
@@ -1024,8 +1078,18 @@ qfec_ctx* qfec_create(int device) {
 void qfec_destroy(qfec_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  stop_service(ctx);  // before the device-wide wait: a resident worker would hold it
-  (void)hipDeviceSynchronize();
+  {
+    std::lock_guard<std::mutex> lock(g_svc_mu);
+    g_svc_ctxs.erase(std::remove(g_svc_ctxs.begin(), g_svc_ctxs.end(), ctx), g_svc_ctxs.end());
+  }
+  stop_service(ctx);
+  // this context's streams only: a device-wide wait would also wait for
+  // another context's resident worker, which a busy connection thread keeps
+  // alive indefinitely (round 6)
+  if (ctx->own_stream) (void)hipStreamSynchronize(ctx->own_stream);
+  if (ctx->stream && ctx->stream != ctx->own_stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& s : ctx->slots)
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
   if (ctx->svc_stream) (void)hipStreamDestroy(ctx->svc_stream);
   if (ctx->svc_sh) (void)hipHostFree(ctx->svc_sh);
   if (ctx->svc_ring) (void)hipHostFree(ctx->svc_ring);
@@ -1080,11 +1144,10 @@ uint64_t qfec_async_ticket(const qfec_ctx* ctx) { return ctx ? ctx->last_ticket 
 int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait) {
   int rc = bind(ctx);
   if (rc) return rc;
-  auto f = ctx->finished.find(ticket);
-  if (f != ctx->finished.end()) {
-    rc = f->second.code;
-    ctx->finished.erase(f);
-    return rc;
+  qfec_ctx::Kept& f = ctx->kept[ticket % qfec_ctx::kKept];
+  if (ticket != 0 && f.ticket == ticket) {
+    f.ticket = 0;  // claimed once
+    return f.code;
   }
   for (int i = 0; i < kSlots; ++i)
     if (ctx->async_ops[i].live && ctx->async_ops[i].seq == ticket)
@@ -2003,6 +2066,8 @@ int qfec_phase_backoff(qfec_ctx* ctx) { return ctx ? (int)ctx->phase_backoff : -
 
 int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_phased : -1; }
 
+uint32_t qfec_debug_last_phase_grid(const qfec_ctx* ctx) { return ctx ? ctx->last_phase_grid : 0u; }
+
 int qfec_service_warm(qfec_ctx* ctx) {
   int rc = bind(ctx);
   if (rc) return rc;
@@ -2049,6 +2114,14 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
   return QFEC_OK;
 }
 
+int qfec_debug_service_hold(qfec_ctx* ctx, int hold) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  int rc = ensure_service(ctx);
+  if (rc) return rc;
+  __atomic_store_n(&ctx->svc_sh->hold, hold ? 1u : 0u, __ATOMIC_SEQ_CST);
+  return QFEC_OK;
+}
+
 int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
   int rc = ensure_service(ctx);
@@ -2089,6 +2162,15 @@ int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on) {
   int rc = bind(ctx);
   if (rc) return rc;
   ctx->no_regsteps = on ? 0u : 1u;
+  return QFEC_OK;
+}
+
+int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (batch != 0u && batch != 16u && batch != 32u)
+    return fail(ctx, QFEC_ERR_INTERNAL, "qfec_debug_phase_rtbatch: batch 0, 16 or 32");
+  ctx->rt_batch = batch;
   return QFEC_OK;
 }
 

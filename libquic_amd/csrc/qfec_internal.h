@@ -54,14 +54,21 @@ struct FixedArgs {
   // test hook (qfec_debug_phase_regsteps): phased launches without the
   // register-held steps (the A/B of DESIGN.md §4's per-k table)
   uint32_t no_regsteps = 0;
+  // CUs held by resident small-batch service workers of OTHER contexts on the
+  // device (round 6): the phased grid leaves them free
+  uint32_t svc_cus = 0;
+  // test hook (qfec_debug_phase_rtbatch): the runtime-k phased body's load
+  // batch (0: 32, the product; 16: round 5's)
+  uint32_t rt_batch = 0;
   // in-slot recover written in place (qfec_recover_inslot_batch with out ==
   // NULL; encode form, parity == nullptr): group g's output row is its own
   // row inplace_missing[g], which holds the redundancy on entry; nullptr: out
   const uint8_t* inplace_missing = nullptr;
 };
 
-// True if launch_fixed(a, nontemporal, ...) runs the phased kernel.
-bool fixed_uses_phases(const FixedArgs& a, bool nontemporal);
+// True if launch_fixed(a, nontemporal, ...) runs the phased kernel; *grid
+// (nullable): its workgroup count.
+bool fixed_uses_phases(const FixedArgs& a, bool nontemporal, uint32_t* grid = nullptr);
 
 struct RaggedArgs {
   const uint8_t* bytes;
@@ -108,11 +115,14 @@ struct SvcJob {
   uint32_t token;
   uint32_t tab_bytes; // table bytes in tab (<= kSvcTab)
   uint32_t t_off, t_len, t_ptr, t_poff, t_plen, t_miss, t_ooff;  // offsets into tab
-  // Round 5: a job whose header and tables fit the first kSvcHead bytes
-  // carries svc_head_hash of them (this word excluded), stored by the host
-  // LAST; the leader reads those bytes in every poll of the ring, so a job it
-  // finds whole there (hash, seq and start agree) needs no second PCIe round
-  // trip for its entry.  0 for a larger job (then never taken from a poll).
+  // Round 5: svc_head_hash of the entry's first min(entry size, kSvcHead)
+  // bytes (this word excluded), stored by the host LAST; the leader reads
+  // those bytes in every poll of the ring.  A job it finds whole there (hash,
+  // seq and start agree) needs no second PCIe round trip for its entry when
+  // it fits them; a larger job's header is then known from the poll, so its
+  // size is too, and the rest of its tables is copied in one pass (the
+  // followers copy it whole, announced with that size).  0 while the host
+  // writes the entry.
   uint64_t head_sum;
   alignas(16) uint8_t tab[kSvcTab];
 };
@@ -146,6 +156,8 @@ struct SvcShared {
                       // 0 on its way out
   uint32_t quit;      // host: exit now (context destroyed)
   uint32_t stamp_on;  // host (measurement hook): the worker records stamps[] for each job
+  uint32_t hold;      // host (test hook qfec_debug_service_hold): followers wait at
+                      // their start while it is 1 (a follower dispatched late)
   // the worker's words, stored every turn
   alignas(64) uint64_t consumed;  // worker: groups finished (a new worker starts here)
   uint64_t jobs;      // worker: jobs finished (stats)
@@ -158,24 +170,31 @@ struct SvcShared {
 };
 constexpr uint32_t kSvcRing = 8;
 // Round 5: the worker is kSvcWgs workgroups.  Workgroup 0 (the leader) polls
-// the host's pub_end and runs the alive / exit protocol above; it hands each
-// turn's end to the others (followers) through SvcDev in device memory, so
-// only the leader's decisions reach the host.  A job of more groups than one
-// workgroup has waves is split over every workgroup; each adds itself to its
-// ring entry's done counter after making its outputs visible and the last one
-// stores the token.  Smaller jobs are the leader's alone.
+// the host's pub_end, walks the published jobs and runs the alive / exit
+// protocol above, so only the leader's decisions reach the host.  A job of
+// more groups than one workgroup has waves is split over every workgroup;
+// each adds itself to its ring entry's done counter after making its outputs
+// visible and the last one stores the token.  Smaller jobs are the leader's
+// alone.
+// Round 6: the leader ANNOUNCES each split job to the followers
+// through SvcDev (job number and entry size, in order); a follower takes the
+// announcements one by one from its own count `taken`, which outlives the
+// launch, and reads no other ring entry.  A follower dispatched late (the CUs
+// held by another kernel) therefore still does every split job's share, and
+// a split job's entry, whose token waits for every follower, is never reused
+// under it.  At most kSlots (3) jobs are outstanding, so kSvcRing
+// announcement words never wrap onto one not yet taken.
 constexpr uint32_t kSvcWgs = 8;
 struct SvcDev {
-  uint64_t to;               // leader: the turn's published end (followers work up to it)
-  uint32_t ready;            // leader: this launch's epoch once `to` is valid
-  uint32_t exit;             // leader: this launch's epoch when the workers leave
-  uint32_t done[kSvcRing];   // workgroups finished per ring entry (kSvcWgs per split job)
-  // leader, just after `to`: the turn's first job's entry size when its poll
-  // found the head whole (the followers copy the entry in one pass), one
-  // word as a leader that runs ahead rewrites it: (uint32_t)to << 32 | (job &
-  // 0xFFFF) << 16 | bytes / 16 (0: size unknown)
-  uint64_t ent;
+  uint32_t exit;             // leader: this launch's epoch when it leaves (after its
+                             // last announcement)
+  uint32_t done[kSvcRing];   // workgroups finished per ring entry's split job (the
+                             // last resets it before the token)
+  uint64_t nsplit;           // leader: split jobs announced so far
+  uint64_t split[kSvcRing];  // announcement i at i % kSvcRing: job << 32 | entry bytes / 16
+  uint64_t taken[kSvcWgs];   // follower w: announcements taken (w = 0 unused)
 };
+// (the host zeroes SvcDev when it creates the service and when it abandons it)
 hipError_t launch_ragged_service(SvcShared* sh, SvcDev* dv, const SvcJob* ring, uint32_t* flags,
                                  uint64_t idle_ticks, uint32_t epoch, hipStream_t s);
 

@@ -114,41 +114,51 @@ __device__ __forceinline__ void xor_rows_n(u32x4& acc, const uint8_t* src, uint6
 }
 
 // Rows [0, k) of a group at runtime k: ceil(k / B) batches of loads in
-// flight, their sizes as even as possible (k = 20, B = 16: 10 + 10, not
-// 16 + 4 -- a batch is a round trip; tools/phase_k_table.py, round 5).
+// flight, their sizes as even as possible (k = 40, B = 32: 20 + 20, not
+// 32 + 8 -- a batch is a round trip).  The phased kernel (one wave per SIMD:
+// a lane's loads in flight are all the CU has) takes B = 32: round 5's
+// B = 16 split k = 20 into 10 + 10 and read at 0.743 / 0.683 of 8 TB/s
+// against 0.781 / 0.741 at k = 32 (16 + 16) (profiles/round5/
+// phase_k_table_r5b.txt; round 6: profiles/round6/phase_k_table_r6*.txt).
 template <int B, bool RECOVER, bool NT>
 __device__ __forceinline__ void xor_rows_rt(u32x4& acc, const uint8_t* src, uint64_t row_stride,
                                             uint32_t k, uint32_t m, const uint8_t* par) {
-  static_assert(B == 8 || B == 16, "batch of 8 or 16 rows");
+  static_assert(B == 8 || B == 16 || B == 32, "batch of 8, 16 or 32 rows");
   const uint32_t nb = (k + B - 1) / B;
   const uint32_t base = nb ? k / nb : 0u, extra = k - base * nb;
   uint32_t r = 0;
   for (uint32_t b = 0; b < nb; ++b) {
     const uint32_t n = base + (b < extra ? 1u : 0u);
-    switch (n) {
 #define QFEC_REM(N)                                                 \
   case N:                                                           \
     xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
     break;
-      QFEC_REM(1) QFEC_REM(2) QFEC_REM(3) QFEC_REM(4) QFEC_REM(5) QFEC_REM(6) QFEC_REM(7)
-      QFEC_REM(8)
-#undef QFEC_REM
-      default:
-        if constexpr (B == 16) {
-          switch (n) {
-#define QFEC_REM(N)                                                 \
-  case N:                                                           \
-    xor_rows_n<N, RECOVER, NT>(acc, src, row_stride, r, m, par);    \
-    break;
-            QFEC_REM(9) QFEC_REM(10) QFEC_REM(11) QFEC_REM(12) QFEC_REM(13) QFEC_REM(14)
-            QFEC_REM(15) QFEC_REM(16)
-#undef QFEC_REM
-            default:
-              break;
-          }
+    if (B == 8 || n <= 8u) {
+      switch (n) {
+        QFEC_REM(1) QFEC_REM(2) QFEC_REM(3) QFEC_REM(4) QFEC_REM(5) QFEC_REM(6) QFEC_REM(7)
+        QFEC_REM(8)
+        default:
+          break;
+      }
+    } else if constexpr (B >= 16) {
+      if (B == 16 || n <= 16u) {
+        switch (n) {
+          QFEC_REM(9) QFEC_REM(10) QFEC_REM(11) QFEC_REM(12) QFEC_REM(13) QFEC_REM(14)
+          QFEC_REM(15) QFEC_REM(16)
+          default:
+            break;
         }
-        break;
+      } else if constexpr (B == 32) {
+        switch (n) {
+          QFEC_REM(17) QFEC_REM(18) QFEC_REM(19) QFEC_REM(20) QFEC_REM(21) QFEC_REM(22)
+          QFEC_REM(23) QFEC_REM(24) QFEC_REM(25) QFEC_REM(26) QFEC_REM(27) QFEC_REM(28)
+          QFEC_REM(29) QFEC_REM(30) QFEC_REM(31) QFEC_REM(32)
+          default:
+            break;
+        }
+      }
     }
+#undef QFEC_REM
     r += n;
   }
 }
@@ -342,7 +352,7 @@ __device__ __forceinline__ void phase_exit(uint32_t* ps, uint32_t* host) {
 template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU = kPhUDefault,
           int STEPS = kPhSteps, int NTHR = kBlock, bool XCDW = false, bool PARFIRST = true,
           bool NTLD = true, bool EDGE = false, bool COMPACT = true, int RS = 0, bool RPF = false,
-          bool RPFE = false, bool INPL = false>
+          bool RPFE = false, bool INPL = false, int RTB = 32>
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   static_assert(!(INPL && RECOVER), "in place: the encode form over the k rows");
@@ -497,14 +507,14 @@ __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C
 #pragma unroll
           for (int r = 0; r < KC; ++r) acc[u] ^= v[u][r];
       } else {
-        // runtime k (> 16: every k up to 16 is templated): batches of 16
-        // loads in flight, the remainder as one batch (xor_rows_rt)
+        // runtime k (> 16: every k up to 16 is templated): batches of up
+        // to RTB loads in flight, as even as possible (xor_rows_rt)
 #pragma unroll
         for (int u = 0; u < kPhU; ++u) {
           const uint64_t g = gidx(i + u);
           const uint8_t* par = RECOVER ? a.parity + (lane_on && g < a.n_groups ? g : 0) * a.parity_stride + off
                                        : nullptr;
-          xor_rows_rt<16, RECOVER, NTLD>(acc[u], src[u], a.row_stride, k, m[u], par);
+          xor_rows_rt<RTB, RECOVER, NTLD>(acc[u], src[u], a.row_stride, k, m[u], par);
         }
       }
       if constexpr (RECOVER) {
@@ -750,11 +760,20 @@ __device__ __forceinline__ void wave_lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Lane src's x (ds_bpermute; src in [0, 64)).  The shuffles below take the
+// caller's lane instead of HIP's __shfl*, which recompute it (mbcnt) and
+// whose lane-derived addresses the compiler hoists out of a resident loop:
+// in the service worker they stayed live through the whole job body and
+// spilled to scratch at 256 VGPRs (round 6).
+__device__ __forceinline__ uint32_t lane_read(uint32_t x, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)x);
+}
+
 // Inclusive prefix sum over the wave.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    const uint32_t y = lane_read(x, lane >= (uint32_t)d ? lane - (uint32_t)d : lane);
     if (lane >= (uint32_t)d) x += y;
   }
   return x;
@@ -1492,14 +1511,14 @@ __device__ __forceinline__ WinOut window_group(const RaggedArgs& a, uint64_t g, 
   const uint32_t rA = slot_packet(lane), rB = slot_packet(lane + 64u);
   // (every shuffle with the whole wave active: a lane that reads an inactive
   // lane's value gets 0, so none sits under the `< ns` condition)
-  const uint32_t shA = (uint32_t)__shfl((int)len, (int)rA, 64);
-  const uint32_t shB = (uint32_t)__shfl((int)len, (int)rB, 64);
+  const uint32_t shA = lane_read(len, rA);
+  const uint32_t shB = lane_read(len, rB);
   const uint32_t lenA = lane < ns ? shA : 0u;
   const uint32_t lenB = lane + 64u < ns ? shB : 0u;
-  const uint32_t olA = (uint32_t)__shfl((int)offlo, (int)rA, 64);
-  const uint32_t ohA = (uint32_t)__shfl((int)offhi, (int)rA, 64);
-  const uint32_t olB = (uint32_t)__shfl((int)offlo, (int)rB, 64);
-  const uint32_t ohB = (uint32_t)__shfl((int)offhi, (int)rB, 64);
+  const uint32_t olA = lane_read(offlo, rA);
+  const uint32_t ohA = lane_read(offhi, rA);
+  const uint32_t olB = lane_read(offlo, rB);
+  const uint32_t ohB = lane_read(offhi, rB);
   // trip 3: every slot's bytes, PB loads in flight per lane.  Branch-free: a
   // slot past the end loads through a descriptor of 0 bytes (its length: the
   // bounds check returns zeros, no memory access; a real slot's load ends
@@ -1612,9 +1631,9 @@ __device__ __forceinline__ uint32_t svc_load32(const uint32_t* p) {
 // The ring entry's first `bytes` bytes (a multiple of 16) into LDS, every
 // thread 16 B per pass (the tables follow the header: one round trip).
 __device__ __forceinline__ void svc_copy_entry(const SvcJob* e, uint8_t* dst, uint32_t from,
-                                               uint32_t bytes) {
+                                               uint32_t bytes, uint32_t tid) {
   const uint8_t* src = reinterpret_cast<const uint8_t*>(e);
-  for (uint32_t o = from + 16u * threadIdx.x; o < bytes; o += 16u * 64u * kSvcWaves)
+  for (uint32_t o = from + 16u * tid; o < bytes; o += 16u * 64u * kSvcWaves)
     *reinterpret_cast<u32x4*>(dst + o) = ld16(src + o);
 }
 
@@ -1627,11 +1646,14 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   __shared__ u32x4 s_red[2][kSvcWaves * 64];  // a one-group job's partial windows
   __shared__ __attribute__((aligned(16))) uint8_t s_ent[sizeof(SvcJob)];
   __shared__ uint64_t s_from, s_to;
+  // the leader: split jobs it has announced; a follower: the next announcement it takes
+  __shared__ uint64_t s_split;
   __shared__ uint32_t s_job, s_exit, s_stamp;
   // the job whose entry size is known (s_need bytes; the leader: s_have of
   // them already in LDS from its poll), else no job
   __shared__ uint32_t s_entjob, s_have, s_need;
   static_assert(sizeof(SvcJob) % 16u == 0u, "entry copied in 16-B pieces");
+  static_assert(kSvcRing > 3u, "announcement ring: more entries than outstanding jobs");
   constexpr uint32_t kHead = (uint32_t)offsetof(SvcJob, tab);
   constexpr uint32_t kFirst = 4096u;  // first pass: the header and the first tables
   const uint32_t tid = threadIdx.x, lane = lane_id();
@@ -1640,112 +1662,224 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
   const bool lead = wg == 0u;
   const SvcJob& J = *reinterpret_cast<const SvcJob*>(s_ent);
   __shared__ uint64_t st[6];  // measurement hook (sh->stamp_on): the leader's stamps of a job (thread 0; LDS, not 12 VGPRs live through the job)
+
+  // This workgroup's share of job jj, whose entry is in LDS: a split job's
+  // group g on wave g / kSvcWgs of workgroup g % kSvcWgs (a 9..64-group job is
+  // one round, spread over the workgroups), a smaller one the leader's alone.
+  // Then its outputs visible, its count (split) and the token from the last.
+  auto run_job = [&](uint32_t jj, bool split) __attribute__((always_inline)) {
+    if (tid == 0) st[1] = wall_clock64();
+    // the job's tables live in LDS (generic pointers: flat loads)
+    RaggedArgs a = J.a;
+    a.pkt_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_off);
+    a.pkt_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_len);
+    a.grp_ptr = reinterpret_cast<const uint32_t*>(J.tab + J.t_ptr);
+    a.parity_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_poff);
+    if (J.recover) {
+      a.parity_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_plen);
+      a.missing = J.tab + J.t_miss;
+      a.out_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_ooff);
+    }
+    const uint64_t n = J.a.n_groups;
+    const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
+    if (n == 1u) {
+      // one group: every wave of the leader on it (its slots dealt round
+      // the waves: a wave issues an instruction every few cycles, and one
+      // wave alone spent ~1 us issuing a group's loads and shifting its
+      // windows), the partial windows XORed out of LDS by two waves
+      const WinOut o =
+          J.recover ? window_group<true, true, kSvcPB, kSvcWaves>(
+                          a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1])
+                    : window_group<false, true, kSvcPB, kSvcWaves>(
+                          a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1]);
+      __syncthreads();
+      if (o.red && wv < 2u) {
+        const u32x4* r = s_red[wv];
+        u32x4 x = r[lane];
+#pragma unroll
+        for (int q = 1; q < kSvcWaves; ++q) x ^= r[q * 64 + lane];
+        if (lane + 64u * wv < o.nwin) st16t<true>(o.dst + (wv == 0u ? o.w0 : o.w1), x);
+      }
+      if (tid == 0) st[2] = wall_clock64();
+    } else {
+      for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
+        if (J.recover)
+          window_group<true, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+        else
+          window_group<false, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
+        if (tid == 0 && g == 0) st[2] = wall_clock64();
+      }
+    }
+    // every wave's output stores acknowledged, then ONE system-scope
+    // release (thread 0's: its L2 write-back covers the workgroup) before
+    // the count / token -- not one per thread
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      st[3] = wall_clock64();
+      __threadfence_system();  // this workgroup's outputs visible before its count
+      st[4] = wall_clock64();
+      bool last = true;
+      if (split) {
+        // every workgroup takes every split job (announced to the followers,
+        // below), so the count reaches kSvcWgs exactly once per job; the
+        // last resets it for the entry's next split job (which the host
+        // publishes only after this job's token, stored after the reset)
+        last = __hip_atomic_fetch_add(&dv->done[jj % kSvcRing], 1u, __ATOMIC_ACQ_REL,
+                                      __HIP_MEMORY_SCOPE_SYSTEM) +
+                   1u ==
+               kSvcWgs;
+        if (last)
+          __hip_atomic_store(&dv->done[jj % kSvcRing], 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (last)
+        __hip_atomic_store(flags + J.flag_slot, J.token, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (s_stamp) {
+        st[5] = wall_clock64();
+        for (int q = 0; q < 6; ++q)
+          __hip_atomic_store(&sh->stamps[q], st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  };
+
+  // One loop for both roles and one run_job site, round 5's loop nest (a
+  // second site, or one job per turn of the outer loop, spilled 72-168 B of
+  // scratch at 256 VGPRs): each turn the leader polls and walks the jobs
+  // published so far; a follower takes one announcement of a split job.
+  // (round 5's followers walked the ring themselves from the
+  // host's `consumed`, read at their own start; a follower dispatched late
+  // -- the CUs held by another kernel -- started past a split job the leader
+  // had already counted and never did its share, so that job's token never
+  // came.  Now a follower starts at its own count of announcements taken,
+  // kept in device memory across launches, and reads only the entries of
+  // split jobs, whose tokens wait for it.)
   if (tid == 0) {
-    // where the previous worker stopped (stable: it has left): jobs are
-    // finished whole and in order, so the next job's number is the count
-    s_from = svc_load64(&sh->consumed);
-    s_job = (uint32_t)svc_load64(&sh->jobs);
-    s_stamp = lead ? svc_load32(&sh->stamp_on) : 0u;
     if (lead) {
-      __hip_atomic_store(&dv->to, s_from, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&dv->ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      // where the previous worker stopped (stable: it has left): jobs are
+      // finished whole and in order, so the next job's number is the count
+      s_from = svc_load64(&sh->consumed);
+      s_to = s_from;
+      s_job = (uint32_t)svc_load64(&sh->jobs);
+      s_stamp = svc_load32(&sh->stamp_on);
+      s_split = __hip_atomic_load(&dv->nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // running: a worker queued behind one that cleared `alive` on its way
       // out says so itself (the host then stops it before a phased
       // launch)
       __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      // test hook: a follower dispatched late (the hold released)
+      while (svc_load32(&sh->hold) != 0u) __builtin_amdgcn_s_sleep(8);
+      s_split = __hip_atomic_load(&dv->taken[wg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_stamp = 0u;
     }
   }
   __syncthreads();
+  // the leader announces split job jj (entry bytes `need`) to the followers (thread 0)
+  auto announce = [&](uint32_t jj, uint32_t need) {
+    const uint64_t i = s_split;
+    __hip_atomic_store(&dv->split[i % kSvcRing], ((uint64_t)jj << 32) | (need >> 4),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dv->nsplit, i + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    s_split = i + 1u;
+  };
+  bool miss = false;
   for (;;) {
-    if (lead && wv == 0u) {
-      // The leader's wave 0 polls.  Every look reads pub_end AND the next
-      // job's first kSvcHead bytes (16 per lane, relaxed system-scope loads,
-      // all in flight together: one PCIe round trip); when the look that sees
-      // the job holds it whole -- its head hash, seq and start agree -- the
-      // entry copy below is skipped (round 5: one round trip less per job).
-      const uint64_t from = s_from;
-      const uint32_t job0 = s_job;
-      const uint64_t* hp = reinterpret_cast<const uint64_t*>(ring + (job0 % kSvcRing)) + 2u * lane;
-      uint64_t h0 = 0, h1 = 0;
-      auto look = [&]() -> uint64_t {
-        const uint64_t t = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        h0 = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        h1 = __hip_atomic_load(hp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return t;
-      };
-      uint64_t to = look();
-      uint32_t ex = 0;
-      const uint64_t t0 = wall_clock64();
-      while (to == from) {
-        if (svc_load32(&sh->quit) != 0u) {
-          ex = 1;
-          break;
-        }
-        if (wall_clock64() - t0 > idle_ticks) {
-          // leaving: say so, then look once more (the host publishes, then
-          // reads alive: one of the two sees the other's store)
-          __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-          __atomic_thread_fence(__ATOMIC_SEQ_CST);
-          to = look();
-          if (to == from) {
+    // tid and lane redefined (opaquely) every turn of the worker's loop:
+    // nothing derived from them is hoisted out of it -- shuffle addresses,
+    // head-hash multipliers, slot masks were, live through the whole job
+    // body, and spilled to scratch at 256 VGPRs
+    if (lead) {
+      if (wv == 0u) {
+        // Wave 0 polls.  Every look
+        // reads pub_end AND the next job's first kSvcHead bytes (16 per lane,
+        // relaxed system-scope loads, all in flight together: one PCIe round
+        // trip); when the look that sees the job holds it whole -- its head
+        // hash, seq and start agree -- the entry copy below is skipped (round
+        // 5: one round trip less per job).
+        const uint64_t from = s_from;
+        const uint32_t job0 = s_job;
+        const uint32_t lane2 = 2u * lane;
+        const uint64_t* hp = reinterpret_cast<const uint64_t*>(ring + (job0 % kSvcRing)) + lane2;
+        uint64_t h0 = 0, h1 = 0;
+        auto look = [&]() -> uint64_t {
+          const uint64_t t = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          h0 = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          h1 = __hip_atomic_load(hp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return t;
+        };
+        uint64_t to = look();
+        uint32_t ex = 0;
+        const uint64_t t0 = wall_clock64();
+        while (to == from) {
+          if (svc_load32(&sh->quit) != 0u) {
             ex = 1;
             break;
           }
-          __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
+          if (wall_clock64() - t0 > idle_ticks) {
+            // leaving: say so, then look once more (the host publishes, then
+            // reads alive: one of the two sees the other's store)
+            __hip_atomic_store(&sh->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            to = look();
+            if (to == from) {
+              ex = 1;
+              break;
+            }
+            __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          to = look();
         }
-        __builtin_amdgcn_s_sleep(2);
-        to = look();
-      }
-      // the head found whole (its hash, seq and start agree): the entry's
-      // size is known -- a small job is all in LDS already, a larger one is
-      // copied in one pass by every workgroup (the followers learn the size
-      // with `to`) instead of a header pass and a table pass
-      if (lane == 0u) {
-        if (ex)
-          __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          __hip_atomic_store(&dv->to, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      uint32_t have = 0, need = 0;
-      if (!ex) {
-        uint64_t* sw = reinterpret_cast<uint64_t*>(s_ent);
-        sw[2u * lane] = h0;
-        sw[2u * lane + 1u] = h1;
-        wave_lds_order();
-        const uint32_t tbb = J.tab_bytes;
-        const uint32_t full = min((kHead + min(tbb, kSvcTab) + 15u) & ~15u, (uint32_t)sizeof(SvcJob));
-        const uint32_t nb = min(full, kSvcHead);
-        uint64_t part = 0;
-        if (2u * lane < nb / 8u && 2u * lane != kSvcHeadSumWord) part += svc_head_word(h0, 2u * lane);
-        if (2u * lane + 1u < nb / 8u && 2u * lane + 1u != kSvcHeadSumWord)
-          part += svc_head_word(h1, 2u * lane + 1u);
+        // the head found whole (its hash, seq and start agree): the entry's
+        // size is known -- a small job is all in LDS already, a larger one's
+        // header is, and the rest is copied in one pass
+        uint32_t have = 0, need = 0;
+        if (!ex) {
+          uint64_t* sw = reinterpret_cast<uint64_t*>(s_ent);
+          sw[lane2] = h0;
+          sw[lane2 + 1u] = h1;
+          wave_lds_order();
+          const uint32_t tbb = J.tab_bytes;
+          const uint32_t full = min((kHead + min(tbb, kSvcTab) + 15u) & ~15u, (uint32_t)sizeof(SvcJob));
+          const uint32_t nb = min(full, kSvcHead);
+          uint64_t part = 0;
+          if (lane2 < nb / 8u && lane2 != kSvcHeadSumWord) part += svc_head_word(h0, lane2);
+          if (lane2 + 1u < nb / 8u && lane2 + 1u != kSvcHeadSumWord)
+            part += svc_head_word(h1, lane2 + 1u);
 #pragma unroll
-        for (int d = 32; d > 0; d >>= 1) part += (uint64_t)__shfl_xor((unsigned long long)part, d, 64);
-        const bool whole = (part | 1ull) == J.head_sum && J.seq == job0 && J.start == from &&
-                           tbb <= kSvcTab;
-        have = whole ? nb : 0u;
-        need = whole ? full : 0u;
+          for (uint32_t d = 32; d > 0; d >>= 1)
+            part += ((uint64_t)lane_read((uint32_t)(part >> 32), lane ^ d) << 32) |
+                    lane_read((uint32_t)part, lane ^ d);
+          const bool whole = (part | 1ull) == J.head_sum && J.seq == job0 && J.start == from &&
+                             tbb <= kSvcTab;
+          have = whole ? nb : 0u;
+          need = whole ? full : 0u;
+        }
+        if (lane == 0u) {
+          st[0] = wall_clock64();
+          s_to = to;
+          s_exit = ex;
+          s_entjob = need != 0u ? job0 : 0xFFFFFFFFu;
+          s_have = have;
+          s_need = need;
+        }
       }
-      if (lane == 0u) {
-        st[0] = wall_clock64();
-        s_to = to;
-        s_exit = ex;
-        s_entjob = need != 0u ? job0 : 0xFFFFFFFFu;
-        s_have = have;
-        s_need = need;
-      }
-    } else if (!lead && tid == 0) {
-      // follower: the leader's word, from device memory (exit read first:
-      // a `to` stored before the exit is then seen and finished first)
-      const uint64_t from = s_from;
-      uint64_t to = from;
+    } else if (tid == 0) {
+      // follower: the next announcement, or the leader's exit
+      const uint64_t mine = s_split;
+      uint64_t ann = 0;
       uint32_t ex = 0;
       for (;;) {
+        // the exit word first: the leader stores it after its last
+        // announcement, so an exit seen here means nsplit is final
         const uint32_t e = __hip_atomic_load(&dv->exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_load(&dv->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
-          to = __hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          if (to > from) break;
+        if (__hip_atomic_load(&dv->nsplit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) > mine) {
+          ann = __hip_atomic_load(&dv->split[mine % kSvcRing], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+          break;
         }
         if (e == epoch) {
           ex = 1;
@@ -1753,153 +1887,90 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      s_to = to;
       s_exit = ex;
+      s_entjob = (uint32_t)(ann >> 32);
       s_have = 0u;
-      s_entjob = 0xFFFFFFFFu;
-      s_need = 0u;
-      while (!ex) {
-        // the leader's word on this turn's first entry (stored a moment after
-        // `to`); a leader gone on to a later turn: size unknown
-        const uint64_t ent = __hip_atomic_load(&dv->ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(ent >> 32) == (uint32_t)to) {
-          s_need = (uint32_t)(ent & 0xFFFFu) << 4;
-          s_entjob = s_job + ((((uint32_t)(ent >> 16) & 0xFFFFu) - s_job) & 0xFFFFu);
-          break;
-        }
-        if (__hip_atomic_load(&dv->to, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != to) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
+      s_need = (uint32_t)(ann & 0xFFFFu) << 4;
     }
     __syncthreads();
     if (s_exit) break;
     // every thread: drop cached copies of host memory (ring entries, payloads)
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    // the leader's word for the followers: after its fence, so the store's
-    // completion does not hold up the leader's own acquire
-    if (lead && tid == 0)
-      __hip_atomic_store(&dv->ent,
-                         ((uint64_t)(uint32_t)s_to << 32) | ((uint64_t)(s_entjob & 0xFFFFu) << 16) |
-                             (s_need >> 4),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the leader: the published jobs, in order (pub_end moves by whole
+    // jobs); a follower: the one announced
     const uint64_t to = s_to;
     uint64_t gi = s_from;
-    uint32_t jj = s_job;
-    bool miss = false;
-    while (gi < to) {  // the published jobs, in order (pub_end moves by whole jobs)
+    uint32_t jj = lead ? s_job : s_entjob;
+    bool once = true;
+    while (lead ? gi < to : once) {
+      once = false;
       const SvcJob* e = ring + (jj % kSvcRing);
-      // a job of known size in one pass (the leader's poll may hold some or
-      // all of it already), else the header and first tables, then the rest
+      // a job of known size in one pass (the leader's poll holds its header
+      // and maybe all of it), else the header and first tables, then the rest
       const uint32_t have = jj == s_entjob ? s_have : 0u;
       const uint32_t need = jj == s_entjob ? s_need : 0u;
+      // a split job whose header the poll holds: announced before the copy,
+      // so the followers' entry copies overlap the leader's
+      if (lead && need != 0u && tid == 0 && J.a.n_groups > (uint64_t)kSvcWaves) announce(jj, need);
       if (need == 0u)
-        svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)));
+        svc_copy_entry(e, s_ent, 0u, min(kFirst, (uint32_t)sizeof(SvcJob)), tid);
       else if (have < need)
-        svc_copy_entry(e, s_ent, have, need);
+        svc_copy_entry(e, s_ent, have, min(need, (uint32_t)sizeof(SvcJob)), tid);
       __syncthreads();
-      if (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab) {
+      if (lead && (J.seq != jj || gi != J.start || J.tab_bytes > kSvcTab)) {
         // a malformed ring: nothing of this turn is done
-        // (every workgroup reads the same entry and stops here too)
+        // (and no announcement of it)
         miss = true;
         break;
       }
       const uint64_t n = J.a.n_groups;
       const bool split = n > (uint64_t)kSvcWaves;
-      if (split || lead) {
-        if (need == 0u && kHead + J.tab_bytes > kFirst) {  // a large job's tables: a second pass
-          svc_copy_entry(e, s_ent, kFirst, (kHead + J.tab_bytes + 15u) & ~15u);
+      if (lead && need == 0u) {
+        const uint32_t full = (kHead + J.tab_bytes + 15u) & ~15u;
+        if (split && tid == 0) announce(jj, full);
+        if (full > kFirst) {  // a large job's tables: a second pass
+          svc_copy_entry(e, s_ent, kFirst, full, tid);
           __syncthreads();
-        }
-        if (tid == 0) st[1] = wall_clock64();
-        // the job's tables live in LDS now (generic pointers: flat loads)
-        RaggedArgs a = J.a;
-        a.pkt_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_off);
-        a.pkt_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_len);
-        a.grp_ptr = reinterpret_cast<const uint32_t*>(J.tab + J.t_ptr);
-        a.parity_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_poff);
-        if (J.recover) {
-          a.parity_len = reinterpret_cast<const uint16_t*>(J.tab + J.t_plen);
-          a.missing = J.tab + J.t_miss;
-          a.out_off = reinterpret_cast<const uint64_t*>(J.tab + J.t_ooff);
-        }
-        // split: group g on wave g / kSvcWgs of workgroup g % kSvcWgs (a
-        // 9..64-group job is one round, spread over the workgroups)
-        const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
-        if (n == 1u) {
-          // one group: every wave of the leader on it (its slots dealt round
-          // the waves: a wave issues an instruction every few cycles, and one
-          // wave alone spent ~1 us issuing a group's loads and shifting its
-          // windows), the partial windows XORed out of LDS by two waves
-          const WinOut o =
-              J.recover ? window_group<true, true, kSvcPB, kSvcWaves>(
-                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1])
-                        : window_group<false, true, kSvcPB, kSvcWaves>(
-                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1]);
-          __syncthreads();
-          if (o.red && wv < 2u) {
-            const u32x4* r = s_red[wv];
-            u32x4 x = r[lane];
-#pragma unroll
-            for (int q = 1; q < kSvcWaves; ++q) x ^= r[q * 64 + lane];
-            if (lane + 64u * wv < o.nwin) st16t<true>(o.dst + (wv == 0u ? o.w0 : o.w1), x);
-          }
-          if (tid == 0) st[2] = wall_clock64();
-        } else {
-          for (uint64_t g = split ? (uint64_t)wv * kSvcWgs + wg : wv; g < n; g += step) {
-            if (J.recover)
-              window_group<true, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-            else
-              window_group<false, true, kSvcPBw>(a, g, lane, s_par[wv], s_head[wv], s_meta[wv]);
-            if (tid == 0 && g == 0) st[2] = wall_clock64();
-          }
-        }
-        // every wave's output stores acknowledged, then ONE system-scope
-        // release (thread 0's: its L2 write-back covers the workgroup) before
-        // the count / token -- not one per thread
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          st[3] = wall_clock64();
-          __threadfence_system();  // this workgroup's outputs visible before its count
-          st[4] = wall_clock64();
-          bool last = true;
-          if (split)
-            last = (__hip_atomic_fetch_add(&dv->done[jj % kSvcRing], 1u, __ATOMIC_ACQ_REL,
-                                           __HIP_MEMORY_SCOPE_SYSTEM) +
-                    1u) % kSvcWgs == 0u;
-          if (last)
-            __hip_atomic_store(flags + J.flag_slot, J.token, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-          if (s_stamp) {
-            st[5] = wall_clock64();
-            for (int q = 0; q < 6; ++q)
-              __hip_atomic_store(&sh->stamps[q], st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
         }
       }
+      // (a follower's entry cannot be wrong while the host keeps its ring:
+      // the entry of a split job is reused only after its token, which waits
+      // for this workgroup)
+      const bool ok = lead || (J.seq == jj && split && J.tab_bytes <= kSvcTab &&
+                               kHead + J.tab_bytes <= need);
+      if (ok) run_job(jj, split);
+      // no share, so no token: the host's wait sees the fault once the
+      // worker has left, and fails the job instead of reporting stale output
+      if (!ok && tid == 0) __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
       gi = J.start + n;
       ++jj;
       __syncthreads();  // s_ent is the next job's
     }
-    if (miss) {
-      // latch the fault and leave WITHOUT this job's token -- the host's wait
-      // sees the stream drained and the fault word and fails the job instead
-      // of reporting stale output as finished
-      if (tid == 0 && lead) {
-        __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      break;
-    }
+    if (miss) break;
     if (tid == 0) {
-      s_job = jj;
-      s_from = to;
       if (lead) {
+        s_job = jj;
+        s_from = to;
         __hip_atomic_store(&sh->consumed, to, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&sh->jobs, (uint64_t)jj, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        s_split = s_split + 1u;
       }
     }
     __syncthreads();
+  }
+  if (tid == 0) {
+    if (lead) {
+      // latch a malformed ring's fault and leave WITHOUT the job's token --
+      // the host's wait sees the stream drained and the fault word and fails
+      // the job instead of reporting stale output as finished
+      if (miss) __hip_atomic_store(&sh->fault, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+      // the followers leave once they have taken every announcement (this
+      // store is after the last one: release)
+      __hip_atomic_store(&dv->exit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&dv->taken[wg], s_split, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // (no store to `alive` here: an idle exit cleared it before its last look,
   // and a late store could clobber the 1 the host wrote for a worker it has
@@ -2060,9 +2131,18 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
     QFEC_K_ALL(QFEC_K_CASE)
 #undef QFEC_K_CASE
     default:
-      hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
-                                           false, true, true, false, true, 0, false, false, INPL>),
-                         dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
+      // runtime k: batches of up to 32 loads (test hook rt_batch = 16: round
+      // 5's batches, the A/B of tools/phase_k_table.py)
+      if (a.rt_batch == 16u)
+        hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
+                                             false, true, true, false, true, 0, false, false, INPL,
+                                             16>),
+                           dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
+      else
+        hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
+                                             false, true, true, false, true, 0, false, false, INPL,
+                                             32>),
+                           dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
   }
   return hipGetLastError();
 }
@@ -2102,7 +2182,11 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   if (a.phase_min == 0 &&
       a.k < (a.parity != nullptr ? kPhMinKRecover : kPhMinKEncode))
     return false;
-  const uint32_t wg = a.ncu + std::min<uint32_t>(a.phase_extra, 64u);
+  // resident service workers of other contexts hold svc_cus CUs' LDS: the
+  // grid leaves them, so every workgroup is resident and the meetings hold
+  // (round 6); more than a quarter of the device so held: one-pass
+  if (a.svc_cus > a.ncu / 4u) return false;
+  const uint32_t wg = a.ncu - a.svc_cus + std::min<uint32_t>(a.phase_extra, 64u);
   // the threshold counts phases of the LDS steps alone (the measured band);
   // the launch's phases hold the register steps too (k = 10)
   const uint64_t per = (uint64_t)wg * kPhSteps * gpb;
@@ -2125,10 +2209,12 @@ uint32_t phase_steps_for(const FixedArgs& a, uint32_t gpb, uint32_t grid, uint32
 
 }  // namespace
 
-bool fixed_uses_phases(const FixedArgs& a, bool nontemporal) {
+bool fixed_uses_phases(const FixedArgs& a, bool nontemporal, uint32_t* grid) {
   if (!a.phase_sync || !nontemporal || a.L < 16u || a.n_groups == 0) return false;
-  uint32_t grid = 0, nphase = 0;
-  return phase_plan(a, kBlock / ((a.L + 15u) / 16u), &grid, &nphase);
+  uint32_t g = 0, nphase = 0;
+  const bool on = phase_plan(a, kBlock / ((a.L + 15u) / 16u), &g, &nphase);
+  if (grid) *grid = on ? g : 0u;
+  return on;
 }
 
 hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {

@@ -101,10 +101,13 @@ SIGNATURES = [
     ("qfec_debug_phase", C.c_int, [_vp, C.c_uint32, C.c_int]),
     ("qfec_debug_phase_min", C.c_int, [_vp, C.c_uint32]),
     ("qfec_debug_phase_regsteps", C.c_int, [_vp, C.c_int]),
+    ("qfec_debug_phase_rtbatch", C.c_int, [_vp, C.c_uint32]),
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
+    ("qfec_debug_last_phase_grid", C.c_uint32, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_debug_service", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_stamps", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
+    ("qfec_debug_service_hold", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
     ("qfec_complete_ticket", C.c_int, [_vp, C.c_uint64, C.c_int]),
@@ -418,6 +421,10 @@ class Context:
         one-pass kernel, -1 none yet."""
         return self.lib.qfec_last_fixed_phased(self.ctx)
 
+    def last_phase_grid(self):
+        """Test hook: workgroups of the last phased launch (0: one-pass)."""
+        return self.lib.qfec_debug_last_phase_grid(self.ctx)
+
     def debug_phase(self, extra, reset_backoff=True):
         """Test hook: extra workgroups in phased launches (forces the abandon
         path); reset_backoff clears the contention backoff."""
@@ -459,9 +466,17 @@ class Context:
         self._check(self.lib.qfec_debug_service_stamps(self.ctx, -1 if on is None else int(bool(on)), st))
         return list(st)
 
+    def debug_service_hold(self, hold):
+        """Test hook: the service's followers wait at their start while held."""
+        return self._check(self.lib.qfec_debug_service_hold(self.ctx, 1 if hold else 0))
+
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""
         return self._check(self.lib.qfec_debug_phase_regsteps(self.ctx, 1 if on else 0))
+
+    def debug_phase_rtbatch(self, batch):
+        """Test hook: the runtime-k phased body's load batch (16, 32; 0 = default 32)."""
+        return self._check(self.lib.qfec_debug_phase_rtbatch(self.ctx, batch))
 
     def complete(self, wait=True):
         """Finish QFEC_ASYNC calls: 0 done, QFEC_PENDING (1) still running."""

@@ -103,7 +103,8 @@ def test_default_kernel_choice_by_group_size(ctx, k):
 
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
                                  (5, 17), (2, 16), (4, 1350), (8, 1001), (6, 1350), (12, 1350),
-                                 (20, 1350), (17, 100), (40, 64)])
+                                 (20, 1350), (17, 100), (40, 64), (64, 1350), (255, 1350),
+                                 (48, 300)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
@@ -366,3 +367,39 @@ def test_phased_register_steps_identical(ctx, k, L):
     assert torch.equal(res[True][1], res[False][1])
     r3 = rows.view(n, k, L)
     assert torch.equal(r3[torch.arange(n, device=DEV), miss.long()], res[True][1].view(n, L))
+
+
+@pytest.mark.parametrize("k,L", [(20, 1350), (64, 1350), (255, 200)])
+def test_runtime_k_load_batch_identical(ctx, k, L):
+    """Group sizes above 16 run the runtime-k phased body; round 6 loads up
+    to 32 rows per batch (round 5: 16; qfec_debug_phase_rtbatch selects it).
+    Both batches give the same bytes, the revived row is the lost row, and
+    sampled groups match the oracle."""
+    n = 8 * phase_groups(L) + 91
+    rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
+    ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+    miss_np = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
+    miss = torch.from_numpy(miss_np).to(DEV)
+    res = {}
+    ctx.debug_phase_min(6)
+    try:
+        for b in (16, 32):
+            ctx.debug_phase_rtbatch(b)
+            par = torch.full((n * L,), 0xA5, dtype=torch.uint8, device=DEV)
+            out = torch.full((n * L,), 0x5A, dtype=torch.uint8, device=DEV)
+            ctx.encode(rows, k, L, n, par)
+            assert ctx.last_fixed_phased() == 1
+            ctx.recover(rows, par, miss, k, L, n, out)
+            assert ctx.last_fixed_phased() == 1
+            ctx.sync()
+            torch.cuda.synchronize()
+            res[b] = (par, out)
+    finally:
+        ctx.debug_phase_rtbatch(0)
+        ctx.debug_phase_min(0)
+    assert torch.equal(res[16][0], res[32][0])
+    assert torch.equal(res[16][1], res[32][1])
+    r3 = rows.view(n, k, L)
+    assert torch.equal(r3[torch.arange(n, device=DEV), miss.long()], res[32][1].view(n, L))
+    sample_vs_oracle(r3, res[32][0].cpu().numpy(), res[32][1].cpu().numpy(), miss_np, k, L, n,
+                     count=16)

@@ -11,7 +11,9 @@ GPU box; one JSON line per k, then a summary.
 
 The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers,
 and the library's default choice (no test hook) after them.  k > 16 has no
-register steps (runtime-k body): its two phased columns are the same kernel.
+register steps (runtime-k body): its two phased columns are the load batch of
+32 (round 6, the default) and of 16 (round 5's, qfec_debug_phase_rtbatch),
+over 2^18 groups above k = 32.
 """
 import json
 import os
@@ -31,13 +33,16 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     dev = torch.device("cuda:0")
-    G, L = 1 << 20, 1350
+    L = 1350
     ctx = qfec.Context(0)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
     out_rows = []
     ks = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2, 4, 5, 8, 10, 16]
     for k in ks:
+        # 2^20 groups up to k = 32; above, 2^18 (>= 8 phases of 40 steps on
+        # 256 CUs, 90 GB at k = 255)
+        G = 1 << 20 if k <= 32 else 1 << 18
         rows = torch.empty(G * k * L, dtype=torch.uint8, device=dev)
         ctx.synth_fixed(rows, k, L, 0, G, 0x5EED0000 + k)
         miss = torch.from_numpy(
@@ -51,7 +56,10 @@ def main():
         for r in range(rounds):
             for m in (1, 0, 2, 3):  # 1: register steps, 0: LDS steps only, 2: one-pass,
                 # 3: the library's default choice (no hook)
-                ctx.debug_phase_regsteps(m != 0)
+                # k > 16 (runtime-k body, no register steps): mode 0 is the
+                # round-5 load batch of 16 instead, mode 1 the default 32
+                ctx.debug_phase_regsteps(m != 0 or k > 16)
+                ctx.debug_phase_rtbatch(16 if (m == 0 and k > 16) else 0)
                 # phased forms at every k (the library's default picks one-pass
                 # below k = 5 / 8 since round 4, from this very table)
                 ctx.debug_phase_min(6 if m in (0, 1) else 0)
@@ -72,6 +80,7 @@ def main():
                     t[(m, op)].append(e0.elapsed_time(e1) / reps / 1e3)
                     phased[(m, op)] = ctx.last_fixed_phased()
         ctx.debug_phase_regsteps(True)
+        ctx.debug_phase_rtbatch(0)
         ctx.debug_phase_min(0)
         ctx.sync()
         torch.cuda.synchronize()
