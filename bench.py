@@ -54,6 +54,8 @@ def parse(argv=None):
     p.add_argument("--no-protect", action="store_true")
     p.add_argument("--no-entropy", action="store_true")
     p.add_argument("--no-connection", action="store_true")
+    p.add_argument("--no-beside-service", action="store_true",
+                   help="skip the phased encode beside another context's resident worker")
     p.add_argument("--no-fused", action="store_true")
     p.add_argument("--no-ceilings", action="store_true")
     p.add_argument("--no-verify", action="store_true")
@@ -430,6 +432,106 @@ def bench_inslot(work, steps, verify=True):
     return res
 
 
+def bench_phase_beside_service(work, reps=6):
+    """the headline encode (phased) on context A while a
+    connection thread keeps context B's small-batch worker resident (the
+    reference's model, one thread per QuicConnection, quic_connection.h:14):
+    B warms its worker and flushes one-group mapped batches back to back.  A's
+    phased grid leaves B's 8 CUs out (qfec_capi.cpp other_service_cus), so no
+    launch abandons its meetings.  Reported: A's encode frac (HIP events on
+    A's stream), its grid, abandoned launches, B's jobs meanwhile and whether
+    A's parity equals the uncontended steps' parity."""
+    import threading
+    from libquic_amd import qfec
+    torch, ctx, s = work.torch, work.ctx, work.stream
+    k, L, G = work.k, work.L, work.G
+    want = work.par.clone()
+    stop, ready = threading.Event(), threading.Event()
+    st = {"jobs": 0, "bad": 0, "err": None, "launches": None}
+
+    def feeder():
+        try:
+            b = qfec.Context(work.dev.index)
+            data, par = qfec.HostBuffer(10 * 1350), qfec.HostBuffer(1350)
+            try:
+                rng = np.random.default_rng(5)
+                data.array[:] = rng.integers(0, 256, 10 * 1350, dtype=np.uint8)
+                off = np.arange(10, dtype=np.uint64) * np.uint64(1350)
+                ln = np.full(10, 1350, np.uint16)
+                ptr = np.array([0, 10], np.uint32)
+                poff = np.zeros(1, np.uint64)
+                plen = np.zeros(1, np.uint16)
+                exp = np.bitwise_xor.reduce(data.array.reshape(10, 1350), axis=0)
+                while not stop.is_set():
+                    b.service_warm()  # the loop turn's start
+                    b.encode_ragged(data.array, off, ln, ptr, 1, par.array, poff, plen,
+                                    mapped=True)
+                    st["jobs"] += 1
+                    st["bad"] += int(not np.array_equal(par.array, exp))
+                    if st["jobs"] == 20:
+                        ready.set()
+                st["launches"] = b.debug_service()["launches"]
+            finally:
+                data.close()
+                par.close()
+                b.close()
+        except Exception as e:  # reported on the line
+            st["err"] = repr(e)
+            ready.set()
+
+    # Each timed launch is queued behind a ~30 ms spin kernel on its stream, so
+    # the events bracket the kernel alone: the feeder thread holds the GIL
+    # between its calls, and an event recorded before a launch the main
+    # thread is still waiting to issue would time that wait too.
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(s)
+    torch.cuda._sleep(1 << 24)
+    c1.record(s)
+    c1.synchronize()
+    spin = max(1 << 20, int((1 << 24) * 30.0 / max(c0.elapsed_time(c1), 1e-3)))
+
+    def encodes(grids):
+        secs = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(spin)
+            e0.record(s)
+            ctx.encode(work.rows, k, L, G, work.par)
+            e1.record(s)
+            grids.append(ctx.last_phase_grid())
+            e1.synchronize()
+            secs.append(e0.elapsed_time(e1) / 1e3)
+        return float(np.mean(secs[1:])) if len(secs) > 1 else float(secs[0])
+
+    alone = encodes([])  # the same launches without the other context
+    th = threading.Thread(target=feeder)
+    th.start()
+    ready.wait(60)
+    before = ctx.phase_abandons()
+    grids = []
+    j0 = st["jobs"]
+    try:
+        enc = encodes(grids)
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    jobs = st["jobs"] - j0
+    work.synchronize()
+    same = bool(torch.equal(work.par, want))
+    del want
+    return {"encode_frac": round(work.bytes_encode / enc / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_us": round(enc * 1e6, 2),
+            "alone_encode_frac": round(work.bytes_encode / alone / 1e9 / HBM_PEAK_GBS, 4),
+            "grids": grids, "ncu": torch.cuda.get_device_properties(work.dev.index).multi_processor_count,
+            "abandoned": ctx.phase_abandons() - before,
+            "service_jobs_meanwhile": jobs, "service_launches": st["launches"],
+            "service_wrong": st["bad"], "service_error": st["err"],
+            "parity_equal_uncontended": same,
+            "note": "context A's phased encode of the headline batch while a thread keeps context "
+                    "B's small-batch worker resident (qfec_service_warm + one-group mapped flushes "
+                    "back to back); mean of the last reps-1 launches"}
+
+
 def measured_traffic(G, k, L, phased=False):
     """PMC bytes per encode launch (tools/pmc.sh -> profiles/traffic_latest.json),
     when that run measured this shape with the same kernel (phased or one-pass)."""
@@ -680,6 +782,10 @@ def main(argv=None):
     if extras and not args.one_pass:
         line["recover_inslot"] = bench_inslot(work, max(4, args.steps // 2 * 2),
                                               verify=not args.no_verify)
+    if extras and not args.one_pass and phased and not args.no_beside_service:
+        work.step()  # the parity the contended encodes must reproduce
+        line["phase_beside_service"] = bench_phase_beside_service(work)
+        _progress("phase beside service done")
     if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)
         if line["roofline"]:  # the encode kernel against this box's measured streaming read
@@ -762,6 +868,10 @@ def line_summary(line):
     for leg in ("one_pass", "ragged", "ragged_packed"):
         if isinstance(line.get(leg), dict):
             s[leg] = {kk: line[leg].get(kk) for kk in ("encode_frac", "recover_frac")}
+    pb = line.get("phase_beside_service")
+    if isinstance(pb, dict):
+        s["phase_beside_service"] = {kk: pb.get(kk) for kk in
+                                     ("encode_frac", "alone_encode_frac", "abandoned")}
     ri = line.get("recover_inslot")
     if isinstance(ri, dict):
         s["recover_inslot_frac"] = {kk: g(ri, kk, "frac") for kk in ("out_of_place", "in_place")}

@@ -440,9 +440,14 @@ int qfec_debug_phase_min(qfec_ctx* ctx, uint32_t min_phases);
  * the per-group-size A/B; results are identical. */
 int qfec_debug_phase_regsteps(qfec_ctx* ctx, int on);
 /* Test hook: the load batch of the runtime-k phased body (group sizes above
- * 16): 16 (round 5's) or 32 (the default; 0 restores it).  For the
- * per-group-size A/B; results are identical. */
+ * 16): 16 or 32 (0 restores the library's measured per-operation choice:
+ * encode 16, recover 32 up to k = 32).  For the per-group-size A/B
+ * (DESIGN.md §4); results are identical. */
 int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch);
+/* Test hook: phased launches leave `cus` more CUs out of their grid (0..64),
+ * as if other contexts' small-batch workers held them -- the A/B of the
+ * round-6 CU arbitration; results are identical. */
+int qfec_debug_phase_reserve(qfec_ctx* ctx, uint32_t cus);
 /* Test hook: fail != 0 makes every ragged call on this context fail with
  * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
  * connection integration: groups go without FEC). */

@@ -100,6 +100,7 @@ struct qfec_ctx {
   uint32_t phase_min = 0;    // test hook (qfec_debug_phase_min)
   uint32_t no_regsteps = 0;  // test hook (qfec_debug_phase_regsteps)
   uint32_t rt_batch = 0;     // test hook (qfec_debug_phase_rtbatch)
+  uint32_t phase_reserve = 0;  // test hook (qfec_debug_phase_reserve)
   bool debug_fail = false;   // test hook (qfec_debug_fail_launches)
   uint32_t* h_flag = nullptr;
   uint32_t* h_flag_dev = nullptr;
@@ -275,14 +276,20 @@ constexpr uint64_t kSvcGroups = 64;
 constexpr uint64_t kSvcIdleTicks = 10000;
 
 // Process-wide registry of the contexts that run a small-batch service
-// (VERDICT r5 item 3): a phased launch on one context counts the workers of
-// the OTHERS on its device that are resident (or queued) and leaves their CUs
-// out of its grid.  A worker is kSvcWgs workgroups of 512 lanes at 252 VGPRs
-// and 57 KiB of LDS: each holds a CU whose LDS a phased workgroup (160 KiB)
-// can no longer get, so a full one-per-CU grid would not be resident and its
-// meetings would time out (round 5: 0.6-0.7x, abandoned).  The model is the
-// reference's: one connection thread per QuicConnection
-// (quic_connection.h:14), here one context per thread, several per process.
+// (VERDICT r5 item 3): a phased launch on one context leaves the CUs of the
+// OTHER contexts' workers on its device out of its grid.  A worker is kSvcWgs
+// workgroups of 512 lanes at 252 VGPRs and 57 KiB of LDS: each holds a CU
+// whose LDS a phased workgroup (160 KiB) can no longer get, so a full
+// one-per-CU grid would not be resident and its meetings would time out
+// (round 5: 0.6-0.7x, abandoned).  The model is the reference's: one
+// connection thread per QuicConnection (quic_connection.h:14), here one
+// context per thread, several per process.
+// Every registered context with its service on counts, resident or not: a
+// worker that is relaunched by its connection thread while the phased grid is
+// being dispatched would otherwise take CUs the grid was sized for (measured
+// on the box: one launch in four abandoned when only resident workers were
+// counted).  Leaving 8 of 256 CUs idle costs the phased encode nothing
+// measurable (it is HBM-bound: bench leg `phase_beside_service`).
 std::mutex g_svc_mu;
 std::vector<qfec_ctx*> g_svc_ctxs;
 
@@ -291,7 +298,8 @@ uint32_t other_service_cus(const qfec_ctx* ctx) {
   uint32_t n = 0;
   for (const qfec_ctx* c : g_svc_ctxs)
     if (c != ctx && c->device == ctx->device && c->svc_sh &&
-        (__atomic_load_n(&c->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ||
+        (__atomic_load_n(&c->svc_on, __ATOMIC_ACQUIRE) ||
+         __atomic_load_n(&c->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ||
          hipStreamQuery(c->svc_stream) == hipErrorNotReady))
       n += qfec::kSvcWgs;
   return n;
@@ -431,7 +439,7 @@ void stop_service(qfec_ctx* ctx) {
 // to the next call, so no later worker may run it over the reused tables.
 // The context's small batches then take the direct path.
 void svc_abandon(qfec_ctx* ctx) {
-  ctx->svc_on = false;
+  __atomic_store_n(&ctx->svc_on, false, __ATOMIC_RELEASE);
   if (!ctx->svc_sh) return;
   stop_service(ctx);
   for (uint32_t i = 0; i < qfec::kSvcRing; ++i)
@@ -848,7 +856,7 @@ int fixed_device(qfec_ctx* ctx, qfec::FixedArgs& a, uint32_t flags) {
   bool phased = a.phase_sync && qfec::fixed_uses_phases(a, nt);
   if (phased) {
     // (the registry only for a batch that would phase at all)
-    a.svc_cus = other_service_cus(ctx);
+    a.svc_cus = other_service_cus(ctx) + ctx->phase_reserve;
     phased = qfec::fixed_uses_phases(a, nt, &grid);
   }
   if (phased) {
@@ -1656,7 +1664,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
         // the service could not be set up or (re)launched: off for this
         // context, this batch launched as before (same flag and token), its
         // tables moved from the ring entry to the slot buffer the launch reads
-        ctx->svc_on = false;
+        __atomic_store_n(&ctx->svc_on, false, __ATOMIC_RELEASE);
         svc = false;
         std::memcpy(s.h_in, je->tab, t.total);
       }
@@ -2083,7 +2091,7 @@ int qfec_service_warm(qfec_ctx* ctx) {
                                                    ctx->svc_stream);
   if (e != hipSuccess) {
     __atomic_store_n(&sh->alive, 0u, __ATOMIC_SEQ_CST);
-    ctx->svc_on = false;
+    __atomic_store_n(&ctx->svc_on, false, __ATOMIC_RELEASE);
     return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
   }
   ++ctx->svc_launches;
@@ -2095,11 +2103,11 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
   if (on == 2) {
     // test hook: the next job's ring entry is written with
     // a wrong job number, so the worker finds its groups in no entry
-    ctx->svc_on = true;
+    __atomic_store_n(&ctx->svc_on, true, __ATOMIC_RELEASE);
     ctx->svc_poison_next = true;
     if (ctx->svc_sh) __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
   } else if (on >= 0) {
-    ctx->svc_on = on != 0;
+    __atomic_store_n(&ctx->svc_on, on != 0, __ATOMIC_RELEASE);
     if (!ctx->svc_on) {
       stop_service(ctx);  // a resident worker leaves at once
     } else if (ctx->svc_sh) {
@@ -2171,6 +2179,14 @@ int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch) {
   if (batch != 0u && batch != 16u && batch != 32u)
     return fail(ctx, QFEC_ERR_INTERNAL, "qfec_debug_phase_rtbatch: batch 0, 16 or 32");
   ctx->rt_batch = batch;
+  return QFEC_OK;
+}
+
+int qfec_debug_phase_reserve(qfec_ctx* ctx, uint32_t cus) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (cus > 64u) return fail(ctx, QFEC_ERR_INTERNAL, "qfec_debug_phase_reserve: at most 64 CUs");
+  ctx->phase_reserve = cus;
   return QFEC_OK;
 }
 

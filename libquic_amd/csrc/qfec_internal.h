@@ -58,7 +58,7 @@ struct FixedArgs {
   // device (round 6): the phased grid leaves them free
   uint32_t svc_cus = 0;
   // test hook (qfec_debug_phase_rtbatch): the runtime-k phased body's load
-  // batch (0: 32, the product; 16: round 5's)
+  // batch (0: the per-operation choice, phase_rt_batch; 16 or 32)
   uint32_t rt_batch = 0;
   // in-slot recover written in place (qfec_recover_inslot_batch with out ==
   // NULL; encode form, parity == nullptr): group g's output row is its own

@@ -356,6 +356,9 @@ template <int KC, bool RECOVER, bool MEET2 = false, bool FLAT = false, int kPhU 
 __global__ __launch_bounds__(NTHR) void phase_xor_kernel(FixedArgs a, uint32_t C, uint32_t gpb,
                                                            uint32_t nphase) {
   static_assert(!(INPL && RECOVER), "in place: the encode form over the k rows");
+  // (the runtime-k body loads the parity in place of the lost row: parity
+  // first with its received rows compact measured 2-6% slower for k = 17-48,
+  // profiles/round6/phase_k_table_r6c.txt against r6b)
   constexpr bool PF = RECOVER && PARFIRST && KC > 0;
   static_assert(!RECOVER || STEPS <= 64, "recover: bad-step masks are 64 bits");
   static_assert(RS == 0 || (KC > 0 && kPhU == 1 && !XCDW && RS <= 64 &&
@@ -1132,7 +1135,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // PF (recover): the parity windows are loaded into the accumulators before the
 // packet table, so their round trip overlaps the table's (measured equal to
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
-// DIAG (tools/tune only, not exact): 1 = no parity stores.
+// DIAG (tools/tune only, not exact): 1 = no parity stores; 2 = output rows
+// stored whole 128-B lines (zeros past the parity length up to the line end:
+// the zero-padded parity of SURVEY.md Appendix A, for output slots that have
+// the room -- the write-granularity probe of round 6).
 template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
 __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
@@ -1262,7 +1268,8 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
                                             lane, wv, s_w, tot);
   s_cnt[tid] = c;
   if (wv == 0u) {  // output windows per group (encode: the max lengths are final)
-    const uint32_t nw = lane < ng ? (s_pl[lane] + 15u) >> 4 : 0u;
+    uint32_t nw = lane < ng ? (s_pl[lane] + 15u) >> 4 : 0u;
+    if (DIAG == 2) nw = lane < ng ? ((s_pl[lane] + 127u) >> 7) << 3 : 0u;
     const uint32_t incl = wave_incl_scan(nw, lane);
     if (lane < (uint32_t)GPB) s_ob[lane] = incl - nw;
     if (lane == 0u) s_ob[GPB] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1329,6 +1336,11 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
     uint8_t* dst = a.out + s_doff[jq];
     const uint32_t* ac = acc + jq * kAccWords;
     if (DIAG == 1 && plen != 0xFFFFFu) continue;  // never a real length: no stores
+    if (DIAG == 2) {  // whole lines: the accumulator is zero past plen
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      st16t<true>(dst + 16u * t, t < (uint32_t)kParWin ? lds_get16<1>(ac, t) : z);
+      continue;
+    }
     if (16u * t + 16u <= plen) {
       st16t<true>(dst + 16u * t, lds_get16<1>(ac, t));
     } else {
@@ -1613,6 +1625,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 // decides; the followers leave on its word).  All control stores are vector
 // stores.
 constexpr int kSvcWaves = 8;
+// the leader's poll reads the next job's head with pub_end for this long after
+// its last job (100-MHz ticks: 50 us, half the idle time), then pub_end alone
+// 
+constexpr uint64_t kSvcQuietTicks = 5000;
 // Load slots per trip of a group's bytes.  A one-group job (all eight waves,
 // three slots each): 24 = every window of a group of up to 12 packets longer
 // than 1024 B in ONE PCIe round trip.  A job of several groups (a wave per
@@ -1830,8 +1846,17 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
             __hip_atomic_store(&sh->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
-          to = look();
+          if (wall_clock64() - t0 > kSvcQuietTicks) {
+            // a quiet stretch: pub_end alone, less often (one 8-B
+            // read instead of 1 KiB over the link every look); a job seen
+            // this way costs one more round trip for its head
+            __builtin_amdgcn_s_sleep(16);
+            to = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (to != from) to = look();
+          } else {
+            __builtin_amdgcn_s_sleep(2);
+            to = look();
+          }
         }
         // the head found whole (its hash, seq and start agree): the entry's
         // size is known -- a small job is all in LDS already, a larger one's
@@ -2109,6 +2134,16 @@ __host__ __device__ constexpr uint32_t phase_reg_steps(uint32_t k) {
   return (k >= 2u && k <= 16u) ? (uint32_t)kPhRegSteps : 0u;
 }
 
+// The runtime-k phased body's load batch (k > 16) by operation and group
+// size, from the round-6 per-k table (tools/phase_k_table.py, 2^20 groups up
+// to k = 32, 2^18 above; batch 16 / 32, fraction of 8 TB/s,
+// profiles/round6/phase_k_table_r6b.txt, r6c.txt): encode 16 at every k
+// (k = 20: 0.796 / 0.764, k = 255: 0.804 / 0.780); recover 32 up to k = 32
+// (k = 20: 0.679 / 0.720), 16 above (k = 64: 0.765 / 0.725).
+__host__ __device__ constexpr uint32_t phase_rt_batch(bool recover, uint32_t k) {
+  return recover && k <= 32u ? 32u : 16u;
+}
+
 template <bool RECOVER, bool INPL = false>
 hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t grid,
                           uint32_t nphase, hipStream_t s) {
@@ -2131,9 +2166,10 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
     QFEC_K_ALL(QFEC_K_CASE)
 #undef QFEC_K_CASE
     default:
-      // runtime k: batches of up to 32 loads (test hook rt_batch = 16: round
-      // 5's batches, the A/B of tools/phase_k_table.py)
-      if (a.rt_batch == 16u)
+      // runtime k: batches of up to 16 or 32 loads, by the measured table
+      // (phase_rt_batch; test hook rt_batch: either, the A/B of
+      // tools/phase_k_table.py)
+      if ((a.rt_batch ? a.rt_batch : phase_rt_batch(RECOVER, a.k)) == 16u)
         hipLaunchKernelGGL((phase_xor_kernel<0, RECOVER, false, false, kPhUDefault, kPhSteps, kBlock,
                                              false, true, true, false, true, 0, false, false, INPL,
                                              16>),

@@ -307,15 +307,18 @@ QuicFecBatcher::~QuicFecBatcher() {
 
 // The turn's first group warms the small-batch service (qfec_service_warm):
 // the worker is then resident by the turn's Launch instead of relaunched
-// there.  Best effort: a failure shows at Launch as before.
+// there.  Only after a turn whose batch the service took: a loop
+// that flushes hundreds of groups a turn never uses the worker, and a warm
+// one would hold 8 CUs and poll the host for its 100-us idle time for
+// nothing.  Best effort: a failure shows at Launch as before.
 void QuicFecBatcher::AddClosedGroup(Visitor* v, const QuicPacketHeader& fec_header,
                                     std::unique_ptr<QuicFecGroup> group) {
-  if (ctx_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
+  if (ctx_ && last_turn_small_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
   enc_.push_back(EncodeItem{v, fec_header, std::move(group)});
 }
 
 void QuicFecBatcher::AddRevivable(Visitor* v, std::unique_ptr<QuicFecGroup> group) {
-  if (ctx_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
+  if (ctx_ && last_turn_small_ && NumQueued() == 0) (void)qfec_service_warm(ctx_);
   rev_.push_back(ReviveItem{v, std::move(group)});
 }
 
@@ -340,6 +343,9 @@ int QuicFecBatcher::Launch() {
   const QuicFecGroup::LaunchProfile before = QuicFecGroup::launch_profile();
   enc_live_.swap(enc_);
   rev_live_.swap(rev_);
+  // (the service takes a mapped batch of up to 64 groups: qfec_capi.cpp kSvcGroups)
+  last_turn_small_ = (enc_live_.size() >= 1u && enc_live_.size() <= 64u) ||
+                     (rev_live_.size() >= 1u && rev_live_.size() <= 64u);
   std::vector<QuicFecGroup*>& gs = launch_groups_;  // keeps its capacity
   gs.clear();
   for (EncodeItem& e : enc_live_) gs.push_back(e.group.get());

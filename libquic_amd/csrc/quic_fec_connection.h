@@ -321,6 +321,9 @@ class QuicFecBatcher {
   std::vector<ReviveItem> rev_, rev_live_;
   QuicFecGroup::Pending enc_pending_, rev_pending_;
   std::vector<QuicFecGroup*> launch_groups_;  // Launch's group list
+  // the last Launch sent a batch the small-batch service takes (1..64 groups
+  // of one kind): only then does the next turn warm the worker
+  bool last_turn_small_ = true;
   Stats stats_;
 };
 

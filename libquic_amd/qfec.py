@@ -102,6 +102,7 @@ SIGNATURES = [
     ("qfec_debug_phase_min", C.c_int, [_vp, C.c_uint32]),
     ("qfec_debug_phase_regsteps", C.c_int, [_vp, C.c_int]),
     ("qfec_debug_phase_rtbatch", C.c_int, [_vp, C.c_uint32]),
+    ("qfec_debug_phase_reserve", C.c_int, [_vp, C.c_uint32]),
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_last_phase_grid", C.c_uint32, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
@@ -473,6 +474,10 @@ class Context:
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""
         return self._check(self.lib.qfec_debug_phase_regsteps(self.ctx, 1 if on else 0))
+
+    def debug_phase_reserve(self, cus):
+        """Test hook: phased grids leave `cus` more CUs out (the CU-arbitration A/B)."""
+        return self._check(self.lib.qfec_debug_phase_reserve(self.ctx, cus))
 
     def debug_phase_rtbatch(self, batch):
         """Test hook: the runtime-k phased body's load batch (16, 32; 0 = default 32)."""

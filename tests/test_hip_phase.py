@@ -104,7 +104,7 @@ def test_default_kernel_choice_by_group_size(ctx, k):
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
                                  (5, 17), (2, 16), (4, 1350), (8, 1001), (6, 1350), (12, 1350),
                                  (20, 1350), (17, 100), (40, 64), (64, 1350), (255, 1350),
-                                 (48, 300)])
+                                 (48, 300), (1, 300)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
@@ -152,10 +152,12 @@ def test_phased_strided(ctx):
                      ps=ps, os_=os_)
 
 
-def test_phased_invalid_missing(ctx):
+@pytest.mark.parametrize("k", [10, 20])
+def test_phased_invalid_missing(ctx, k):
     """A lost-slot index >= k latches QUIC_INVALID_FEC_DATA; that group's output
-    is untouched, every other group is revived (as in the one-pass kernel)."""
-    k, L = 10, 1350
+    is untouched, every other group is revived (as in the one-pass kernel).
+    k = 20: the runtime-k body."""
+    L = 1350
     n = 8 * phase_groups(L) + 1
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
     ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
@@ -163,7 +165,7 @@ def test_phased_invalid_missing(ctx):
     ctx.encode(rows, k, L, n, par)
     miss_np = Q.drop_index(Q.SEED_DROP, np.arange(n), k).astype(np.uint8)
     bad = np.array([0, 1, 2, 40 * 3, n // 2, n - 1])
-    miss_np[bad] = [10, 11, 255, 200, 10, 99]
+    miss_np[bad] = [k, k + 1, 255, 200, k, 99]
     miss = torch.from_numpy(miss_np).to(DEV)
     out = torch.full((n * L,), 0xEE, dtype=torch.uint8, device=DEV)
     ctx.recover(rows, par, miss, k, L, n, out)
@@ -371,10 +373,11 @@ def test_phased_register_steps_identical(ctx, k, L):
 
 @pytest.mark.parametrize("k,L", [(20, 1350), (64, 1350), (255, 200)])
 def test_runtime_k_load_batch_identical(ctx, k, L):
-    """Group sizes above 16 run the runtime-k phased body; round 6 loads up
-    to 32 rows per batch (round 5: 16; qfec_debug_phase_rtbatch selects it).
-    Both batches give the same bytes, the revived row is the lost row, and
-    sampled groups match the oracle."""
+    """Group sizes above 16 run the runtime-k phased body, in load batches of
+    16 or 32 rows (round 6: the library picks by operation and k,
+    phase_rt_batch; qfec_debug_phase_rtbatch forces either).  Both batches
+    give the same bytes, the revived row is the lost row, and sampled groups
+    match the oracle."""
     n = 8 * phase_groups(L) + 91
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)
     ctx.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)

@@ -9,11 +9,14 @@ GPU box; one JSON line per k, then a summary.
 
   python tools/phase_k_table.py [rounds=3] [reps=8] [k,k,...]
 
-The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers,
-and the library's default choice (no test hook) after them.  k > 16 has no
+The one-pass kernel (QFEC_ONE_PASS) is timed beside them on the same buffers;
+the library's default choice (no test hook) is run once to see which kernel it
+picks, and reported as that kernel's column (the same kernel on the same
+buffers: a second timing of it only adds noise), with its ratio to the best.  k > 16 has no
 register steps (runtime-k body): its two phased columns are the load batch of
-32 (round 6, the default) and of 16 (round 5's, qfec_debug_phase_rtbatch),
-over 2^18 groups above k = 32.
+32 ("register steps" column) and of 16 ("LDS steps only" column; both set
+through qfec_debug_phase_rtbatch), over 2^18 groups above k = 32; the
+default column is the library's per-operation choice (phase_rt_batch).
 """
 import json
 import os
@@ -57,19 +60,26 @@ def main():
             for m in (1, 0, 2, 3):  # 1: register steps, 0: LDS steps only, 2: one-pass,
                 # 3: the library's default choice (no hook)
                 # k > 16 (runtime-k body, no register steps): mode 0 is the
-                # round-5 load batch of 16 instead, mode 1 the default 32
+                # load batch of 16, mode 1 the batch of 32 (mode 3: the
+                # library's per-op choice, phase_rt_batch)
                 ctx.debug_phase_regsteps(m != 0 or k > 16)
-                ctx.debug_phase_rtbatch(16 if (m == 0 and k > 16) else 0)
+                ctx.debug_phase_rtbatch((16 if m == 0 else 32 if m == 1 else 0) if k > 16 else 0)
                 # phased forms at every k (the library's default picks one-pass
                 # below k = 5 / 8 since round 4, from this very table)
                 ctx.debug_phase_min(6 if m in (0, 1) else 0)
+                # modes 0 and 1 swap their two output buffers round by round
+                # (their A/B is not also an A/B of two DRAM placements)
+                bi = (m + r) % 2 if m in (0, 1) else m
                 for op in ("enc", "rec"):
                     def run():
                         if op == "enc":
-                            ctx.encode(rows, k, L, G, par[m], one_pass=(m == 2))
+                            ctx.encode(rows, k, L, G, par[bi], one_pass=(m == 2))
                         else:
-                            ctx.recover(rows, par[m], miss, k, L, G, out[m], one_pass=(m == 2))
+                            ctx.recover(rows, par[bi], miss, k, L, G, out[bi], one_pass=(m == 2))
                     run()  # warm
+                    phased[(m, op)] = ctx.last_fixed_phased()
+                    if m == 3:
+                        continue  # the default: which kernel it picks (timed as its column)
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
@@ -78,7 +88,6 @@ def main():
                     e1.record(stream)
                     e1.synchronize()
                     t[(m, op)].append(e0.elapsed_time(e1) / reps / 1e3)
-                    phased[(m, op)] = ctx.last_fixed_phased()
         ctx.debug_phase_regsteps(True)
         ctx.debug_phase_rtbatch(0)
         ctx.debug_phase_min(0)
@@ -90,25 +99,43 @@ def main():
         b = G * (k + 1) * L  # encode: k rows read + parity written; recover: k-1 + parity + out
         rec = {"k": k, "groups": G, "L": L, "identical": bool(same), "round_trip": bool(trip),
                "phased": {f"{m}{op}": phased[(m, op)] for (m, op) in phased}}
-        for m, tag in ((1, "regsteps"), (0, "lds_only"), (2, "one_pass"), (3, "default")):
+        for m, tag in ((1, "regsteps"), (0, "lds_only"), (2, "one_pass")):
             for op in ("enc", "rec"):
                 s = float(np.median(t[(m, op)]))
                 rec[f"{tag}_{op}_us"] = round(s * 1e6, 1)
                 rec[f"{tag}_{op}_frac"] = round(b / s / 1e9 / HBM, 4)
+        for op in ("enc", "rec"):
+            # the library's default IS one of the timed kernels on the same
+            # buffers: one-pass, or phased with register steps (k <= 16) /
+            # the load batch phase_rt_batch picks (k > 16: 16 -> column 0)
+            if phased[(3, op)] != 1:
+                col = 2
+            elif k <= 16:
+                col = 1
+            else:
+                col = 0 if (op == "enc" or k > 32) else 1
+            tag = {0: "lds_only", 1: "regsteps", 2: "one_pass"}[col]
+            rec[f"default_{op}_frac"] = rec[f"{tag}_{op}_frac"]
+            rec[f"default_{op}_is"] = tag
+            best = max(rec[f"regsteps_{op}_frac"], rec[f"lds_only_{op}_frac"],
+                       rec[f"one_pass_{op}_frac"])
+            rec[f"default_{op}_of_best"] = round(rec[f"default_{op}_frac"] / best, 4)
         print(json.dumps(rec), flush=True)
         out_rows.append(rec)
         del rows, par, out
         torch.cuda.empty_cache()
     print("\n| k | encode: register steps / LDS steps only / one-pass -> default (kernel) | "
-          "recover: register steps / LDS steps only / one-pass -> default (kernel) |")
-    print("|---|---|---|")
+          "recover: register steps / LDS steps only / one-pass -> default (kernel) | "
+          "default / best of the three, enc / rec |")
+    print("|---|---|---|---|")
     for r in out_rows:
         ke = "phased" if r["phased"]["3enc"] == 1 else "one-pass"
         kr = "phased" if r["phased"]["3rec"] == 1 else "one-pass"
         print(f"| {r['k']} | {r['regsteps_enc_frac']:.3f} / {r['lds_only_enc_frac']:.3f} / "
               f"{r['one_pass_enc_frac']:.3f} -> **{r['default_enc_frac']:.3f}** ({ke}) | "
               f"{r['regsteps_rec_frac']:.3f} / {r['lds_only_rec_frac']:.3f} / "
-              f"{r['one_pass_rec_frac']:.3f} -> **{r['default_rec_frac']:.3f}** ({kr}) |")
+              f"{r['one_pass_rec_frac']:.3f} -> **{r['default_rec_frac']:.3f}** ({kr}) | "
+              f"{r['default_enc_of_best']:.3f} / {r['default_rec_of_best']:.3f} |")
     ok = all(r["identical"] and r["round_trip"] for r in out_rows)
     print("all identical and round trips exact:", ok)
     return 0 if ok else 2

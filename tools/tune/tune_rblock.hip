@@ -4,9 +4,10 @@
 // parity lengths, revived rows) are compared byte for byte with the
 // product's before it is timed.
 //
-//   tune_rblock [reps=10] [rounds=5] [palign=16] [slot=1536]
+//   tune_rblock [reps=10] [rounds=5] [palign=16] [slot=1536] [diag=0]
 //     palign 16: payloads on 16-B boundaries (the payload arena's layout);
 //     palign 1: byte-packed.  slot: parity / revived row stride per group.
+//     diag 1: also the DIAG forms (whole-line stores; no stores).
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rblock.hip \
 //          -o tools/tune/build/tune_rblock
@@ -60,6 +61,14 @@ struct V {
   [=](const RaggedArgs& a) {                                                               \
     static_assert(!TL, "TL variant removed");                                              \
     hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, U, true, true, 0>),          \
+                       dim3((uint32_t)((a.n_groups + 7) / 8)), dim3(256), 0, 0, a);        \
+  }
+// round 6: DIAG 1 (no stores) and 2 (output rows stored as whole 128-B lines,
+// zeros past the parity length: compared against the product's rows with the
+// output buffers zeroed first, so the padding reads back as the product's)
+#define BLKD(REC, D)                                                                       \
+  [=](const RaggedArgs& a) {                                                               \
+    hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, D>),          \
                        dim3((uint32_t)((a.n_groups + 7) / 8)), dim3(256), 0, 0, a);        \
   }
 
@@ -116,8 +125,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&plen_v, G * 2));
   CK(hipMalloc(&err, 4));
   CK(hipMemset(err, 0, 4));
-  CK(hipMemset(par_ref, 0xA5, OB));
-  CK(hipMemset(out_ref, 0xA5, OB));
+  CK(hipMemset(par_ref, 0, OB));  // (zero: the DIAG 2 rows' padding compares equal)
+  CK(hipMemset(out_ref, 0, OB));
 
   RaggedArgs e{};
   e.bytes = data;
@@ -150,13 +159,20 @@ int main(int argc, char** argv) {
   vs.push_back({"product AL U2 encode (again)", false, BLK(false, 2, false)});
   vs.push_back({"product AL U2 recover", true, BLK(true, 2, false)});
   vs.push_back({"product AL U1 recover", true, BLK(true, 1, false)});
+  const bool diag = argc > 5 && atoi(argv[5]) != 0;
+  if (diag) {
+    vs.push_back({"whole-line stores encode", false, BLKD(false, 2)});
+    vs.push_back({"whole-line stores recover", true, BLKD(true, 2)});
+    vs.push_back({"no stores encode (inexact)", false, BLKD(false, 1)});
+    vs.push_back({"no stores recover (inexact)", true, BLKD(true, 1)});
+  }
 
   std::vector<uint8_t> h_ref(OB), h_v(OB);
   std::vector<uint16_t> hp_ref(G), hp_v(G);
   CK(hipMemcpy(hp_ref.data(), plen_ref, G * 2, hipMemcpyDeviceToHost));
   bool all_ok = true;
   for (const V& v : vs) {
-    CK(hipMemset(buf, 0xA5, OB));
+    CK(hipMemset(buf, 0, OB));
     CK(hipMemset(plen_v, 0, G * 2));
     CK(hipMemset(err, 0, 4));
     v.run(v.rec ? rv : ev);
@@ -171,7 +187,7 @@ int main(int argc, char** argv) {
       ok = ok && hp_ref == hp_v;
     }
     std::printf("check %-26s == product: %s (err %u)\n", v.name.c_str(), ok ? "yes" : "NO", e_h);
-    all_ok = all_ok && ok;
+    if (v.name.find("inexact") == std::string::npos) all_ok = all_ok && ok;
   }
   if (!all_ok) return 2;
 
