@@ -490,10 +490,13 @@ def bench_phase_beside_service(work, reps=6):
     c1.synchronize()
     spin = max(1 << 20, int((1 << 24) * 30.0 / max(c0.elapsed_time(c1), 1e-3)))
 
+    spins = []
+
     def encodes(grids):
         secs = []
         for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            es, e0, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            es.record(s)
             torch.cuda._sleep(spin)
             e0.record(s)
             ctx.encode(work.rows, k, L, G, work.par)
@@ -501,12 +504,14 @@ def bench_phase_beside_service(work, reps=6):
             grids.append(ctx.last_phase_grid())
             e1.synchronize()
             secs.append(e0.elapsed_time(e1) / 1e3)
+            spins.append(es.elapsed_time(e0))
         return float(np.mean(secs[1:])) if len(secs) > 1 else float(secs[0])
 
     alone = encodes([])  # the same launches without the other context
     th = threading.Thread(target=feeder)
     th.start()
     ready.wait(60)
+    w0 = time.perf_counter()
     before = ctx.phase_abandons()
     grids = []
     j0 = st["jobs"]
@@ -516,6 +521,7 @@ def bench_phase_beside_service(work, reps=6):
         stop.set()
         th.join(timeout=60)
     jobs = st["jobs"] - j0
+    wall = time.perf_counter() - w0
     work.synchronize()
     same = bool(torch.equal(work.par, want))
     del want
@@ -525,6 +531,8 @@ def bench_phase_beside_service(work, reps=6):
             "grids": grids, "ncu": torch.cuda.get_device_properties(work.dev.index).multi_processor_count,
             "abandoned": ctx.phase_abandons() - before,
             "service_jobs_meanwhile": jobs, "service_launches": st["launches"],
+            "service_us_per_job": round(wall / max(jobs, 1) * 1e6, 2),
+            "spin_ms": [round(x, 1) for x in spins],
             "service_wrong": st["bad"], "service_error": st["err"],
             "parity_equal_uncontended": same,
             "note": "context A's phased encode of the headline batch while a thread keeps context "
@@ -783,6 +791,7 @@ def main(argv=None):
         line["recover_inslot"] = bench_inslot(work, max(4, args.steps // 2 * 2),
                                               verify=not args.no_verify)
     if extras and not args.one_pass and phased and not args.no_beside_service:
+        _progress("phase beside service")
         work.step()  # the parity the contended encodes must reproduce
         line["phase_beside_service"] = bench_phase_beside_service(work)
         _progress("phase beside service done")

@@ -448,6 +448,10 @@ int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch);
  * as if other contexts' small-batch workers held them -- the A/B of the
  * round-6 CU arbitration; results are identical. */
 int qfec_debug_phase_reserve(qfec_ctx* ctx, uint32_t cus);
+/* Test hook: the CUs a phased launch on ctx would leave to other contexts'
+ * small-batch workers now; *why (nullable) gets why they count (bit 0 a job
+ * or warm in the last 2 ms, bit 1 a worker alive, bit 2 its stream busy). */
+uint32_t qfec_debug_other_service_cus(qfec_ctx* ctx, uint32_t* why);
 /* Test hook: fail != 0 makes every ragged call on this context fail with
  * QFEC_ERR_INTERNAL before touching the device (the GPU-failure path of the
  * connection integration: groups go without FEC). */
@@ -462,9 +466,12 @@ int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
  * setting; 2 enables it and writes the NEXT job's ring entry with a wrong job
  * number -- a malformed ring, whose job must fail with QFEC_ERR_INTERNAL and
  * turn the service off rather than report stale output); stats (may be NULL)
- * receives {worker launches, jobs finished, worker alive}.  Test /
- * measurement hook; the service is on by default.  Any failed service job
- * turns the service off for the context (small batches then launch). */
+ * receives {worker launches, jobs finished, worker alive}; on = 3 leaves the
+ * setting and fills stats[0..4] with those plus {worker stream busy, us since
+ * the context's last service job or warm} (the view the phased launches of
+ * other contexts take of it).  Test / measurement hook; the service is on by
+ * default.  Any failed service job turns the service off for the context
+ * (small batches then launch). */
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
 /* Measurement hook of the service: on = 1 / 0 makes the worker record
  * 100-MHz wall-clock stamps of each job it finishes (-1 leaves the
@@ -473,6 +480,13 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
  * done, outputs made visible, token stored.  (Worker launched by a later
  * job picks the setting up at its start.) */
 int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps);
+/* Measurement hook (round 6; stamps on through qfec_debug_service_stamps):
+ * the last service job end to end, 44 words: [0..5] the leader's stamps as
+ * above, [6] when the token was stored and [7] by which workgroup; [8 + 4w ..]
+ * workgroup w's share: entry in LDS, groups done, outputs visible, counted
+ * (100-MHz ticks); [40..43] the host's steady-clock ns of the last service
+ * call: entry, job published, token seen, return. */
+int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out);
 /* Test hook: hold != 0 keeps the service's follower workgroups waiting at
  * their start (as if dispatched late behind another kernel) until it is
  * cleared; the leader runs on.  A split job's token then waits for them. */

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <cstdarg>
 #include <cstdio>
@@ -149,6 +150,10 @@ struct qfec_ctx {
   uint32_t svc_seq = 0;
   uint64_t svc_launches = 0;
   bool svc_on = true;  // test hook qfec_debug_service
+  uint64_t svc_used_ns = 0;  // steady clock of the last service job / warm (other_service_cus)
+  // measurement hook (stamps on): the last service call's host stamps, steady
+  // ns: entry, published, token seen, return (qfec_debug_service_trace)
+  uint64_t svc_hst[4] = {0, 0, 0, 0};
   bool svc_poison_next = false;  // test hook: the next job's ring entry malformed
   // device scratch of the host-pointer xor / protection / entropy calls:
   // grow-only buffers kept for the context's life (no allocation per call)
@@ -284,24 +289,44 @@ constexpr uint64_t kSvcIdleTicks = 10000;
 // (round 5: 0.6-0.7x, abandoned).  The model is the reference's: one
 // connection thread per QuicConnection (quic_connection.h:14), here one
 // context per thread, several per process.
-// Every registered context with its service on counts, resident or not: a
-// worker that is relaunched by its connection thread while the phased grid is
-// being dispatched would otherwise take CUs the grid was sized for (measured
-// on the box: one launch in four abandoned when only resident workers were
-// counted).  Leaving 8 of 256 CUs idle costs the phased encode nothing
-// measurable (it is HBM-bound: bench leg `phase_beside_service`).
+// A context counts while its worker is resident or queued, AND for
+// kSvcRecentNs after its last service job or warm: a worker that its
+// connection thread relaunches while the phased grid is being dispatched
+// would otherwise take CUs the grid was sized for (measured on the box: one
+// launch in four abandoned when only resident workers were counted,
+// profiles/round6/pytest_service_r6a_registry_resident_only.log).  A context
+// whose service has been quiet that long is not counted: leaving 8 of 256 CUs
+// out costs the phased kernel 1.4% (encode 0.804 -> 0.793,
+// profiles/round6/phase_reserve_ab_r6d.txt).
+constexpr uint64_t kSvcRecentNs = 2000000;  // 2 ms: 20x the worker's idle time
 std::mutex g_svc_mu;
 std::vector<qfec_ctx*> g_svc_ctxs;
 
-uint32_t other_service_cus(const qfec_ctx* ctx) {
+uint64_t steady_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// why: bit 0 recent use, bit 1 alive, bit 2 stream busy (OR over the contexts
+// counted; the test hook qfec_debug_other_service_cus)
+uint32_t other_service_cus(const qfec_ctx* ctx, uint32_t* why = nullptr) {
+  const uint64_t now = steady_ns();
   std::lock_guard<std::mutex> lock(g_svc_mu);
-  uint32_t n = 0;
-  for (const qfec_ctx* c : g_svc_ctxs)
-    if (c != ctx && c->device == ctx->device && c->svc_sh &&
-        (__atomic_load_n(&c->svc_on, __ATOMIC_ACQUIRE) ||
-         __atomic_load_n(&c->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ||
-         hipStreamQuery(c->svc_stream) == hipErrorNotReady))
-      n += qfec::kSvcWgs;
+  uint32_t n = 0, w = 0;
+  for (const qfec_ctx* c : g_svc_ctxs) {
+    if (c == ctx || c->device != ctx->device || !c->svc_sh) continue;
+    const uint32_t r =
+        (__atomic_load_n(&c->svc_on, __ATOMIC_ACQUIRE) &&
+                 now - __atomic_load_n(&c->svc_used_ns, __ATOMIC_ACQUIRE) < kSvcRecentNs
+             ? 1u
+             : 0u) |
+        (__atomic_load_n(&c->svc_sh->alive, __ATOMIC_ACQUIRE) != 0u ? 2u : 0u) |
+        (hipStreamQuery(c->svc_stream) == hipErrorNotReady ? 4u : 0u);
+    if (r) n += qfec::kSvcWgs;
+    w |= r;
+  }
+  if (why) *why = w;
   return n;
 }
 
@@ -349,6 +374,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
                const SvcTabs& tb) {
   int rc = ensure_service(ctx);
   if (rc) return rc;
+  __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
   qfec::SvcShared* sh = ctx->svc_sh;
   const uint32_t seq = ctx->svc_seq++;
   qfec::SvcJob& j = ctx->svc_ring[seq % qfec::kSvcRing];
@@ -1523,6 +1549,8 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
                   const uint8_t* parity, uint8_t* parity_out, const uint64_t* parity_off,
                   const uint16_t* parity_len, uint16_t* parity_len_out, const uint8_t* missing,
                   uint8_t* out, const uint64_t* out_off, bool async) {
+  const bool hst = ctx->svc_sh && ctx->svc_sh->stamp_on;  // (measurement hook)
+  if (hst) ctx->svc_hst[0] = steady_ns();
   int rc = ensure_staging(ctx);
   if (rc) return rc;
   if ((rc = check_mapped(ctx, bytes, "bytes")) ||
@@ -1555,6 +1583,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     if (!c.live) return QFEC_OK;
     if (c.token) {
       const int wrc = c.svc ? wait_flag_svc(ctx, si, c.token) : wait_flag(ctx, si, c.token);
+      if (hst && c.svc) ctx->svc_hst[2] = steady_ns();
       if (wrc) {
         c.live = false;
         if (c.svc) svc_abandon(ctx);  // no later worker may run the failed job
@@ -1660,7 +1689,9 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
       // (no launch); a flag is all their completion needs
       const SvcTabs tb{(uint32_t)t.total, (uint32_t)t.off, (uint32_t)t.len, (uint32_t)t.ptr,
                        (uint32_t)t.poff, (uint32_t)t.plen, (uint32_t)t.miss, (uint32_t)t.ooff};
-      if (svc && svc_submit(ctx, slot, a, recover, token, tb) != QFEC_OK) {
+      const bool sub_fail = svc && svc_submit(ctx, slot, a, recover, token, tb) != QFEC_OK;
+      if (hst && svc) ctx->svc_hst[1] = steady_ns();
+      if (sub_fail) {
         // the service could not be set up or (re)launched: off for this
         // context, this batch launched as before (same flag and token), its
         // tables moved from the ring entry to the slot buffer the launch reads
@@ -1704,6 +1735,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   }
   for (int i = 0; i < kSlots; ++i)
     if ((rc = finish((slot + i) % kSlots))) return rc;
+  if (hst) ctx->svc_hst[3] = steady_ns();
   return direct ? QFEC_OK : collect_error(ctx, ctx->slots[0].stream, kErrHost);
 }
 
@@ -2081,6 +2113,7 @@ int qfec_service_warm(qfec_ctx* ctx) {
   if (rc) return rc;
   if (!ctx->svc_on) return QFEC_OK;
   if ((rc = ensure_staging(ctx)) || (rc = ensure_service(ctx))) return rc;
+  __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
   qfec::SvcShared* sh = ctx->svc_sh;
   if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) != 0u) return QFEC_OK;
   // nothing is published here, so a worker that is leaving needs no second
@@ -2106,7 +2139,7 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
     __atomic_store_n(&ctx->svc_on, true, __ATOMIC_RELEASE);
     ctx->svc_poison_next = true;
     if (ctx->svc_sh) __atomic_store_n(&ctx->svc_sh->quit, 0u, __ATOMIC_SEQ_CST);
-  } else if (on >= 0) {
+  } else if (on == 0 || on == 1) {
     __atomic_store_n(&ctx->svc_on, on != 0, __ATOMIC_RELEASE);
     if (!ctx->svc_on) {
       stop_service(ctx);  // a resident worker leaves at once
@@ -2118,6 +2151,11 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
     stats[0] = ctx->svc_launches;
     stats[1] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->jobs, __ATOMIC_ACQUIRE) : 0;
     stats[2] = ctx->svc_sh ? __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_ACQUIRE) : 0;
+  }
+  if (stats && on == 3) {  // (mode 3: the query plus the registry's view of this context)
+    stats[3] = ctx->svc_stream && hipStreamQuery(ctx->svc_stream) == hipErrorNotReady ? 1u : 0u;
+    const uint64_t used = __atomic_load_n(&ctx->svc_used_ns, __ATOMIC_ACQUIRE);
+    stats[4] = used ? (steady_ns() - used) / 1000u : ~0ull;  // us since its last job / warm
   }
   return QFEC_OK;
 }
@@ -2138,6 +2176,18 @@ int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps) {
   if (stamps)
     for (int q = 0; q < 6; ++q)
       stamps[q] = __atomic_load_n(&ctx->svc_sh->stamps[q], __ATOMIC_ACQUIRE);
+  return QFEC_OK;
+}
+
+int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return fail(ctx, QFEC_ERR_INTERNAL, "qfec_debug_service_trace: null argument");
+  int rc = ensure_service(ctx);
+  if (rc) return rc;
+  for (int q = 0; q < 8; ++q) out[q] = __atomic_load_n(&ctx->svc_sh->stamps[q], __ATOMIC_ACQUIRE);
+  for (uint32_t w = 0; w < qfec::kSvcWgs; ++w)
+    for (int q = 0; q < 4; ++q)
+      out[8 + 4 * w + q] = __atomic_load_n(&ctx->svc_sh->wg_stamps[w][q], __ATOMIC_ACQUIRE);
+  for (int q = 0; q < 4; ++q) out[8 + 4 * qfec::kSvcWgs + q] = ctx->svc_hst[q];
   return QFEC_OK;
 }
 
@@ -2180,6 +2230,11 @@ int qfec_debug_phase_rtbatch(qfec_ctx* ctx, uint32_t batch) {
     return fail(ctx, QFEC_ERR_INTERNAL, "qfec_debug_phase_rtbatch: batch 0, 16 or 32");
   ctx->rt_batch = batch;
   return QFEC_OK;
+}
+
+uint32_t qfec_debug_other_service_cus(qfec_ctx* ctx, uint32_t* why) {
+  if (!ctx) return 0;
+  return other_service_cus(ctx, why);
 }
 
 int qfec_debug_phase_reserve(qfec_ctx* ctx, uint32_t cus) {

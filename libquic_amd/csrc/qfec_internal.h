@@ -165,8 +165,13 @@ struct SvcShared {
                       // without finishing (no token for any job of that turn)
   // 100-MHz wall-clock stamps of the last job (qfec_debug_service_stamps):
   // [0] work seen, [1] entry in LDS, [2] wave 0's first group done, [3] every
-  // group done, [4] outputs visible (fence), [5] token stored
+  // group done, [4] outputs visible (fence), [5] the leader's count / token
+  // stored; [6] the token stored (by the last workgroup of a split job), [7]
+  // that workgroup (round 6, qfec_debug_service_trace)
   alignas(64) uint64_t stamps[8];
+  // round 6: every workgroup's stamps of its share of the last job: [0] its
+  // entry in LDS, [1] its groups done, [2] its outputs visible, [3] counted
+  uint64_t wg_stamps[8][4];
 };
 constexpr uint32_t kSvcRing = 8;
 // Round 5: the worker is kSvcWgs workgroups.  Workgroup 0 (the leader) polls
@@ -185,6 +190,8 @@ constexpr uint32_t kSvcRing = 8;
 // under it.  At most kSlots (3) jobs are outstanding, so kSvcRing
 // announcement words never wrap onto one not yet taken.
 constexpr uint32_t kSvcWgs = 8;
+static_assert(sizeof(SvcShared::wg_stamps) / sizeof(SvcShared::wg_stamps[0]) == kSvcWgs,
+              "one stamp row per service workgroup");
 struct SvcDev {
   uint32_t exit;             // leader: this launch's epoch when it leaves (after its
                              // last announcement)

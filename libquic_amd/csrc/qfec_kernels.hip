@@ -1135,10 +1135,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // PF (recover): the parity windows are loaded into the accumulators before the
 // packet table, so their round trip overlaps the table's (measured equal to
 // loading them after the scan, profiles/round3/ragged_block/block3.txt).
-// DIAG (tools/tune only, not exact): 1 = no parity stores; 2 = output rows
-// stored whole 128-B lines (zeros past the parity length up to the line end:
-// the zero-padded parity of SURVEY.md Appendix A, for output slots that have
-// the room -- the write-granularity probe of round 6).
+// DIAG (tools/tune only; bits): 1 = no parity stores (not exact); 2 = output
+// rows stored as whole 128-B lines (zeros past the parity length up to the
+// line end: the zero-padded parity of SURVEY.md Appendix A, for output slots
+// that have the room -- the write-granularity probe of round 6); 4 = no tail
+// logic (every window XORed whole, in place: the VALU probe of round 6, not
+// exact).
 template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
 __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
@@ -1269,7 +1271,7 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
   s_cnt[tid] = c;
   if (wv == 0u) {  // output windows per group (encode: the max lengths are final)
     uint32_t nw = lane < ng ? (s_pl[lane] + 15u) >> 4 : 0u;
-    if (DIAG == 2) nw = lane < ng ? ((s_pl[lane] + 127u) >> 7) << 3 : 0u;
+    if (DIAG & 2) nw = lane < ng ? ((s_pl[lane] + 127u) >> 7) << 3 : 0u;
     const uint32_t incl = wave_incl_scan(nw, lane);
     if (lane < (uint32_t)GPB) s_ob[lane] = incl - nw;
     if (lane == 0u) s_ob[GPB] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1304,7 +1306,7 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
       // bytes past the packet masked: an aligned 16-B load holding one packet
       // byte cannot leave that byte's page.  Otherwise the 16 bytes ending at
       // the packet end, shifted down.
-      inp[u] = full || (AL && win < ln && (at & 15u) == 0u);
+      inp[u] = full || (AL && win < ln && (at & 15u) == 0u) || (DIAG & 4);
       v[u] = ld16t<true>(a.bytes + (inp[u] ? at : at - win + ln - 16u));
       sh[u] = full ? 0u : min(win + 16u - ln, 15u);
       tt[u] = f < W ? (md[u].z >> 16) * kAccWords + (f - md[u].w) : 0xFFFFFFFFu;
@@ -1313,7 +1315,9 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
     for (int u = 0; u < U; ++u)
       if (tt[u] != 0xFFFFFFFFu) {
         u32x4 w;
-        if constexpr (AL) {
+        if constexpr ((DIAG & 4) != 0) {
+          w = v[u];
+        } else if constexpr (AL) {
           // in place: v & (ones >> sh); shifted: v >> sh (sh = 0 when full)
           const u32x4 ones = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
           const u32x4 m = shr_bytes_bf(inp[u] ? ones : v[u], sh[u]);
@@ -1335,8 +1339,8 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
     const uint32_t plen = s_pl[jq];
     uint8_t* dst = a.out + s_doff[jq];
     const uint32_t* ac = acc + jq * kAccWords;
-    if (DIAG == 1 && plen != 0xFFFFFu) continue;  // never a real length: no stores
-    if (DIAG == 2) {  // whole lines: the accumulator is zero past plen
+    if ((DIAG & 1) && plen != 0xFFFFFu) continue;  // never a real length: no stores
+    if (DIAG & 2) {  // whole lines: the accumulator is zero past plen
       const u32x4 z = {0u, 0u, 0u, 0u};
       st16t<true>(dst + 16u * t, t < (uint32_t)kParWin ? lds_get16<1>(ac, t) : z);
       continue;
@@ -1754,8 +1758,16 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
                            __HIP_MEMORY_SCOPE_SYSTEM);
       if (s_stamp) {
         st[5] = wall_clock64();
-        for (int q = 0; q < 6; ++q)
-          __hip_atomic_store(&sh->stamps[q], st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lead)
+          for (int q = 0; q < 6; ++q)
+            __hip_atomic_store(&sh->stamps[q], st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t row[4] = {st[1], st[3], st[4], st[5]};
+        for (int q = 0; q < 4; ++q)
+          __hip_atomic_store(&sh->wg_stamps[wg][q], row[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (last) {
+          __hip_atomic_store(&sh->stamps[6], st[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&sh->stamps[7], (uint64_t)wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
     }
   };
@@ -1788,7 +1800,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
       // test hook: a follower dispatched late (the hold released)
       while (svc_load32(&sh->hold) != 0u) __builtin_amdgcn_s_sleep(8);
       s_split = __hip_atomic_load(&dv->taken[wg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_stamp = 0u;
+      s_stamp = svc_load32(&sh->stamp_on);  // (its own row of wg_stamps)
     }
   }
   __syncthreads();
@@ -2222,7 +2234,10 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   // grid leaves them, so every workgroup is resident and the meetings hold
   // (round 6); more than a quarter of the device so held: one-pass
   if (a.svc_cus > a.ncu / 4u) return false;
-  const uint32_t wg = a.ncu - a.svc_cus + std::min<uint32_t>(a.phase_extra, 64u);
+  // (the test hook phase_extra: that many workgroups beyond one per CU, the
+  // other contexts' workers ignored)
+  const uint32_t wg =
+      a.phase_extra ? a.ncu + std::min<uint32_t>(a.phase_extra, 64u) : a.ncu - a.svc_cus;
   // the threshold counts phases of the LDS steps alone (the measured band);
   // the launch's phases hold the register steps too (k = 10)
   const uint64_t per = (uint64_t)wg * kPhSteps * gpb;

@@ -103,11 +103,13 @@ SIGNATURES = [
     ("qfec_debug_phase_regsteps", C.c_int, [_vp, C.c_int]),
     ("qfec_debug_phase_rtbatch", C.c_int, [_vp, C.c_uint32]),
     ("qfec_debug_phase_reserve", C.c_int, [_vp, C.c_uint32]),
+    ("qfec_debug_other_service_cus", C.c_uint32, [_vp, C.POINTER(C.c_uint32)]),
     ("qfec_last_fixed_phased", C.c_int, [_vp]),
     ("qfec_debug_last_phase_grid", C.c_uint32, [_vp]),
     ("qfec_debug_fail_launches", C.c_int, [_vp, C.c_int]),
     ("qfec_debug_service", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_stamps", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
+    ("qfec_debug_service_trace", C.c_int, [_vp, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_hold", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
@@ -455,16 +457,26 @@ class Context:
         """Small-batch service hook: on True / False enables / disables the
         resident worker (None leaves it); poison_next malforms the next job's
         ring entry (test of the ring-miss path); returns {launches, jobs, alive}."""
-        st = (C.c_uint64 * 3)()
-        mode = 2 if poison_next else (-1 if on is None else int(bool(on)))
+        st = (C.c_uint64 * 5)()
+        mode = 2 if poison_next else (3 if on is None else int(bool(on)))
         self._check(self.lib.qfec_debug_service(self.ctx, mode, st))
-        return {"launches": st[0], "jobs": st[1], "alive": st[2]}
+        d = {"launches": st[0], "jobs": st[1], "alive": st[2]}
+        if mode == 3:  # the registry's view: worker stream busy, us since last use
+            d["stream_busy"], d["idle_us"] = st[3], st[4]
+        return d
 
     def debug_service_stamps(self, on=None):
         """Measurement hook: the worker's wall-clock stamps (10-ns ticks) of
         the last job: seen, entry, first group, all groups, fence, token."""
         st = (C.c_uint64 * 6)()
         self._check(self.lib.qfec_debug_service_stamps(self.ctx, -1 if on is None else int(bool(on)), st))
+        return list(st)
+
+    def debug_service_trace(self):
+        """Measurement hook: the last service job end to end (44 words, see
+        qfec.h qfec_debug_service_trace)."""
+        st = (C.c_uint64 * 44)()
+        self._check(self.lib.qfec_debug_service_trace(self.ctx, st))
         return list(st)
 
     def debug_service_hold(self, hold):
@@ -474,6 +486,12 @@ class Context:
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""
         return self._check(self.lib.qfec_debug_phase_regsteps(self.ctx, 1 if on else 0))
+
+    def debug_other_service_cus(self):
+        """Test hook: (CUs a phased launch here leaves to other contexts' workers, why-bits)."""
+        why = C.c_uint32(0)
+        n = self.lib.qfec_debug_other_service_cus(self.ctx, C.byref(why))
+        return int(n), int(why.value)
 
     def debug_phase_reserve(self, cus):
         """Test hook: phased grids leave `cus` more CUs out (the CU-arbitration A/B)."""

@@ -453,6 +453,40 @@ def test_phased_launch_beside_a_continuously_fed_service():
     assert not errors, errors
 
 
+def test_quiet_service_context_leaves_the_phased_grid_whole():
+    """Round 6: another context counts against a phased grid only while its
+    worker runs or for 2 ms after its last job or warm (kSvcRecentNs); a
+    context whose service has been quiet longer costs the grid nothing
+    (8 CUs left out cost the phased encode 1.4%)."""
+    import torch
+    from oracle import qfec_np as Q
+    a, b = qfec.Context(0), qfec.Context(0)
+    try:
+        z, want_l = _mapped_case(2, g0=96000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=23)
+        _check(b, z, want_l)  # b registered, its worker resident
+        k, L = 10, 1350
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        n = 8 * ncu * 40 * (256 // ((L + 15) // 16)) + 5
+        rows = torch.empty(n * k * L, dtype=torch.uint8, device="cuda:0")
+        a.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+        par = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        b.service_warm()
+        a.encode(rows, k, L, n, par)
+        assert a.last_fixed_phased() == 1
+        assert a.last_phase_grid() == ncu - 8  # b's worker counted
+        a.sync()
+        time.sleep(0.01)  # past b's idle exit and the 2-ms window
+        st = b.debug_service()
+        assert st["alive"] == 0, st
+        assert a.debug_other_service_cus() == (0, 0), (str(st), a.debug_other_service_cus())
+        a.encode(rows, k, L, n, par)
+        assert a.last_phase_grid() == ncu, str(b.debug_service())
+        a.sync()
+    finally:
+        a.close()
+        b.close()
+
+
 def test_split_job_waits_for_late_followers():
     """a follower workgroup dispatched late (test hook: the
     followers held at their start) must still do its share of every split

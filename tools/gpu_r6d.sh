@@ -18,6 +18,8 @@ tail -13 "$OUT/phase_k_table.txt" &&
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --no-ragged --no-protect --no-entropy \
   --no-fused --no-e2e --no-cpu-baseline --no-ceilings > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 tools/tune/build/tune_rblock 10 4 16 1536 1 > "$OUT/tune_rblock_diag.txt" 2>&1
+tail -12 "$OUT/tune_rblock_diag.txt" &&
+timeout -k 10 120 tools/tune/build/tune_hostbw 200 > "$OUT/tune_hostbw.txt" 2>&1
 rc=$?
-tail -12 "$OUT/tune_rblock_diag.txt"
+cat "$OUT/tune_hostbw.txt"
 exit $rc

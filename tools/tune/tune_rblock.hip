@@ -63,9 +63,10 @@ struct V {
     hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, U, true, true, 0>),          \
                        dim3((uint32_t)((a.n_groups + 7) / 8)), dim3(256), 0, 0, a);        \
   }
-// round 6: DIAG 1 (no stores) and 2 (output rows stored as whole 128-B lines,
+// round 6: DIAG 1 (no stores), 2 (output rows stored as whole 128-B lines,
 // zeros past the parity length: compared against the product's rows with the
-// output buffers zeroed first, so the padding reads back as the product's)
+// output buffers zeroed first, so the padding reads back as the product's),
+// 4 (no tail logic: every window XORed whole), 5 (4 without stores)
 #define BLKD(REC, D)                                                                       \
   [=](const RaggedArgs& a) {                                                               \
     hipLaunchKernelGGL((qfec::ragged_block_kernel<REC, 4, 8, 2, true, true, D>),          \
@@ -165,6 +166,8 @@ int main(int argc, char** argv) {
     vs.push_back({"whole-line stores recover", true, BLKD(true, 2)});
     vs.push_back({"no stores encode (inexact)", false, BLKD(false, 1)});
     vs.push_back({"no stores recover (inexact)", true, BLKD(true, 1)});
+    vs.push_back({"no tail logic encode (inexact)", false, BLKD(false, 4)});
+    vs.push_back({"no tail, no stores enc (inexact)", false, BLKD(false, 5)});
   }
 
   std::vector<uint8_t> h_ref(OB), h_v(OB);
