@@ -119,6 +119,14 @@ extern "C" {
                                for that caller; without the flag the output is
                                untouched on failure, as NullDecrypter leaves it
                                (crypto/null_decrypter.cc:57-62). */
+#define QFEC_SMALL_GROUPS 64u /* ragged device calls (round 6): a hint that the
+                                * batch's groups carry few payload bytes each
+                                * (under ~4 KiB on average: short packets or
+                                * k <= 4), so a large batch runs two groups per
+                                * wave instead of eight per block (+8-14% there,
+                                * DESIGN.md §4 band table).  Host-pointer and
+                                * mapped batches choose by themselves (the host
+                                * holds their tables); results are identical. */
 
 /* qfec_complete() with wait == 0: the QFEC_ASYNC work is still running. */
 #define QFEC_PENDING 1

@@ -1530,7 +1530,9 @@ int ragged_host(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint64_
       a.parity_off = reinterpret_cast<const uint64_t*>(s.d_in + lay.poff);
       a.parity_len_out = reinterpret_cast<uint16_t*>(s.d_out + lay.out_plen);
     }
-    QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+    // (the chunk's shape is known here: groups of few bytes run two per wave)
+    QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream,
+                                      c.nbytes < qfec::kRaggedSmallGroupBytes * c.n));
     QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, lay.out_total, hipMemcpyDeviceToHost,
                                  s.stream));
     QFEC_HIP(ctx, hipEventRecord(s.done, s.stream));
@@ -1625,6 +1627,13 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
   // batches above kDirectGroups to the device and waited on an event.)
   const bool direct =
       n <= out_cap && Tab(grp_ptr[n] - grp_ptr[0], n, recover).total <= kStageBytes;
+  // a large chunk's shape (the host holds the tables): groups of few bytes
+  // run two per wave (launch_ragged small_groups)
+  auto small_groups = [&](uint64_t p0, uint64_t np, uint64_t cnt) {
+    uint64_t nb = 0;
+    for (uint64_t p = p0; p < p0 + np; ++p) nb += pkt_len[p];
+    return nb < qfec::kRaggedSmallGroupBytes * cnt;
+  };
   uint64_t g = 0;
   while (g < n) {
     const uint64_t g0 = g;
@@ -1703,10 +1712,10 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
         if (cnt <= kDirectGroups)
           QFEC_HIP(ctx, qfec::launch_ragged_latency(a, recover, s.stream));
         else
-          QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+          QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream, small_groups(p0, np, cnt)));
       }
     } else {
-      QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream));
+      QFEC_HIP(ctx, qfec::launch_ragged(a, recover, s.stream, small_groups(p0, np, cnt)));
     }
     if (!recover && !direct)
       QFEC_HIP(ctx, hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
@@ -1773,7 +1782,7 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
   a.out = parity_out;
   a.n_groups = n_groups;
   a.err = ctx->d_err;
-  QFEC_HIP(ctx, qfec::launch_ragged(a, false, ctx->stream));
+  QFEC_HIP(ctx, qfec::launch_ragged(a, false, ctx->stream, (flags & QFEC_SMALL_GROUPS) != 0));
   return QFEC_OK;
 }
 
@@ -1826,7 +1835,7 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
   a.out_off = out_off;
   a.n_groups = n_groups;
   a.err = ctx->d_err;
-  QFEC_HIP(ctx, qfec::launch_ragged(a, true, ctx->stream));
+  QFEC_HIP(ctx, qfec::launch_ragged(a, true, ctx->stream, (flags & QFEC_SMALL_GROUPS) != 0));
   return QFEC_OK;
 }
 

@@ -273,7 +273,14 @@ hipError_t launch_entropy_validate(const EntropyValidateArgs& a, hipStream_t s);
 
 // nontemporal: nt loads and stores (the streaming default; see qfec.h QFEC_CACHED)
 hipError_t launch_fixed(const FixedArgs& a, bool nontemporal, hipStream_t s);
-hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s);
+// small_groups: the batch's groups carry few bytes each (round 6's band
+// table: below kRaggedSmallGroupBytes on average): two groups per wave
+// (ragged_multi_kernel) instead of the block kernel.
+hipError_t launch_ragged(const RaggedArgs& a, bool recover, hipStream_t s, bool small_groups = false);
+// average payload bytes per group below which a large ragged batch runs two
+// groups per wave (launch_ragged small_groups; tools/tune/tune_rblock.hip
+// mode 2, profiles/round6/ragged_band_r6h.txt)
+constexpr uint64_t kRaggedSmallGroupBytes = 4096;
 // Small batches whose payloads are read over PCIe (mapped host memory): one
 // wave per group, all of a group's loads in flight at once.
 hipError_t launch_ragged_latency(const RaggedArgs& a, bool recover, hipStream_t s);

@@ -1386,6 +1386,252 @@ __global__ __launch_bounds__(64 * WAVES) void ragged_block_kernel(RaggedArgs a) 
 }
 
 
+// Two groups per wave (round 2's product kernel; since round 6 the kernel of
+// large batches whose groups are small -- launch_ragged's shape-aware choice,
+// below): GPW consecutive groups in
+// ONE flat window space — their received packets fill the 64-lane packet
+// table together — so the per-group load chain (group pointer -> packet table
+// -> packet bytes), which parks the one-group waves for 70% of their cycles
+// (SQ_WAIT_ANY, profiles/round1/sq_stalls_fec_pq.txt), and the partially idle
+// last iteration are paid once per GPW groups.  Groups that do not fit (more
+// than 64 received packets together, a packet below 16 B, any invalid field)
+// run the per-group body above with its exact error semantics.  Measured
+// +1.0-1.6% encode and recover over one group per wave in three interleaved
+// A/B runs (tune_multi_t2.txt, ragged_slots_p*.txt, tune_multi_sp.txt);
+// three groups per wave overflow the table too often (-10%).  tools/tune runs
+// it with GPW = 2.
+
+template <int N, typename T>
+__device__ __forceinline__ T sel_n(const T (&v)[N], uint32_t j) {
+  T r = v[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) r = j == (uint32_t)i ? v[i] : r;
+  return r;
+}
+
+// GPW groups g0 .. g0+ng-1 of one wave, up to their XOR into the LDS
+// accumulators `par` (GPW x kAccWords).  Returns false when the groups took
+// the per-group body (odd packets, invalid fields, > 64 received packets):
+// then their outputs are already stored; true: ragged_pair_store writes them
+// from `par` with lengths pl[] at offsets doff[].
+
+template <bool RECOVER, bool NT, int GPW, int U, bool BF, bool PBF = true>
+__device__ __forceinline__ bool ragged_pair_xor(const RaggedArgs& a, uint64_t g0, uint32_t ng,
+                                                uint32_t lane, uint32_t* par, uint64_t* head,
+                                                u32x4* meta, uint32_t (&pl)[GPW],
+                                                uint64_t (&doff)[GPW]) {
+  constexpr int ACC = 1;
+  // wave-uniform group scalars
+  uint32_t kb[GPW + 1], rb[GPW + 1], mm[GPW];
+  const uint32_t P0 = a.grp_ptr[g0];
+  bool ok = true;
+  kb[0] = rb[0] = 0;
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    uint32_t k = 0, m = 0xFFFFFFFFu, p = 0;
+    uint64_t d = 0;
+    if ((uint32_t)j < ng) {
+      k = a.grp_ptr[g0 + j + 1] - P0 - kb[j];
+      if constexpr (RECOVER) {
+        m = a.missing[g0 + j];
+        p = a.parity_len[g0 + j];
+        d = a.out_off[g0 + j];
+        ok = ok && m < k && p >= 16u && p <= kMaxPacket;
+      } else {
+        d = a.parity_off[g0 + j];
+      }
+      ok = ok && k >= 1u && k <= 255u;
+    }
+    kb[j + 1] = kb[j] + k;
+    rb[j + 1] = rb[j] + (RECOVER && k ? k - 1u : k);
+    mm[j] = m;
+    pl[j] = p;
+    doff[j] = d;
+  }
+  const uint32_t R = rb[GPW];
+  ok = ok && R <= 64u;
+
+  // lane r: received packet r of the wave's groups
+  uint32_t jl = 0, base = 0, kbase = 0, ml = 0xFFFFFFFFu, lim = kMaxPacket;
+#pragma unroll
+  for (int j = 1; j < GPW; ++j) {
+    const bool in = lane >= rb[j];
+    jl += in ? 1u : 0u;
+    base = in ? rb[j] : base;
+    kbase = in ? kb[j] : kbase;
+  }
+  ml = sel_n<GPW>(mm, jl);
+  if constexpr (RECOVER) lim = sel_n<GPW>(pl, jl);
+  uint32_t len = 0, offlo = 0, offhi = 0;
+  if (ok && lane < R) {
+    const uint32_t i = lane - base;
+    const uint32_t p = P0 + kbase + i + (RECOVER && i >= ml ? 1u : 0u);
+    len = a.pkt_len[p];
+    const uint64_t o = a.pkt_off[p];
+    offlo = (uint32_t)o;
+    offhi = (uint32_t)(o >> 32);
+  }
+  // accumulators: the parity rows (recover) or zero (encode)
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      uint32_t* acc = par + j * kAccWords;
+      if constexpr (RECOVER) {
+        const uint8_t* prow = a.parity + ((uint32_t)j < ng ? a.parity_off[g0 + j] : 0ull);
+        const uint32_t plj = (uint32_t)j < ng ? pl[j] : 0u;
+        // branch-free parity windows: every lane loads a window inside the
+        // row (lanes past plj re-read its last 16 bytes and keep zero), so
+        // neither load runs with lanes masked off.  plj >= 16 whenever the
+        // pair takes this path (ok); the branch is wave-uniform.
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        u32x4 w0 = zero, w1 = zero;
+        if (!PBF) {  // the round-2 form (A/B reference, tools/tune/ragged_exp.inc)
+          if (16u * lane < plj) w0 = packet_window<NT>(prow, plj, lane);
+          if (16u * (lane + 64u) < plj) w1 = packet_window<NT>(prow, plj, lane + 64u);
+        } else if (plj >= 16u) {
+          w0 = parity_window_bf<NT>(prow, plj, lane);
+          w1 = parity_window_bf<NT>(prow, plj, lane + 64u);
+        }
+        lds_put16<ACC>(acc, lane, w0);
+        if (lane + 64u < kParWin) lds_put16<ACC>(acc, lane + 64u, w1);
+      } else {
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        for (uint32_t t = lane; t < kParWin; t += 64u) lds_put16<ACC>(acc, t, zero);
+      }
+    }
+  }
+  const bool odd = lane < R && (len < 16u || len > lim);
+  if (!ok || wave_any(odd)) {
+    // per-group body (exact error semantics of the one-group kernel)
+    for (uint32_t j = 0; j < ng; ++j) {
+      GroupPrefetch f;
+      group_scalars<RECOVER>(a, g0 + j, f);
+      group_vectors<RECOVER, NT>(a, g0 + j, lane, f);
+      wave_lds_order();
+      ragged_group<RECOVER, NT, U, ACC, BF>(a, g0 + j, lane, f, par, head, meta);
+      wave_lds_order();
+    }
+    return false;
+  }
+  const uint32_t n = (len + 15u) >> 4;
+  const uint32_t incl = wave_incl_scan(n, lane);
+  const uint32_t S = incl - n;
+  const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t nit = (W + 63u) >> 6;  // W <= 64 x 91
+  for (uint32_t q = lane; q < nit; q += 64u) head[q] = 0ull;
+  wave_lds_order();
+  if (lane < R) {
+    meta[lane] = u32x4{offlo, offhi, len | (jl << 16), S};
+    __hip_atomic_fetch_or(&head[S >> 6], 1ull << (S & 63u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  wave_lds_order();  // accumulators, packet table and start mask complete
+  const uint64_t below = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+  const uint32_t last = R - 1u;
+  uint32_t before = 0;
+  for (uint32_t it = 0; it < nit; it += U) {
+    uint64_t M[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) M[u] = it + u < nit ? head[it + u] : 0ull;
+    u32x4 md[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t pi = min(before + (uint32_t)__popcll(M[u] & below) - 1u, last);
+      before += (uint32_t)__popcll(M[u]);
+      md[u] = meta[pi];
+    }
+    u32x4 v[U];
+    uint32_t tt[U], sh[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t fl = 64u * (it + u) + lane;
+      const uint32_t ln = md[u].z & 0xFFFFu;
+      const uint32_t win = 16u * (fl - md[u].w);
+      const bool full = win + 16u <= ln;
+      v[u] = ld16t<NT>(a.bytes + (((uint64_t)md[u].y << 32) | md[u].x) + (full ? win : ln - 16u));
+      sh[u] = full ? 0u : min(win + 16u - ln, 15u);
+      tt[u] = fl < W ? (md[u].z >> 16) * kAccWords + (fl - md[u].w) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (BF) {
+        // branch-free: a lane past W XORs ZERO into window `lane` of the first
+        // accumulator (a no-op, conflict-free), so no load or LDS atomic sits
+        // in an exec-masked block
+        uint32_t keep = tt[u] != 0xFFFFFFFFu ? 0xFFFFFFFFu : 0u;
+        __asm__ volatile("" : "+v"(keep));
+        lds_xor16<ACC>(par, tt[u] != 0xFFFFFFFFu ? tt[u] : lane, shr_bytes_bf(v[u], sh[u]) & keep);
+      } else if (tt[u] != 0xFFFFFFFFu) {
+        lds_xor16<ACC>(par, tt[u], shr_bytes_bf(v[u], sh[u]));
+      }
+    }
+  }
+  if constexpr (!RECOVER) {
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      pl[j] = wave_max11(lane < R && jl == (uint32_t)j ? len : 0u);
+      if (lane == 0 && (uint32_t)j < ng) a.parity_len_out[g0 + j] = (uint16_t)pl[j];
+    }
+  }
+  return true;
+}
+
+template <bool NT, int GPW>
+__device__ __forceinline__ void ragged_pair_store(const RaggedArgs& a, uint32_t ng, uint32_t lane,
+                                                  const uint32_t* par, const uint32_t (&pl)[GPW],
+                                                  const uint64_t (&doff)[GPW]) {
+  constexpr int ACC = 1;
+  wave_lds_order();  // every lane's XORs done
+  // write-out, flattened over the groups' output windows
+  uint32_t ob[GPW + 1];
+  ob[0] = 0;
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) ob[j + 1] = ob[j] + ((uint32_t)j < ng ? (pl[j] + 15u) >> 4 : 0u);
+  const uint32_t NW = ob[GPW];
+  for (uint32_t q = lane; q < NW; q += 64u) {
+    uint32_t jq = 0, qb = 0;
+#pragma unroll
+    for (int j = 1; j < GPW; ++j) {
+      const bool in = q >= ob[j];
+      jq += in ? 1u : 0u;
+      qb = in ? ob[j] : qb;
+    }
+    const uint32_t t = q - qb;
+    const uint32_t plen = sel_n<GPW>(pl, jq);
+    uint8_t* dst = a.out + sel_n<GPW>(doff, jq);
+    const uint32_t* acc = par + jq * kAccWords;
+    if (16u * t + 16u <= plen) {
+      st16t<NT>(dst + 16u * t, lds_get16<ACC>(acc, t));
+    } else {
+      const uint32_t o = plen - 16u * t;  // 1..15
+      const u32x4 lo = lds_get16<ACC>(acc, t - 1u), hi = lds_get16<ACC>(acc, t);
+      st16t<NT>(dst + plen - 16u, bytes16_at(lo, hi, o));
+    }
+  }
+}
+
+// (with done_flag set -- a direct mapped batch -- it signals completion like
+// the block kernel: every wave reaches ragged_signal_done)
+template <bool RECOVER, bool NT, int GPW, int U = 2, int WAVES = kFlatWaves, bool BF = false>
+__global__ __launch_bounds__(64 * WAVES) void ragged_multi_kernel(RaggedArgs a) {
+  __shared__ uint32_t s_par[WAVES][GPW * kAccWords];
+  __shared__ uint64_t s_head[WAVES][kParWin];
+  __shared__ u32x4 s_meta[WAVES][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * WAVES + wv) * GPW;
+  if (g0 < a.n_groups) {  // wave-uniform
+    const uint32_t ng = (uint32_t)min<uint64_t>((uint64_t)GPW, a.n_groups - g0);
+    uint32_t pl[GPW];
+    uint64_t doff[GPW];
+    if (ragged_pair_xor<RECOVER, NT, GPW, U, BF>(a, g0, ng, lane, s_par[wv], s_head[wv],
+                                                  s_meta[wv], pl, doff))
+      ragged_pair_store<NT, GPW>(a, ng, lane, s_par[wv], pl, doff);
+  }
+  ragged_signal_done(a);
+}
+
+
 // Ragged CSR, parity-window form — the SMALL-BATCH (latency) kernel: the
 // mapped host path runs a batch of <= kDirectGroups groups with it
 // (qfec_capi.cpp ragged_mapped), where the payloads are read over PCIe and a
@@ -2334,7 +2580,7 @@ hipError_t launch_fixed(const FixedArgs& a0, bool nontemporal, hipStream_t s) {
 
 constexpr int kRaggedBlockWaves = 4, kRaggedBlockGroups = 8;  // ragged_block_kernel shape
 
-hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
+hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s, bool small_groups) {
   if (a0.n_groups == 0) return hipSuccess;
   const uint64_t gpb = kRaggedBlockGroups;
   const uint64_t maxg = kMaxBlocks256 * gpb;
@@ -2352,12 +2598,22 @@ hipError_t launch_ragged(const RaggedArgs& a0, bool recover, hipStream_t s) {
       a.parity_len_out = a0.parity_len_out + g;
     }
     const uint64_t blocks = (a.n_groups + gpb - 1) / gpb;
-    if (recover)
+    // (two groups per wave x 4 waves: the block kernel's 8 groups per block)
+    static_assert(2 * kFlatWaves == kRaggedBlockGroups, "one grid for both kernels");
+    if (small_groups) {
+      if (recover)
+        hipLaunchKernelGGL((ragged_multi_kernel<true, true, 2>), dim3((uint32_t)blocks),
+                           dim3(kBlock), 0, s, a);
+      else
+        hipLaunchKernelGGL((ragged_multi_kernel<false, true, 2>), dim3((uint32_t)blocks),
+                           dim3(kBlock), 0, s, a);
+    } else if (recover) {
       hipLaunchKernelGGL((ragged_block_kernel<true, kRaggedBlockWaves, kRaggedBlockGroups>),
                          dim3((uint32_t)blocks), dim3(64 * kRaggedBlockWaves), 0, s, a);
-    else
+    } else {
       hipLaunchKernelGGL((ragged_block_kernel<false, kRaggedBlockWaves, kRaggedBlockGroups>),
                          dim3((uint32_t)blocks), dim3(64 * kRaggedBlockWaves), 0, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -28,6 +28,7 @@ QFEC_PTR_MAPPED = 4
 QFEC_ONE_PASS = 8
 QFEC_ASYNC = 16
 QFEC_SCRATCH_OUTPUT = 32
+QFEC_SMALL_GROUPS = 64
 QFEC_PENDING = 1
 MAX_PACKET_SIZE = 1452
 DEFAULT_MAX_PACKET_SIZE = 1350
@@ -328,21 +329,24 @@ class Context:
 
     # -- ragged ------------------------------------------------------------
     def encode_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity_out, parity_off,
-                      parity_len_out, *, host=False, mapped=False, async_=False):
+                      parity_len_out, *, host=False, mapped=False, async_=False,
+                      small_groups=False):
         rc = self.lib.qfec_encode_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                          _ptr(grp_ptr), n_groups, _ptr(parity_out),
                                          _ptr(parity_off), _ptr(parity_len_out),
-                                         _fl(host, mapped) | (QFEC_ASYNC if async_ else 0))
+                                         _fl(host, mapped) | (QFEC_ASYNC if async_ else 0)
+                                         | (QFEC_SMALL_GROUPS if small_groups else 0))
         return self._check(rc)
 
     def recover_ragged(self, data, pkt_off, pkt_len, grp_ptr, n_groups, parity, parity_off,
                        parity_len, missing, out, out_off, *, host=False, mapped=False,
-                       async_=False):
+                       async_=False, small_groups=False):
         rc = self.lib.qfec_recover_ragged(self.ctx, _ptr(data), _ptr(pkt_off), _ptr(pkt_len),
                                           _ptr(grp_ptr), n_groups, _ptr(parity),
                                           _ptr(parity_off), _ptr(parity_len), _ptr(missing),
                                           _ptr(out), _ptr(out_off),
-                                          _fl(host, mapped) | (QFEC_ASYNC if async_ else 0))
+                                          _fl(host, mapped) | (QFEC_ASYNC if async_ else 0)
+                                          | (QFEC_SMALL_GROUPS if small_groups else 0))
         return self._check(rc)
 
     def xor_into(self, src, n, dst, *, host=False, mapped=False):

@@ -31,9 +31,10 @@ def dview(a):
     return torch.from_numpy(a.view(_SIGNED[a.dtype]).copy()).to(DEV)
 
 
-def run_ragged(ctx, z, host=False):
+def run_ragged(ctx, z, host=False, small=False):
     """host: False = device pointers, True = QFEC_PTR_HOST (staged), "mapped" =
-    QFEC_PTR_MAPPED (payloads in qfec_host_alloc memory, read in place)."""
+    QFEC_PTR_MAPPED (payloads in qfec_host_alloc memory, read in place);
+    small: the QFEC_SMALL_GROUPS hint (device pointers: two groups per wave)."""
     n = z["grp_ptr"].size - 1
     psize = z["parity"].size
     if host == "mapped":
@@ -65,10 +66,10 @@ def run_ragged(ctx, z, host=False):
     par = torch.zeros(psize, dtype=torch.uint8, device=DEV)
     plen = torch.zeros(n, dtype=torch.int16, device=DEV)
     ctx.encode_ragged(data, d["pkt_off"], d["pkt_len"], d["grp_ptr"], n, par, d["parity_off"],
-                      plen)
+                      plen, small_groups=small)
     out = torch.zeros(z["recovered"].size, dtype=torch.uint8, device=DEV)
     ctx.recover_ragged(data, d["pkt_off"], d["pkt_len"], d["grp_ptr"], n, par, d["parity_off"],
-                       plen, d["missing"], out, d["out_off"])
+                       plen, d["missing"], out, d["out_off"], small_groups=small)
     ctx.sync()
     torch.cuda.synchronize()
     return par.cpu().numpy(), plen.cpu().numpy().view(np.uint16), out.cpu().numpy()
@@ -215,13 +216,16 @@ def test_cpp_quic_fec_group():
     assert " 0 failures" in r.stdout
 
 
-@pytest.mark.parametrize("host", [False, True, "mapped"])
-def test_ragged_pair_boundaries(ctx, host):
-    """The round-2 product (ragged_multi_kernel) ran two consecutive groups
-    per wave in one flat window space when their received packets fit the
-    64-lane table, all are >= 16 B and every field is valid; otherwise the
-    per-group body.  Its switch points, kept as a shape test of the block
-    kernel (these 17 groups are blocks of 8 with mixed fits and fallbacks).
+@pytest.mark.parametrize("host,small", [(False, False), (False, True), (True, False),
+                                        ("mapped", False)])
+def test_ragged_pair_boundaries(ctx, host, small):
+    """ragged_multi_kernel (round 2's product; since round 6 the kernel of
+    batches of small groups: QFEC_SMALL_GROUPS, small=True) runs two
+    consecutive groups per wave in one flat window space when their received
+    packets fit the 64-lane table, all are >= 16 B and every field is valid;
+    otherwise the per-group body.  Its switch points (for the block kernel,
+    small=False, a shape test: these 17 groups are blocks of 8 with mixed
+    fits and fallbacks).
     Pairs straddling each switch: 63 / 64 / 65 received packets (encode: k;
     recover: k - 1), a packet below 16 B in one group, a redundancy shorter
     than 16 B, k = 1 next to k = 255, and an odd group count (the last wave
@@ -255,7 +259,43 @@ def test_ragged_pair_boundaries(ctx, host):
     assert rc == 0 and rc2 == 0
     z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
              out_off=poff, parity=want_p, recovered=want_o)
-    par, plen, out = run_ragged(ctx, z, host=host)
+    par, plen, out = run_ragged(ctx, z, host=host, small=small)
+    assert np.array_equal(plen, want_l)
+    assert np.array_equal(par, want_p)
+    assert np.array_equal(out, want_o)
+
+
+@pytest.mark.parametrize("host,small", [(False, True), (False, False), (True, False),
+                                        ("mapped", False)])
+@pytest.mark.parametrize("shape", ["k2-4", "short"])
+def test_ragged_small_groups(ctx, host, small, shape):
+    """Round 6's shape-aware choice: a large batch whose groups carry few
+    bytes (k 2-4 of 16-1452 B, or k 5-15 of 16-400 B: under 4 KiB a group on
+    average) runs two groups per wave -- on device pointers with the
+    QFEC_SMALL_GROUPS hint, on host / mapped tables by the host's own count
+    (those batches here exceed the small-batch paths: 3,001 groups).  The
+    same batch without the hint runs the block kernel.  Bit-exact against the
+    oracle either way."""
+    rng = np.random.default_rng(31 if shape == "k2-4" else 32)
+    n = 3001
+    ks = rng.integers(2, 5, n) if shape == "k2-4" else rng.integers(5, 16, n)
+    hi = 1452 if shape == "k2-4" else 400
+    ln = rng.integers(16, hi + 1, int(ks.sum())).astype(np.uint16)
+    ptr = np.zeros(n + 1, np.uint32)
+    ptr[1:] = np.cumsum(ks)
+    assert ln.astype(np.int64).sum() < 4096 * n  # the small-group side of the rule
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(((ln[:-1].astype(np.uint64) + 15) // 16) * 16)
+    data = rng.integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    poff = np.arange(n, dtype=np.uint64) * np.uint64(1456)
+    miss = (rng.integers(0, 1 << 30, n) % ks).astype(np.uint8)
+    rc, want_p, want_l = OC.encode_ragged(data, off, ln, ptr, poff, n * 1456)
+    rc2, want_o = OC.recover_ragged(data, off, ln, ptr, want_p, poff, want_l, miss, poff,
+                                    n * 1456)
+    assert rc == 0 and rc2 == 0
+    z = dict(data=data, pkt_off=off, pkt_len=ln, grp_ptr=ptr, parity_off=poff, missing=miss,
+             out_off=poff, parity=want_p, recovered=want_o)
+    par, plen, out = run_ragged(ctx, z, host=host, small=small)
     assert np.array_equal(plen, want_l)
     assert np.array_equal(par, want_p)
     assert np.array_equal(out, want_o)

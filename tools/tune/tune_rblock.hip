@@ -4,10 +4,12 @@
 // parity lengths, revived rows) are compared byte for byte with the
 // product's before it is timed.
 //
-//   tune_rblock [reps=10] [rounds=5] [palign=16] [slot=1536] [diag=0]
+//   tune_rblock [reps=10] [rounds=5] [palign=16] [slot=1536] [mode=0] [kmin kmax lmin lmax]
 //     palign 16: payloads on 16-B boundaries (the payload arena's layout);
 //     palign 1: byte-packed.  slot: parity / revived row stride per group.
-//     diag 1: also the DIAG forms (whole-line stores; no stores).
+//     mode 1: also the DIAG forms (whole-line stores; no stores; no tail);
+//     mode 2: the block kernel against ragged_multi_kernel (two groups per
+//     wave) on the given group shape (round 6's band table).
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rblock.hip \
 //          -o tools/tune/build/tune_rblock
@@ -87,13 +89,18 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> miss(G);
   uint64_t bytes = 0;
   double enc_alg = 0, rec_alg = 0;
+  // round 6: the group shape (default configs[3]: k 5-15, 64-1350 B)
+  const uint32_t kmin = argc > 6 ? (uint32_t)atoi(argv[6]) : 5u;
+  const uint32_t kmax = argc > 7 ? (uint32_t)atoi(argv[7]) : 15u;
+  const uint32_t lmin = argc > 8 ? (uint32_t)atoi(argv[8]) : 64u;
+  const uint32_t lmax = argc > 9 ? (uint32_t)atoi(argv[9]) : 1350u;
   for (uint64_t g = 0; g < G; ++g) {
-    const uint32_t k = 5 + (uint32_t)(sm64(seed ^ (0x6Bull << 56) ^ g) % 11);
+    const uint32_t k = kmin + (uint32_t)(sm64(seed ^ (0x6Bull << 56) ^ g) % (kmax - kmin + 1u));
     miss[g] = (uint8_t)(sm64(seed ^ (0x4Dull << 56) ^ g) % k);
     uint32_t mx = 0;
     double s = 0, sm = 0;
     for (uint32_t i = 0; i < k; ++i) {
-      const uint32_t ln = 64 + (uint32_t)(sm64(seed ^ (0x4Cull << 56) ^ (g * 256 + i)) % 1287);
+      const uint32_t ln = lmin + (uint32_t)(sm64(seed ^ (0x4Cull << 56) ^ (g * 256 + i)) % (lmax - lmin + 1u));
       len.push_back((uint16_t)ln);
       off.push_back(bytes);
       bytes += (ln + palign - 1) / palign * palign;
@@ -155,12 +162,24 @@ int main(int argc, char** argv) {
   rv.out = buf;
 
   std::vector<V> vs;
+  const int mode = argc > 5 ? atoi(argv[5]) : 0;
+  if (mode == 2) {  // round 6 band table: the block kernel against two groups per wave
+#define MULTI(REC)                                                                          \
+  [=](const RaggedArgs& a) {                                                                \
+    hipLaunchKernelGGL((qfec::ragged_multi_kernel<REC, true, 2, 2, 4>),                     \
+                       dim3((uint32_t)((a.n_groups + 7) / 8)), dim3(256), 0, 0, a);         \
+  }
+    vs.push_back({"block encode", false, BLK(false, 2, false)});
+    vs.push_back({"multi2 encode", false, MULTI(false)});
+    vs.push_back({"block recover", true, BLK(true, 2, false)});
+    vs.push_back({"multi2 recover", true, MULTI(true)});
+  } else {
   vs.push_back({"product AL U2 encode", false, BLK(false, 2, false)});
   vs.push_back({"product AL U1 encode", false, BLK(false, 1, false)});
   vs.push_back({"product AL U2 encode (again)", false, BLK(false, 2, false)});
   vs.push_back({"product AL U2 recover", true, BLK(true, 2, false)});
   vs.push_back({"product AL U1 recover", true, BLK(true, 1, false)});
-  const bool diag = argc > 5 && atoi(argv[5]) != 0;
+  const bool diag = mode == 1;
   if (diag) {
     vs.push_back({"whole-line stores encode", false, BLKD(false, 2)});
     vs.push_back({"whole-line stores recover", true, BLKD(true, 2)});
@@ -168,6 +187,7 @@ int main(int argc, char** argv) {
     vs.push_back({"no stores recover (inexact)", true, BLKD(true, 1)});
     vs.push_back({"no tail logic encode (inexact)", false, BLKD(false, 4)});
     vs.push_back({"no tail, no stores enc (inexact)", false, BLKD(false, 5)});
+  }
   }
 
   std::vector<uint8_t> h_ref(OB), h_v(OB);
@@ -211,10 +231,10 @@ int main(int argc, char** argv) {
       ms[i].push_back(m / reps);
     }
   }
-  std::printf("\nconfigs[3]: %llu groups, k 5-15, len 64-1350, palign %llu, slot %llu; "
+  std::printf("\n%llu groups, k %u-%u, len %u-%u (%.0f B per group), palign %llu, slot %llu; "
               "algorithmic GB: encode %.3f, recover %.3f\n",
-              (unsigned long long)G, (unsigned long long)palign, (unsigned long long)slot,
-              enc_alg / 1e9, rec_alg / 1e9);
+              (unsigned long long)G, kmin, kmax, lmin, lmax, enc_alg / (double)G,
+              (unsigned long long)palign, (unsigned long long)slot, enc_alg / 1e9, rec_alg / 1e9);
   for (size_t i = 0; i < vs.size(); ++i) {
     std::vector<float> s = ms[i];
     std::sort(s.begin(), s.end());
