@@ -436,60 +436,26 @@ def bench_phase_beside_service(work, reps=6):
     """the headline encode (phased) on context A while a
     connection thread keeps context B's small-batch worker resident (the
     reference's model, one thread per QuicConnection, quic_connection.h:14):
-    B warms its worker and flushes one-group mapped batches back to back.  A's
+    a native thread owning B (qfec_debug_service_feed) warms its worker at
+    each turn's start and flushes one-group mapped batches back to back.  A's
     phased grid leaves B's 8 CUs out (qfec_capi.cpp other_service_cus), so no
     launch abandons its meetings.  Reported: A's encode frac (HIP events on
-    A's stream), its grid, abandoned launches, B's jobs meanwhile and whether
-    A's parity equals the uncontended steps' parity."""
-    import threading
+    A's stream), the same launches without B, A's grids, abandoned launches,
+    B's batches meanwhile and whether A's parity equals the uncontended
+    steps' parity."""
     from libquic_amd import qfec
     torch, ctx, s = work.torch, work.ctx, work.stream
     k, L, G = work.k, work.L, work.G
     want = work.par.clone()
-    stop, ready = threading.Event(), threading.Event()
-    st = {"jobs": 0, "bad": 0, "err": None, "launches": None}
-
-    def feeder():
-        try:
-            b = qfec.Context(work.dev.index)
-            data, par = qfec.HostBuffer(10 * 1350), qfec.HostBuffer(1350)
-            try:
-                rng = np.random.default_rng(5)
-                data.array[:] = rng.integers(0, 256, 10 * 1350, dtype=np.uint8)
-                off = np.arange(10, dtype=np.uint64) * np.uint64(1350)
-                ln = np.full(10, 1350, np.uint16)
-                ptr = np.array([0, 10], np.uint32)
-                poff = np.zeros(1, np.uint64)
-                plen = np.zeros(1, np.uint16)
-                exp = np.bitwise_xor.reduce(data.array.reshape(10, 1350), axis=0)
-                while not stop.is_set():
-                    b.service_warm()  # the loop turn's start
-                    b.encode_ragged(data.array, off, ln, ptr, 1, par.array, poff, plen,
-                                    mapped=True)
-                    st["jobs"] += 1
-                    st["bad"] += int(not np.array_equal(par.array, exp))
-                    if st["jobs"] == 20:
-                        ready.set()
-                st["launches"] = b.debug_service()["launches"]
-            finally:
-                data.close()
-                par.close()
-                b.close()
-        except Exception as e:  # reported on the line
-            st["err"] = repr(e)
-            ready.set()
-
-    # Each timed launch is queued behind a ~30 ms spin kernel on its stream, so
-    # the events bracket the kernel alone: the feeder thread holds the GIL
-    # between its calls, and an event recorded before a launch the main
-    # thread is still waiting to issue would time that wait too.
+    # each timed launch is queued behind a ~10 ms spin kernel on its stream,
+    # so the events bracket the kernel alone, whatever the host thread does
+    # between enqueueing the first event and the launch
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     c0.record(s)
     torch.cuda._sleep(1 << 24)
     c1.record(s)
     c1.synchronize()
-    spin = max(1 << 20, int((1 << 24) * 30.0 / max(c0.elapsed_time(c1), 1e-3)))
-
+    spin = max(1 << 20, int((1 << 24) * 10.0 / max(c0.elapsed_time(c1), 1e-3)))
     spins = []
 
     def encodes(grids):
@@ -508,36 +474,38 @@ def bench_phase_beside_service(work, reps=6):
         return float(np.mean(secs[1:])) if len(secs) > 1 else float(secs[0])
 
     alone = encodes([])  # the same launches without the other context
-    th = threading.Thread(target=feeder)
-    th.start()
-    ready.wait(60)
-    w0 = time.perf_counter()
-    before = ctx.phase_abandons()
-    grids = []
-    j0 = st["jobs"]
+    b = qfec.Context(work.dev.index)
     try:
-        enc = encodes(grids)
+        b.debug_service_feed(True)
+        time.sleep(0.02)  # its worker resident and busy
+        before = ctx.phase_abandons()
+        grids = []
+        w0 = time.perf_counter()
+        try:
+            enc = encodes(grids)
+        finally:
+            fed = b.debug_service_feed(False)
+        wall = time.perf_counter() - w0
+        launches = b.debug_service()["launches"]
     finally:
-        stop.set()
-        th.join(timeout=60)
-    jobs = st["jobs"] - j0
-    wall = time.perf_counter() - w0
+        b.close()
     work.synchronize()
     same = bool(torch.equal(work.par, want))
     del want
     return {"encode_frac": round(work.bytes_encode / enc / 1e9 / HBM_PEAK_GBS, 4),
             "encode_us": round(enc * 1e6, 2),
             "alone_encode_frac": round(work.bytes_encode / alone / 1e9 / HBM_PEAK_GBS, 4),
-            "grids": grids, "ncu": torch.cuda.get_device_properties(work.dev.index).multi_processor_count,
+            "grids": grids,
+            "ncu": torch.cuda.get_device_properties(work.dev.index).multi_processor_count,
             "abandoned": ctx.phase_abandons() - before,
-            "service_jobs_meanwhile": jobs, "service_launches": st["launches"],
-            "service_us_per_job": round(wall / max(jobs, 1) * 1e6, 2),
+            "service_jobs_meanwhile": fed["jobs"], "service_wrong": fed["wrong"],
+            "service_launches": launches,
+            "service_us_per_job": round(wall / max(fed["jobs"], 1) * 1e6, 2),
             "spin_ms": [round(x, 1) for x in spins],
-            "service_wrong": st["bad"], "service_error": st["err"],
             "parity_equal_uncontended": same,
-            "note": "context A's phased encode of the headline batch while a thread keeps context "
-                    "B's small-batch worker resident (qfec_service_warm + one-group mapped flushes "
-                    "back to back); mean of the last reps-1 launches"}
+            "note": "context A's phased encode of the headline batch while a native thread owning "
+                    "context B warms its small-batch worker and flushes one-group mapped batches "
+                    "back to back (qfec_debug_service_feed); mean of the last reps-1 launches"}
 
 
 def measured_traffic(G, k, L, phased=False):

@@ -495,6 +495,12 @@ int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps);
  * (100-MHz ticks); [40..43] the host's steady-clock ns of the last service
  * call: entry, job published, token seen, return. */
 int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out);
+/* Measurement hook (round 6): on = 1 starts a native thread that owns ctx
+ * (the caller must not use ctx until it is stopped) and flushes one-group
+ * mapped batches of 10 x 1350 B back to back, warming the small-batch worker
+ * at each turn's start; on = 0 stops it and returns its code, with stats
+ * (nullable) = {batches flushed, batches whose parity was wrong}. */
+int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats);
 /* Test hook: hold != 0 keeps the service's follower workgroups waiting at
  * their start (as if dispatched late behind another kernel) until it is
  * cleared; the leader runs on.  A split job's token then waits for them. */

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -2198,6 +2199,86 @@ int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out) {
       out[8 + 4 * w + q] = __atomic_load_n(&ctx->svc_sh->wg_stamps[w][q], __ATOMIC_ACQUIRE);
   for (int q = 0; q < 4; ++q) out[8 + 4 * qfec::kSvcWgs + q] = ctx->svc_hst[q];
   return QFEC_OK;
+}
+
+// Measurement hook (round 6, bench leg phase_beside_service): a native
+// connection thread that owns ctx until stopped and flushes one-group mapped
+// batches back to back, warming the worker at each turn's start -- what an
+// event loop with one connection per turn does.  A Python feeder thread
+// starved the measuring thread of the GIL for seconds at a time.
+namespace {
+struct Feeder {
+  std::thread th;
+  std::atomic<bool> stop{false};
+  std::atomic<uint64_t> jobs{0}, wrong{0};
+  std::atomic<int> rc{QFEC_OK};
+};
+std::mutex g_feed_mu;
+std::vector<std::pair<qfec_ctx*, Feeder*>> g_feeders;
+}  // namespace
+
+int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats) {
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
+  std::lock_guard<std::mutex> lock(g_feed_mu);
+  auto it = std::find_if(g_feeders.begin(), g_feeders.end(),
+                         [ctx](const std::pair<qfec_ctx*, Feeder*>& f) { return f.first == ctx; });
+  if (on) {
+    if (it != g_feeders.end()) return fail(ctx, QFEC_ERR_INTERNAL, "feeder already running");
+    Feeder* f = new Feeder();
+    f->th = std::thread([ctx, f] {
+      constexpr uint32_t k = 10, L = 1350;
+      uint8_t* data = static_cast<uint8_t*>(qfec_host_alloc(k * L));
+      uint8_t* par = static_cast<uint8_t*>(qfec_host_alloc(L));
+      if (!data || !par) {
+        f->rc = QFEC_ERR_INTERNAL;
+        qfec_host_free(data);
+        qfec_host_free(par);
+        return;
+      }
+      uint8_t want[L];
+      std::memset(want, 0, L);
+      for (uint32_t i = 0; i < k * L; ++i) {
+        data[i] = (uint8_t)(i * 131u + 7u);
+        want[i % L] ^= data[i];
+      }
+      uint64_t off[k];
+      uint16_t len[k];
+      for (uint32_t i = 0; i < k; ++i) {
+        off[i] = (uint64_t)i * L;
+        len[i] = (uint16_t)L;
+      }
+      const uint32_t ptr[2] = {0u, k};
+      const uint64_t poff = 0;
+      uint16_t plen = 0;
+      while (!f->stop.load(std::memory_order_relaxed)) {
+        (void)qfec_service_warm(ctx);  // the turn's start
+        const int r = qfec_encode_ragged(ctx, data, off, len, ptr, 1, par, &poff, &plen,
+                                         QFEC_PTR_MAPPED);
+        if (r != QFEC_OK) {
+          f->rc = r;
+          break;
+        }
+        if (plen != L || std::memcmp(par, want, L) != 0) f->wrong.fetch_add(1);
+        f->jobs.fetch_add(1, std::memory_order_relaxed);
+      }
+      qfec_host_free(data);
+      qfec_host_free(par);
+    });
+    g_feeders.emplace_back(ctx, f);
+    return QFEC_OK;
+  }
+  if (it == g_feeders.end()) return fail(ctx, QFEC_ERR_INTERNAL, "no feeder running");
+  Feeder* f = it->second;
+  g_feeders.erase(it);
+  f->stop = true;
+  f->th.join();
+  if (stats) {
+    stats[0] = f->jobs.load();
+    stats[1] = f->wrong.load();
+  }
+  const int rc = f->rc.load();
+  delete f;
+  return rc;
 }
 
 int qfec_debug_fail_launches(qfec_ctx* ctx, int on) {

@@ -2388,8 +2388,14 @@ hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t
 // templated k takes kPhRegSteps (round 4; round 3 had
 // them for k = 10 only; round 5 templates every k up to 16).  Larger k run
 // the runtime-k body with the LDS steps alone.
+// Round 6: group sizes above 16 templated for the phased kernel alone (the
+// one-pass kernel keeps its runtime-k body there).
+#define QFEC_K_PHASE_WIDE(X) X(20)
+__host__ __device__ constexpr bool phase_k_templated(uint32_t k) {
+  return (k >= 2u && k <= 16u) || k == 20u;
+}
 __host__ __device__ constexpr uint32_t phase_reg_steps(uint32_t k) {
-  return (k >= 2u && k <= 16u) ? (uint32_t)kPhRegSteps : 0u;
+  return phase_k_templated(k) ? (uint32_t)kPhRegSteps : 0u;
 }
 
 // The runtime-k phased body's load batch (k > 16) by operation and group
@@ -2406,7 +2412,8 @@ template <bool RECOVER, bool INPL = false>
 hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t grid,
                           uint32_t nphase, hipStream_t s) {
   const bool rs = a.no_regsteps == 0u;
-  switch (a.k) {
+  // (test hook rt_batch: the runtime-k body even where k is templated)
+  switch (a.rt_batch != 0u && a.k > 16u ? 0u : a.k) {
     // templated k: kPhRegSteps more steps per phase held in registers after
     // the LDS steps (recover: their parity rows first, RPF), or without them
     // (test hook; not for the in-place form)
@@ -2422,6 +2429,7 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
                          gpb, nphase);                                                          \
     break;
     QFEC_K_ALL(QFEC_K_CASE)
+    QFEC_K_PHASE_WIDE(QFEC_K_CASE)
 #undef QFEC_K_CASE
     default:
       // runtime k: batches of up to 16 or 32 loads, by the measured table
@@ -2491,7 +2499,10 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
   if (np < (a.phase_min ? a.phase_min : kPhMinPhases) || np > 0xFFFFFFFFull) return false;
   const uint64_t per_l =
       (uint64_t)wg *
-      (kPhSteps + (a.no_regsteps && !a.inplace_missing ? 0u : phase_reg_steps(a.k))) * gpb;
+      (kPhSteps + ((a.no_regsteps && !a.inplace_missing) || (a.rt_batch != 0u && a.k > 16u)
+                       ? 0u
+                       : phase_reg_steps(a.k))) *
+      gpb;
   *grid = wg;
   *nphase = (uint32_t)((a.n_groups + per_l - 1) / per_l);
   return true;

@@ -111,6 +111,7 @@ SIGNATURES = [
     ("qfec_debug_service", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_stamps", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_trace", C.c_int, [_vp, C.POINTER(C.c_uint64)]),
+    ("qfec_debug_service_feed", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_hold", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
@@ -482,6 +483,14 @@ class Context:
         st = (C.c_uint64 * 44)()
         self._check(self.lib.qfec_debug_service_trace(self.ctx, st))
         return list(st)
+
+    def debug_service_feed(self, on):
+        """Measurement hook: a native thread owning this context flushes
+        one-group mapped batches back to back (on=True); on=False stops it and
+        returns {jobs, wrong}."""
+        st = (C.c_uint64 * 2)()
+        self._check(self.lib.qfec_debug_service_feed(self.ctx, 1 if on else 0, st))
+        return None if on else {"jobs": st[0], "wrong": st[1]}
 
     def debug_service_hold(self, hold):
         """Test hook: the service's followers wait at their start while held."""
