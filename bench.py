@@ -56,6 +56,9 @@ def parse(argv=None):
     p.add_argument("--no-connection", action="store_true")
     p.add_argument("--no-beside-service", action="store_true",
                    help="skip the phased encode beside another context's resident worker")
+    p.add_argument("--beside-only", action="store_true",
+                   help="only the phased-encode-beside-a-fed-service leg, as one JSON line "
+                        "(the default run starts it as a child process under a time limit)")
     p.add_argument("--no-fused", action="store_true")
     p.add_argument("--no-ceilings", action="store_true")
     p.add_argument("--no-verify", action="store_true")
@@ -476,8 +479,7 @@ def bench_phase_beside_service(work, reps=6):
     alone = encodes([])  # the same launches without the other context
     b = qfec.Context(work.dev.index)
     try:
-        b.debug_service_feed(True)
-        time.sleep(0.02)  # its worker resident and busy
+        b.debug_service_feed(True)  # (back once its first batch is done)
         before = ctx.phase_abandons()
         grids = []
         w0 = time.perf_counter()
@@ -486,7 +488,8 @@ def bench_phase_beside_service(work, reps=6):
         finally:
             fed = b.debug_service_feed(False)
         wall = time.perf_counter() - w0
-        launches = b.debug_service()["launches"]
+        bst = b.debug_service()
+        launches, rotations = bst["launches"], bst.get("rotations")
     finally:
         b.close()
     work.synchronize()
@@ -499,7 +502,7 @@ def bench_phase_beside_service(work, reps=6):
             "ncu": torch.cuda.get_device_properties(work.dev.index).multi_processor_count,
             "abandoned": ctx.phase_abandons() - before,
             "service_jobs_meanwhile": fed["jobs"], "service_wrong": fed["wrong"],
-            "service_launches": launches,
+            "service_launches": launches, "service_rotations": rotations,
             "service_us_per_job": round(wall / max(fed["jobs"], 1) * 1e6, 2),
             "spin_ms": [round(x, 1) for x in spins],
             "parity_equal_uncontended": same,
@@ -626,6 +629,18 @@ def main(argv=None):
 
     import torch
     import torch.distributed as dist
+
+    if args.beside_only:  # the beside-service leg on its own (a child of the default run)
+        torch.cuda.set_device(0)
+        work = HipFixedWorkload(torch, torch.device("cuda", 0), 0, args.groups, args.k, args.L)
+        work.step()
+        work.synchronize()
+        if work.ctx.last_fixed_phased() != 1:
+            print(json.dumps({"phase_beside_service": None, "note": "batch not phased"}), flush=True)
+        else:
+            print(json.dumps({"phase_beside_service": bench_phase_beside_service(work)}), flush=True)
+        work.ctx.close()
+        return 0
 
     if args.protect_only:  # instruction-count runs of the protection kernels
         from libquic_amd import qfec
@@ -759,9 +774,19 @@ def main(argv=None):
         line["recover_inslot"] = bench_inslot(work, max(4, args.steps // 2 * 2),
                                               verify=not args.no_verify)
     if extras and not args.one_pass and phased and not args.no_beside_service:
+        # in a child process under a time limit: the leg runs two contexts and
+        # a native feeder thread, and a stall there must not cost the line
         _progress("phase beside service")
-        work.step()  # the parity the contended encodes must reproduce
-        line["phase_beside_service"] = bench_phase_beside_service(work)
+        import subprocess
+        cmd = [sys.executable, os.path.abspath(__file__), "--beside-only", "--groups", str(G),
+               "--k", str(k), "--L", str(L)]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            line["phase_beside_service"] = (json.loads(js[-1])["phase_beside_service"] if js else
+                                            {"error": f"rc {r.returncode}", "stderr": r.stderr[-400:]})
+        except subprocess.TimeoutExpired:
+            line["phase_beside_service"] = {"error": "timed out (240 s)"}
         _progress("phase beside service done")
     if extras and not args.no_ceilings:
         line["ceilings"] = bench_ceilings(work.ctx, torch, work.rows, work.stream)

@@ -475,9 +475,9 @@ int qfec_debug_fail_launches(qfec_ctx* ctx, int on);
  * number -- a malformed ring, whose job must fail with QFEC_ERR_INTERNAL and
  * turn the service off rather than report stale output); stats (may be NULL)
  * receives {worker launches, jobs finished, worker alive}; on = 3 leaves the
- * setting and fills stats[0..4] with those plus {worker stream busy, us since
- * the context's last service job or warm} (the view the phased launches of
- * other contexts take of it).  Test / measurement hook; the service is on by
+ * setting and fills stats[0..5] with those plus {worker stream busy, us since
+ * the context's last service job or warm (the view the phased launches of
+ * other contexts take of it), workers stopped for their 2-ms residency bound}.  Test / measurement hook; the service is on by
  * default.  Any failed service job turns the service off for the context
  * (small batches then launch). */
 int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats);
@@ -497,8 +497,8 @@ int qfec_debug_service_stamps(qfec_ctx* ctx, int on, uint64_t* stamps);
 int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out);
 /* Measurement hook (round 6): on = 1 starts a native thread that owns ctx
  * (the caller must not use ctx until it is stopped) and flushes one-group
- * mapped batches of 10 x 1350 B back to back, warming the small-batch worker
- * at each turn's start; on = 0 stops it and returns its code, with stats
+ * mapped batches of 10 x 1350 B in loop turns 20 us apart, warming the
+ * small-batch worker at each turn's start; on = 0 stops it and returns its code, with stats
  * (nullable) = {batches flushed, batches whose parity was wrong}. */
 int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats);
 /* Test hook: hold != 0 keeps the service's follower workgroups waiting at

@@ -150,8 +150,10 @@ struct qfec_ctx {
   uint64_t svc_published = 0;
   uint32_t svc_seq = 0;
   uint64_t svc_launches = 0;
+  uint64_t svc_rotations = 0;  // workers stopped for their residency bound (svc_submit)
   bool svc_on = true;  // test hook qfec_debug_service
   uint64_t svc_used_ns = 0;  // steady clock of the last service job / warm (other_service_cus)
+  uint64_t svc_launch_ns = 0;  // steady clock of the worker's last launch (kSvcMaxResidentNs)
   // measurement hook (stamps on): the last service call's host stamps, steady
   // ns: entry, published, token seen, return (qfec_debug_service_trace)
   uint64_t svc_hst[4] = {0, 0, 0, 0};
@@ -182,7 +184,11 @@ int fail(qfec_ctx* ctx, int code, const char* fmt, ...) {
 
 int bind(qfec_ctx* ctx) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
-  QFEC_HIP(ctx, hipSetDevice(ctx->device));
+  // (hipGetDevice reads the thread's current device; the set only when it
+  // differs -- every C-ABI call binds, and a connection thread makes many)
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != ctx->device)
+    QFEC_HIP(ctx, hipSetDevice(ctx->device));
   return QFEC_OK;
 }
 
@@ -343,6 +349,12 @@ int ensure_service(qfec_ctx* ctx) {
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_sh_dev), ctx->svc_sh, 0));
   QFEC_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->svc_ring_dev), ctx->svc_ring, 0));
   QFEC_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->svc_dev), sizeof(qfec::SvcDev)));
+  // (The runtime multiplexes a process's streams onto 4 hardware queues;
+  // work on a stream that shares the worker's queue waits behind the
+  // resident worker: svc_submit bounds its residency, kSvcMaxResidentNs.  A
+  // greatest-priority stream instead -- its own pool of queues -- made every
+  // phased launch of another context beside a fed worker abandon its
+  // meetings: measured and not kept, profiles/round6/pytest_r6j.log.)
   QFEC_HIP(ctx, hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
   // zeroed on the worker's own stream (a non-blocking stream is not ordered
   // after the null stream's memset)
@@ -371,12 +383,30 @@ qfec::SvcJob* svc_next_entry(qfec_ctx* ctx) {
 struct SvcTabs {
   uint32_t bytes, off, len, ptr, poff, plen, miss, ooff;
 };
+// Bounded residency (round 6): the runtime multiplexes a process's streams
+// onto 4 hardware queues, and work on any stream that shares the worker's
+// queue waits behind the resident worker -- for as long as a connection
+// thread keeps it fed (measured: another context's phased launch stalled for
+// seconds, once for good, beside a worker fed back to back).  So a worker
+// that has been resident this long is stopped at the next job and launched
+// anew behind whatever queued up meanwhile: a wait of at most ~2 ms for the
+// other work, one relaunch per 2 ms for the service.
+constexpr uint64_t kSvcMaxResidentNs = 2000000;
+void stop_service(qfec_ctx* ctx);
+
 int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token,
                const SvcTabs& tb) {
   int rc = ensure_service(ctx);
   if (rc) return rc;
-  __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
+  const uint64_t now = steady_ns();
+  __atomic_store_n(&ctx->svc_used_ns, now, __ATOMIC_RELEASE);
   qfec::SvcShared* sh = ctx->svc_sh;
+  if (ctx->svc_launch_ns != 0 && now - ctx->svc_launch_ns > kSvcMaxResidentNs &&
+      __atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) != 0u) {
+    stop_service(ctx);  // (published jobs it did not finish: the next worker's)
+    __atomic_store_n(&sh->quit, 0u, __ATOMIC_SEQ_CST);
+    ++ctx->svc_rotations;
+  }
   const uint32_t seq = ctx->svc_seq++;
   qfec::SvcJob& j = ctx->svc_ring[seq % qfec::kSvcRing];
   j.a = a;
@@ -427,6 +457,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
       return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
     }
     ++ctx->svc_launches;
+    ctx->svc_launch_ns = now;
   }
   return QFEC_OK;
 }
@@ -2138,6 +2169,7 @@ int qfec_service_warm(qfec_ctx* ctx) {
     return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
   }
   ++ctx->svc_launches;
+  ctx->svc_launch_ns = steady_ns();
   return QFEC_OK;
 }
 
@@ -2166,6 +2198,7 @@ int qfec_debug_service(qfec_ctx* ctx, int on, uint64_t* stats) {
     stats[3] = ctx->svc_stream && hipStreamQuery(ctx->svc_stream) == hipErrorNotReady ? 1u : 0u;
     const uint64_t used = __atomic_load_n(&ctx->svc_used_ns, __ATOMIC_ACQUIRE);
     stats[4] = used ? (steady_ns() - used) / 1000u : ~0ull;  // us since its last job / warm
+    stats[5] = ctx->svc_rotations;
   }
   return QFEC_OK;
 }
@@ -2251,6 +2284,12 @@ int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats) {
       const uint64_t poff = 0;
       uint16_t plen = 0;
       while (!f->stop.load(std::memory_order_relaxed)) {
+        // a loop turn's other work: 20 us without runtime calls (a feeder
+        // calling into the HIP runtime back to back stalled the measuring
+        // thread's launches and event waits for seconds)
+        const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(20);
+        while (std::chrono::steady_clock::now() < t_end) {
+        }
         (void)qfec_service_warm(ctx);  // the turn's start
         const int r = qfec_encode_ragged(ctx, data, off, len, ptr, 1, par, &poff, &plen,
                                          QFEC_PTR_MAPPED);
@@ -2265,6 +2304,9 @@ int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats) {
       qfec_host_free(par);
     });
     g_feeders.emplace_back(ctx, f);
+    // back once the first batch is done (the worker resident and the
+    // context registered), or the thread failed
+    while (f->jobs.load() == 0 && f->rc.load() == QFEC_OK) std::this_thread::yield();
     return QFEC_OK;
   }
   if (it == g_feeders.end()) return fail(ctx, QFEC_ERR_INTERNAL, "no feeder running");

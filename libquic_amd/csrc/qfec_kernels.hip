@@ -2388,14 +2388,21 @@ hipError_t launch_fixed_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint64_t
 // templated k takes kPhRegSteps (round 4; round 3 had
 // them for k = 10 only; round 5 templates every k up to 16).  Larger k run
 // the runtime-k body with the LDS steps alone.
-// Round 6: group sizes above 16 templated for the phased kernel alone (the
-// one-pass kernel keeps its runtime-k body there).
-#define QFEC_K_PHASE_WIDE(X) X(20)
-__host__ __device__ constexpr bool phase_k_templated(uint32_t k) {
-  return (k >= 2u && k <= 16u) || k == 20u;
+// Round 6: the phased RECOVER of group sizes 17-25 is templated too (its
+// register steps, parity rows first and compact received rows, as k <= 16):
+// recover 0.709 / 0.731 / 0.759 (runtime body) -> 0.779 / 0.785 / 0.797 at
+// k = 17 / 20 / 24, where the templated encode is no faster than the runtime
+// body's batches of 16 (k = 20: 0.804 vs 0.809); from k = 26 the templated
+// recover spills (528 B of scratch) and loses (0.70-0.71 against the
+// runtime body's 0.76-0.77) (profiles/round6/phase_k_table_r6{i,j}.txt).  So
+// encode, the in-place form, recover above 25 and the one-pass kernel keep
+// the runtime body above 16.
+#define QFEC_K_PHASE_RECOVER(X) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25)
+__host__ __device__ constexpr bool phase_k_templated(bool recover, uint32_t k) {
+  return (k >= 2u && k <= 16u) || (recover && k >= 17u && k <= 25u);
 }
-__host__ __device__ constexpr uint32_t phase_reg_steps(uint32_t k) {
-  return phase_k_templated(k) ? (uint32_t)kPhRegSteps : 0u;
+__host__ __device__ constexpr uint32_t phase_reg_steps(bool recover, uint32_t k) {
+  return phase_k_templated(recover, k) ? (uint32_t)kPhRegSteps : 0u;
 }
 
 // The runtime-k phased body's load batch (k > 16) by operation and group
@@ -2429,9 +2436,15 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
                          gpb, nphase);                                                          \
     break;
     QFEC_K_ALL(QFEC_K_CASE)
-    QFEC_K_PHASE_WIDE(QFEC_K_CASE)
-#undef QFEC_K_CASE
     default:
+      if constexpr (RECOVER) {
+        switch (a.rt_batch != 0u ? 0u : a.k) {
+          QFEC_K_PHASE_RECOVER(QFEC_K_CASE)
+          default:
+            break;
+        }
+        if (a.rt_batch == 0u && phase_k_templated(true, a.k)) break;
+      }
       // runtime k: batches of up to 16 or 32 loads, by the measured table
       // (phase_rt_batch; test hook rt_batch: either, the A/B of
       // tools/phase_k_table.py)
@@ -2446,6 +2459,7 @@ hipError_t launch_phase_k(const FixedArgs& a, uint32_t C, uint32_t gpb, uint32_t
                                              32>),
                            dim3(grid), dim3(kBlock), 0, s, a, C, gpb, nphase);
   }
+#undef QFEC_K_CASE
   return hipGetLastError();
 }
 
@@ -2501,7 +2515,7 @@ bool phase_plan(const FixedArgs& a, uint32_t gpb, uint32_t* grid, uint32_t* npha
       (uint64_t)wg *
       (kPhSteps + ((a.no_regsteps && !a.inplace_missing) || (a.rt_batch != 0u && a.k > 16u)
                        ? 0u
-                       : phase_reg_steps(a.k))) *
+                       : phase_reg_steps(a.parity != nullptr && !a.inplace_missing, a.k))) *
       gpb;
   *grid = wg;
   *nphase = (uint32_t)((a.n_groups + per_l - 1) / per_l);

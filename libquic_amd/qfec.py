@@ -462,12 +462,12 @@ class Context:
         """Small-batch service hook: on True / False enables / disables the
         resident worker (None leaves it); poison_next malforms the next job's
         ring entry (test of the ring-miss path); returns {launches, jobs, alive}."""
-        st = (C.c_uint64 * 5)()
+        st = (C.c_uint64 * 6)()
         mode = 2 if poison_next else (3 if on is None else int(bool(on)))
         self._check(self.lib.qfec_debug_service(self.ctx, mode, st))
         d = {"launches": st[0], "jobs": st[1], "alive": st[2]}
         if mode == 3:  # the registry's view: worker stream busy, us since last use
-            d["stream_busy"], d["idle_us"] = st[3], st[4]
+            d["stream_busy"], d["idle_us"], d["rotations"] = st[3], st[4], st[5]
         return d
 
     def debug_service_stamps(self, on=None):

@@ -104,7 +104,8 @@ def test_default_kernel_choice_by_group_size(ctx, k):
 @pytest.mark.parametrize("k,L", [(10, 1350), (7, 1350), (33, 1350), (16, 1452), (2, 100),
                                  (5, 17), (2, 16), (4, 1350), (8, 1001), (6, 1350), (12, 1350),
                                  (20, 1350), (17, 100), (40, 64), (64, 1350), (255, 1350),
-                                 (48, 300), (1, 300)])
+                                 (48, 300), (1, 300), (32, 1350), (24, 700), (17, 1350),
+                                 (26, 512)])
 def test_phased_vs_one_pass_and_oracle(ctx, k, L):
     n = 8 * phase_groups(L) + 777  # 9 phases, the last one ragged
     rows = torch.empty(n * k * L, dtype=torch.uint8, device=DEV)

@@ -401,9 +401,8 @@ def test_phased_launch_beside_a_continuously_fed_service():
         want = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
         a.encode(rows, k, L, n, want, one_pass=True)
         a.sync()
-        b.debug_service_feed(True)
+        b.debug_service_feed(True)  # (back once its first batch is done)
         try:
-            time.sleep(0.02)  # the worker resident and busy
             before = a.phase_abandons()
             par = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
             s = torch.cuda.current_stream()
