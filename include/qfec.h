@@ -505,6 +505,11 @@ int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats);
  * their start (as if dispatched late behind another kernel) until it is
  * cleared; the leader runs on.  A split job's token then waits for them. */
 int qfec_debug_service_hold(qfec_ctx* ctx, int hold);
+/* Test hook (round 6): the small-batch worker's residency bound, ns (default
+ * 2,000,000; 0 rotates the worker at every job published while it runs --
+ * the successor queued behind it, no wait); returns the previous bound, or 0
+ * for a null ctx. */
+uint64_t qfec_debug_service_resident(qfec_ctx* ctx, uint64_t ns);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

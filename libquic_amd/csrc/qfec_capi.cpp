@@ -154,6 +154,7 @@ struct qfec_ctx {
   bool svc_on = true;  // test hook qfec_debug_service
   uint64_t svc_used_ns = 0;  // steady clock of the last service job / warm (other_service_cus)
   uint64_t svc_launch_ns = 0;  // steady clock of the worker's last launch (kSvcMaxResidentNs)
+  uint64_t svc_max_resident_ns;  // the residency bound (kSvcMaxResidentNs; test hook)
   // measurement hook (stamps on): the last service call's host stamps, steady
   // ns: entry, published, token seen, return (qfec_debug_service_trace)
   uint64_t svc_hst[4] = {0, 0, 0, 0};
@@ -388,11 +389,12 @@ struct SvcTabs {
 // queue waits behind the resident worker -- for as long as a connection
 // thread keeps it fed (measured: another context's phased launch stalled for
 // seconds, once for good, beside a worker fed back to back).  So a worker
-// that has been resident this long is stopped at the next job and launched
-// anew behind whatever queued up meanwhile: a wait of at most ~2 ms for the
-// other work, one relaunch per 2 ms for the service.
+// that has been resident this long is rotated at the next job: told to leave
+// between turns, a successor queued behind whatever the hardware queue took
+// meanwhile -- a wait of at most ~2 ms for the other work, one relaunch per
+// 2 ms for the service, and no wait on the connection thread.
 constexpr uint64_t kSvcMaxResidentNs = 2000000;
-void stop_service(qfec_ctx* ctx);
+void svc_abandon(qfec_ctx* ctx);
 
 int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token,
                const SvcTabs& tb) {
@@ -401,11 +403,27 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   const uint64_t now = steady_ns();
   __atomic_store_n(&ctx->svc_used_ns, now, __ATOMIC_RELEASE);
   qfec::SvcShared* sh = ctx->svc_sh;
-  if (ctx->svc_launch_ns != 0 && now - ctx->svc_launch_ns > kSvcMaxResidentNs &&
+  if (ctx->svc_launch_ns != 0 && now - ctx->svc_launch_ns >= ctx->svc_max_resident_ns &&
       __atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) != 0u) {
-    stop_service(ctx);  // (published jobs it did not finish: the next worker's)
-    __atomic_store_n(&sh->quit, 0u, __ATOMIC_SEQ_CST);
+    // rotate without waiting for it (round 6: a synchronous stop cost the
+    // one-connection path ~0.35 us a group, profiles/round6/bench_r6fin2.json):
+    // the resident worker -- and a spare queued behind it -- leave at their
+    // next look, published jobs or not; the successor launched now runs after
+    // them on the worker stream, behind whatever other work the hardware
+    // queue took meanwhile, and starts at what they consumed
+    __atomic_store_n(&sh->rotate, ctx->svc_epoch, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
+    const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev,
+                                                     ctx->svc_ring_dev, ctx->h_flag_dev,
+                                                     kSvcIdleTicks, ++ctx->svc_epoch,
+                                                     ctx->svc_stream);
+    if (e != hipSuccess) {
+      svc_abandon(ctx);  // every worker gone, the ring rewound, the service off
+      return fail(ctx, QFEC_ERR_INTERNAL, "small-batch service launch: %s", hipGetErrorString(e));
+    }
+    ++ctx->svc_launches;
     ++ctx->svc_rotations;
+    ctx->svc_launch_ns = now;
   }
   const uint32_t seq = ctx->svc_seq++;
   qfec::SvcJob& j = ctx->svc_ring[seq % qfec::kSvcRing];
@@ -1138,11 +1156,20 @@ qfec_ctx* qfec_create(int device) {
   *ctx->h_phase = 0;
   ctx->ncu = ncu > 0 ? (uint32_t)ncu : 0;
   ctx->stream = ctx->own_stream;
+  ctx->svc_max_resident_ns = kSvcMaxResidentNs;
+  // (measurement knob: QFEC_SVC_RESIDENT_US overrides the residency bound)
+  if (const char* r = std::getenv("QFEC_SVC_RESIDENT_US"))
+    ctx->svc_max_resident_ns = std::strtoull(r, nullptr, 10) * 1000ull;
   return ctx;
 }
 
+namespace {
+void stop_feeder(qfec_ctx* ctx);  // (a measurement feeder still running on ctx)
+}  // namespace
+
 void qfec_destroy(qfec_ctx* ctx) {
   if (!ctx) return;
+  stop_feeder(ctx);
   (void)hipSetDevice(ctx->device);
   {
     std::lock_guard<std::mutex> lock(g_svc_mu);
@@ -2234,6 +2261,13 @@ int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out) {
   return QFEC_OK;
 }
 
+uint64_t qfec_debug_service_resident(qfec_ctx* ctx, uint64_t ns) {
+  if (!ctx) return 0;
+  const uint64_t prev = ctx->svc_max_resident_ns;
+  ctx->svc_max_resident_ns = ns;
+  return prev;
+}
+
 // Measurement hook (round 6, bench leg phase_beside_service): a native
 // connection thread that owns ctx until stopped and flushes one-group mapped
 // batches back to back, warming the worker at each turn's start -- what an
@@ -2248,6 +2282,21 @@ struct Feeder {
 };
 std::mutex g_feed_mu;
 std::vector<std::pair<qfec_ctx*, Feeder*>> g_feeders;
+
+void stop_feeder(qfec_ctx* ctx) {
+  Feeder* f = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_feed_mu);
+    auto it = std::find_if(g_feeders.begin(), g_feeders.end(),
+                           [ctx](const std::pair<qfec_ctx*, Feeder*>& x) { return x.first == ctx; });
+    if (it == g_feeders.end()) return;
+    f = it->second;
+    g_feeders.erase(it);
+  }
+  f->stop = true;
+  f->th.join();
+  delete f;
+}
 }  // namespace
 
 int qfec_debug_service_feed(qfec_ctx* ctx, int on, uint64_t* stats) {

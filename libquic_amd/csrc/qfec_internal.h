@@ -158,6 +158,9 @@ struct SvcShared {
   uint32_t stamp_on;  // host (measurement hook): the worker records stamps[] for each job
   uint32_t hold;      // host (test hook qfec_debug_service_hold): followers wait at
                       // their start while it is 1 (a follower dispatched late)
+  uint32_t rotate;    // host: a worker whose launch epoch is at most this leaves at
+                      // its next look, published jobs or not -- its successor is
+                      // already queued behind it (svc_submit's residency bound)
   // the worker's words, stored every turn
   alignas(64) uint64_t consumed;  // worker: groups finished (a new worker starts here)
   uint64_t jobs;      // worker: jobs finished (stats)

@@ -2077,12 +2077,17 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         const uint32_t lane2 = 2u * lane;
         const uint64_t* hp = reinterpret_cast<const uint64_t*>(ring + (job0 % kSvcRing)) + lane2;
         uint64_t h0 = 0, h1 = 0;
+        uint32_t rot = 0;  // the rotate word, read with every look (same round trip)
         auto look = [&]() -> uint64_t {
           const uint64_t t = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          rot = __hip_atomic_load(&sh->rotate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           h0 = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           h1 = __hip_atomic_load(hp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           return t;
         };
+        // rotated out (wrap-safe epoch compare): leave between turns, the
+        // published jobs to the successor queued behind (it starts at consumed)
+        auto rotated = [&]() { return (int32_t)(rot - epoch) >= 0; };
         uint64_t to = look();
         uint32_t ex = 0;
         const uint64_t t0 = wall_clock64();
@@ -2116,6 +2121,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
             to = look();
           }
         }
+        if (!ex && rotated()) ex = 1;
         // the head found whole (its hash, seq and start agree): the entry's
         // size is known -- a small job is all in LDS already, a larger one's
         // header is, and the rest is copied in one pass

@@ -112,6 +112,7 @@ SIGNATURES = [
     ("qfec_debug_service_stamps", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_trace", C.c_int, [_vp, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_feed", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
+    ("qfec_debug_service_resident", C.c_uint64, [_vp, C.c_uint64]),
     ("qfec_debug_service_hold", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
@@ -495,6 +496,11 @@ class Context:
     def debug_service_hold(self, hold):
         """Test hook: the service's followers wait at their start while held."""
         return self._check(self.lib.qfec_debug_service_hold(self.ctx, 1 if hold else 0))
+
+    def debug_service_resident(self, ns):
+        """Test hook: the worker's residency bound in ns (0: rotate at every
+        job); returns the previous bound."""
+        return int(self.lib.qfec_debug_service_resident(self.ctx, int(ns)))
 
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""

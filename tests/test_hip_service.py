@@ -435,6 +435,106 @@ def test_phased_launch_beside_a_continuously_fed_service():
         b.close()
 
 
+def test_fed_worker_rotates_and_other_work_proceeds():
+    """Round 6: a worker fed back to back stays resident at most 2 ms at a
+    stretch (kSvcMaxResidentNs): the runtime multiplexes a process's streams
+    onto 4 hardware queues, and work on a stream sharing the worker's queue
+    waited behind it -- for seconds, once for good, before the bound.  With a
+    native thread feeding context B for ~0.3 s, context A's kernels on its own
+    streams (one-pass encodes, then device syncs) each finish within 100 ms,
+    B's worker was stopped and relaunched many times, and every B batch was
+    exact."""
+    import torch
+    from oracle import qfec_np as Q
+    a, b = qfec.Context(0), qfec.Context(0)
+    try:
+        k, L, n = 10, 1350, 4096
+        rows = torch.empty(n * k * L, dtype=torch.uint8, device="cuda:0")
+        a.synth_fixed(rows, k, L, 0, n, Q.SEED_FIXED)
+        want = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        a.encode(rows, k, L, n, want, one_pass=True)
+        a.sync()
+        par = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        b.debug_service_feed(True)
+        worst = 0.0
+        try:
+            t_end = time.perf_counter() + 0.3
+            while time.perf_counter() < t_end:
+                t0 = time.perf_counter()
+                a.encode(rows, k, L, n, par, one_pass=True)
+                a.sync()
+                worst = max(worst, time.perf_counter() - t0)
+        finally:
+            fed = b.debug_service_feed(False)
+        st = b.debug_service()
+        print(f"worst one-pass encode beside a fed worker {worst * 1e3:.2f} ms; feeder {fed}; "
+              f"service {st}")
+        assert torch.equal(par, want)
+        assert fed["wrong"] == 0 and fed["jobs"] > 100, fed
+        assert st["rotations"] >= 10, st
+        assert worst < 0.1, worst
+    finally:
+        a.close()
+        b.close()
+
+
+def test_rotation_at_every_job_with_jobs_in_flight():
+    """Round 6: a rotation does not wait for the worker -- it is told to leave
+    between turns (published jobs or not) and its successor is queued behind
+    it, starting at what it consumed.  With the bound at 0 every job published
+    while a worker runs rotates it: up to three asynchronous jobs in flight
+    (1 group: the leader's; 9-64 groups: split over the workgroups, whose
+    followers leave by their own launch epoch), completed in order and out of
+    order, encode and recover -- every byte exact, and the worker was rotated
+    at most jobs."""
+    from test_hip_mapped import _mapped_case as mc
+    ctx = qfec.Context(0)
+    bufs = []
+    try:
+        assert ctx.debug_service_resident(0) == 2_000_000
+        shapes = [mc(n, g0=52000 + 100 * i, kmin=2, kmax=16, lmin=1, lmax=1452, seed=70 + i)
+                  for i, n in enumerate((1, 9, 64, 3, 40))]
+        slots = []
+        for z, want_l in shapes:
+            n = len(z["grp_ptr"]) - 1
+            data = qfec.HostBuffer(len(z["data"]))
+            data.array[:] = z["data"]
+            par = qfec.HostBuffer(n * 1452)
+            bufs += [data, par]
+            slots.append((z, want_l, data, par, n))
+        before = ctx.debug_service()
+        jobs = 0
+        for it in range(40):
+            batch = [slots[(it + j) % len(slots)] for j in range(1 + it % 3)]
+            pend = []
+            for z, want_l, data, par, n in batch:
+                par.array[:] = 0
+                plen = np.zeros(n, dtype=np.uint16)
+                ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], n,
+                                  par.array, z["parity_off"], plen, mapped=True, async_=True)
+                pend.append((ctx.async_ticket(), z, want_l, par, plen, n))
+                jobs += 1
+            for t, z, want_l, par, plen, n in (reversed(pend) if it % 2 else pend):
+                assert ctx.complete_ticket(t) == 0
+                assert np.array_equal(plen, want_l), it
+                for g in range(n):
+                    o, m = int(z["parity_off"][g]), int(want_l[g])
+                    assert np.array_equal(par.array[o:o + m], z["parity"][o:o + m]), (it, n, g)
+            if it % 4 == 3:  # recover too (synchronous, the same rotation path)
+                z, want_l = shapes[it % len(shapes)]
+                _check(ctx, z, want_l)
+                jobs += 2
+        st = ctx.debug_service()
+        print(f"rotation at every job: {jobs} jobs, service {st}")
+        assert st["jobs"] >= before["jobs"] + jobs, st
+        assert st["rotations"] >= jobs // 2, st
+    finally:
+        ctx.debug_service_resident(2_000_000)
+        for b in bufs:
+            b.close()
+        ctx.close()
+
+
 def test_quiet_service_context_leaves_the_phased_grid_whole():
     """Round 6: another context counts against a phased grid only while its
     worker runs or for 2 ms after its last job or warm (kSvcRecentNs); a
