@@ -183,10 +183,16 @@ int fail(qfec_ctx* ctx, int code, const char* fmt, ...) {
       return fail((ctx), QFEC_ERR_INTERNAL, "%s: %s", #expr, hipGetErrorString(_e)); \
   } while (0)
 
+// The calling thread's current device made ctx's, before anything that
+// allocates or launches.  (hipGetDevice reads it, ~50 ns; the set only when it
+// differs.)  The connection thread's per-turn calls skip it where they touch
+// only the context's own streams, events and host-mapped words -- completion
+// polls, a warm call that finds the worker running, a small batch handed to
+// the running worker (round 6: five binds a loop turn were ~0.2 us per group
+// at one connection) -- and bind on their slow paths (first allocations,
+// (re)launches, staged copies, error collection).
 int bind(qfec_ctx* ctx) {
   if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
-  // (hipGetDevice reads the thread's current device; the set only when it
-  // differs -- every C-ABI call binds, and a connection thread makes many)
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess || cur != ctx->device)
     QFEC_HIP(ctx, hipSetDevice(ctx->device));
@@ -254,6 +260,8 @@ bool is_pinned_or_device(const void* p) {
 
 int ensure_staging(qfec_ctx* ctx) {
   if (ctx->staging_ready) return QFEC_OK;
+  int rc = bind(ctx);
+  if (rc) return rc;
   for (auto& s : ctx->slots) {
     QFEC_HIP(ctx, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     QFEC_HIP(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -340,6 +348,8 @@ uint32_t other_service_cus(const qfec_ctx* ctx, uint32_t* why = nullptr) {
 
 int ensure_service(qfec_ctx* ctx) {
   if (ctx->svc_stream) return QFEC_OK;
+  int rc = bind(ctx);
+  if (rc) return rc;
   const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
   QFEC_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->svc_sh), sizeof(qfec::SvcShared), fl));
   std::memset(static_cast<void*>(ctx->svc_sh), 0, sizeof(qfec::SvcShared));
@@ -411,6 +421,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
     // next look, published jobs or not; the successor launched now runs after
     // them on the worker stream, behind whatever other work the hardware
     // queue took meanwhile, and starts at what they consumed
+    if ((rc = bind(ctx))) return rc;
     __atomic_store_n(&sh->rotate, ctx->svc_epoch, __ATOMIC_SEQ_CST);
     __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
     const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev,
@@ -460,10 +471,12 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
   if (__atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) == 0u) {
     __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
-    const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev,
-                                                     ctx->svc_ring_dev, ctx->h_flag_dev,
-                                                     kSvcIdleTicks, ++ctx->svc_epoch,
-                                                     ctx->svc_stream);
+    const hipError_t e =
+        bind(ctx) != QFEC_OK
+            ? hipErrorInvalidDevice
+            : qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev, ctx->svc_ring_dev,
+                                          ctx->h_flag_dev, kSvcIdleTicks, ++ctx->svc_epoch,
+                                          ctx->svc_stream);
     if (e != hipSuccess) {
       // no worker runs (none was alive): take the job back, so that no later
       // worker ever runs it over a reused slot buffer
@@ -517,6 +530,7 @@ void stop_service(qfec_ctx* ctx) {
 void svc_abandon(qfec_ctx* ctx) {
   __atomic_store_n(&ctx->svc_on, false, __ATOMIC_RELEASE);
   if (!ctx->svc_sh) return;
+  (void)bind(ctx);  // (reached from completion calls, which do not bind)
   stop_service(ctx);
   for (uint32_t i = 0; i < qfec::kSvcRing; ++i)
     __atomic_store_n(&ctx->svc_ring[i].seq, 0xFFFFFFFFu, __ATOMIC_RELEASE);
@@ -689,6 +703,8 @@ int latch_error(qfec_ctx* ctx, uint32_t bits) {
 
 // Read and clear the device error word after `stream` has drained.
 int collect_error(qfec_ctx* ctx, hipStream_t stream, int word) {
+  int rc = bind(ctx);  // (reached from completion calls, which do not bind)
+  if (rc) return rc;
   QFEC_HIP(ctx, hipMemcpyAsync(ctx->h_err + word, ctx->d_err + word, sizeof(uint32_t),
                                hipMemcpyDeviceToHost, stream));
   QFEC_HIP(ctx, hipStreamSynchronize(stream));
@@ -1235,8 +1251,9 @@ int qfec_complete(qfec_ctx* ctx, int wait) {
 uint64_t qfec_async_ticket(const qfec_ctx* ctx) { return ctx ? ctx->last_ticket : 0; }
 
 int qfec_complete_ticket(qfec_ctx* ctx, uint64_t ticket, int wait) {
-  int rc = bind(ctx);
-  if (rc) return rc;
+  // no bind: a completion polls the context's own flags, streams and events
+  // (collect_error and svc_abandon bind on the slow paths)
+  if (!ctx) return fail(nullptr, QFEC_ERR_INTERNAL, "null qfec_ctx");
   qfec_ctx::Kept& f = ctx->kept[ticket % qfec_ctx::kKept];
   if (ticket != 0 && f.ticket == ticket) {
     f.ticket = 0;  // claimed once
@@ -1709,6 +1726,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
     // in one round trip); everything else through the slot's mapped buffer
     bool svc = direct && ctx->svc_on && cnt <= kSvcGroups && t.total <= qfec::kSvcTab &&
                ensure_service(ctx) == QFEC_OK;
+    if (!svc && (rc = bind(ctx))) return rc;  // (a launch follows; the service binds itself)
     qfec::SvcJob* je = svc ? svc_next_entry(ctx) : nullptr;
     uint8_t* h = svc ? je->tab : s.h_in;
     std::memcpy(h + t.off, pkt_off + p0, np * 8);  // payloads stay where they are
@@ -1766,6 +1784,7 @@ int ragged_mapped(qfec_ctx* ctx, bool recover, const uint8_t* bytes, const uint6
         __atomic_store_n(&ctx->svc_on, false, __ATOMIC_RELEASE);
         svc = false;
         std::memcpy(s.h_in, je->tab, t.total);
+        if ((rc = bind(ctx))) return rc;
       }
       if (!svc) {
         if (cnt <= kDirectGroups)
@@ -1813,7 +1832,8 @@ int qfec_encode_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt_
                        const uint16_t* pkt_len, const uint32_t* grp_ptr, uint64_t n_groups,
                        uint8_t* parity_out, const uint64_t* parity_off,
                        uint16_t* parity_len_out, uint32_t flags) {
-  int rc = bind(ctx);
+  // (mapped batches bind where they launch: ragged_mapped)
+  int rc = (flags & QFEC_PTR_MAPPED) && ctx ? QFEC_OK : bind(ctx);
   if (rc) return rc;
   ctx->last_ticket = 0;
   if (ctx->debug_fail)
@@ -1850,7 +1870,8 @@ int qfec_recover_ragged(qfec_ctx* ctx, const uint8_t* bytes, const uint64_t* pkt
                         const uint8_t* parity, const uint64_t* parity_off,
                         const uint16_t* parity_len, const uint8_t* missing_idx, uint8_t* out,
                         const uint64_t* out_off, uint32_t flags) {
-  int rc = bind(ctx);
+  // (mapped batches bind where they launch: ragged_mapped)
+  int rc = (flags & QFEC_PTR_MAPPED) && ctx ? QFEC_OK : bind(ctx);
   if (rc) return rc;
   ctx->last_ticket = 0;
   if (ctx->debug_fail)
@@ -2177,6 +2198,12 @@ int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_p
 uint32_t qfec_debug_last_phase_grid(const qfec_ctx* ctx) { return ctx ? ctx->last_phase_grid : 0u; }
 
 int qfec_service_warm(qfec_ctx* ctx) {
+  // the worker already running (a loop turn's usual case): no runtime call
+  if (ctx && ctx->svc_on && ctx->svc_sh &&
+      __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_SEQ_CST) != 0u) {
+    __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
+    return QFEC_OK;
+  }
   int rc = bind(ctx);
   if (rc) return rc;
   if (!ctx->svc_on) return QFEC_OK;
