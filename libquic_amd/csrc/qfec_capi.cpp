@@ -2198,10 +2198,13 @@ int qfec_last_fixed_phased(const qfec_ctx* ctx) { return ctx ? ctx->last_fixed_p
 uint32_t qfec_debug_last_phase_grid(const qfec_ctx* ctx) { return ctx ? ctx->last_phase_grid : 0u; }
 
 int qfec_service_warm(qfec_ctx* ctx) {
-  // the worker already running (a loop turn's usual case): no runtime call
+  // the worker already running (a loop turn's usual case): no runtime call;
+  // the warm count it polls restarts its idle time (a turn that takes most
+  // of the 100 us to assemble its batch still finds it resident)
   if (ctx && ctx->svc_on && ctx->svc_sh &&
       __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_SEQ_CST) != 0u) {
     __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
+    __atomic_store_n(&ctx->svc_sh->warm, ctx->svc_sh->warm + 1u, __ATOMIC_RELEASE);
     return QFEC_OK;
   }
   int rc = bind(ctx);

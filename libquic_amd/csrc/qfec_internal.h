@@ -161,6 +161,8 @@ struct SvcShared {
   uint32_t rotate;    // host: a worker whose launch epoch is at most this leaves at
                       // its next look, published jobs or not -- its successor is
                       // already queued behind it (svc_submit's residency bound)
+  uint32_t warm;      // host: bumped by qfec_service_warm on a running worker -- a
+                      // batch is coming; the worker's idle time restarts from it
   // the worker's words, stored every turn
   alignas(64) uint64_t consumed;  // worker: groups finished (a new worker starts here)
   uint64_t jobs;      // worker: jobs finished (stats)

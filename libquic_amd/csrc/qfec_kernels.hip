@@ -2078,9 +2078,11 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         const uint64_t* hp = reinterpret_cast<const uint64_t*>(ring + (job0 % kSvcRing)) + lane2;
         uint64_t h0 = 0, h1 = 0;
         uint32_t rot = 0;  // the rotate word, read with every look (same round trip)
+        uint32_t wm = 0;   // the host's warm count, likewise
         auto look = [&]() -> uint64_t {
           const uint64_t t = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           rot = __hip_atomic_load(&sh->rotate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          wm = __hip_atomic_load(&sh->warm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           h0 = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           h1 = __hip_atomic_load(hp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           return t;
@@ -2090,7 +2092,8 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
         auto rotated = [&]() { return (int32_t)(rot - epoch) >= 0; };
         uint64_t to = look();
         uint32_t ex = 0;
-        const uint64_t t0 = wall_clock64();
+        uint64_t t0 = wall_clock64();
+        uint32_t warm_seen = wm;
         while (to == from) {
           if (svc_load32(&sh->quit) != 0u) {
             ex = 1;
@@ -2115,10 +2118,18 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
             // this way costs one more round trip for its head
             __builtin_amdgcn_s_sleep(16);
             to = __hip_atomic_load(&sh->pub_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            wm = __hip_atomic_load(&sh->warm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (to != from) to = look();
           } else {
             __builtin_amdgcn_s_sleep(2);
             to = look();
+          }
+          // a warm call (a batch is coming this loop turn): the idle time
+          // restarts, so a turn whose batch takes most of it to assemble
+          // still finds the worker resident (round 6)
+          if (wm != warm_seen) {
+            warm_seen = wm;
+            t0 = wall_clock64();
           }
         }
         if (!ex && rotated()) ex = 1;

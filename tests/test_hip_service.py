@@ -478,6 +478,36 @@ def test_fed_worker_rotates_and_other_work_proceeds():
         b.close()
 
 
+def test_warm_restarts_the_idle_time():
+    """Round 6: qfec_service_warm on a running worker bumps a count the
+    worker polls, and its 100-us idle time restarts from it -- a loop turn
+    that takes most of the idle time to assemble its batch still finds the
+    worker resident.  Warm calls 50 us apart for 2 ms, no job: without the
+    restart the worker would leave every ~100 us and be relaunched ~15 times;
+    with it, it stays (a hiccup of the Python loop may cost one relaunch)."""
+    z, want_l = _mapped_case(2, g0=47000, kmin=10, kmax=10, lmin=1350, lmax=1350, seed=4)
+    ctx = qfec.Context(0)
+    try:
+        _check(ctx, z, want_l)
+        ctx.service_warm()
+        before = ctx.debug_service()["launches"]
+        t_end = time.perf_counter() + 0.002
+        nxt = time.perf_counter()
+        calls = 0
+        while time.perf_counter() < t_end:
+            if time.perf_counter() >= nxt:
+                ctx.service_warm()
+                calls += 1
+                nxt += 50e-6
+        st = ctx.debug_service()
+        print(f"{calls} warm calls over 2 ms: {st['launches'] - before} relaunches; {st}")
+        assert calls >= 20
+        assert st["launches"] - before <= 3, st
+        _check(ctx, z, want_l)
+    finally:
+        ctx.close()
+
+
 def test_rotation_at_every_job_with_jobs_in_flight():
     """Round 6: a rotation does not wait for the worker -- it is told to leave
     between turns (published jobs or not) and its successor is queued behind
