@@ -1251,8 +1251,10 @@ def _stall_picture(name):
     ceilings (SIMD-32: a wave64 VALU instruction issues in 2 cycles, 2 per CU
     per cycle; a 64-lane ds_read_b32 moves 256 B at 128 B per CU per cycle,
     0.5 per CU per cycle) and where its waves' cycles go (PMC:
-    tools/pmc_aead_stall.sh -> profiles/round5/aead_stall.json)."""
-    path = os.path.join(ROOT, "profiles", "round5", "aead_stall.json")
+    tools/pmc_aead_stall.sh -> profiles/round5/aead_stall.json, kept as
+    profiles/aead_stall_latest.json: the round directories do not travel to
+    the GPU box)."""
+    path = os.path.join(ROOT, "profiles", "aead_stall_latest.json")
     if not os.path.exists(path):
         return {}
     with open(path) as f:
@@ -1262,7 +1264,7 @@ def _stall_picture(name):
     keys = ("valu_issue_frac", "lds_issue_frac", "waves_per_simd", "active_any_frac",
             "wait_any_frac", "wait_inst_any_frac", "wait_lds_frac")
     return {"stall": {k: round(kd[k], 3) for k in keys if k in kd} |
-            {"source": "profiles/round5/aead_stall.json"}}
+            {"source": "profiles/aead_stall_latest.json (= round5/aead_stall.json)"}}
 
 
 def cpu_protect_baseline(hdr, L, n=1 << 16, seconds=4.0):
