@@ -74,6 +74,13 @@ def test_no_device_fails_loudly():
     # null-context calls return QUIC_INTERNAL_ERROR, never crash
     assert lib.qfec_sync(None) == -1
     assert lib.qfec_encode_batch(None, None, 10, 1350, 1, None, 0) == -1
+    # round 6: the calls that skip the device bind on their fast paths still
+    # refuse a null context
+    assert lib.qfec_complete_ticket(None, 1, 0) == -1
+    assert lib.qfec_service_warm(None) == -1
+    assert lib.qfec_encode_ragged(None, None, None, None, None, 1, None, None, None,
+                                  qfec.QFEC_PTR_MAPPED | qfec.QFEC_ASYNC) == -1
+    assert lib.qfec_debug_service_resident(None, 0) == 0
 
 
 def test_oracle_not_linked_by_product():
