@@ -73,6 +73,25 @@ __device__ __forceinline__ void st16t(uint8_t* p, u32x4 v) {
   }
 }
 
+// A 16-B store with an explicit cache policy (round 6 store-policy probe,
+// tools/tune only): 0 nt (the product's st16t<true>), 1 sc1, 2 sc0 sc1,
+// 3 nt sc1, 4 nt sc0 sc1 -- vector stores; sc1 drops the line from the XCD's
+// L2 (write-through), nt keeps it (MI355X_MICROARCH.md, store flavours).
+template <int POL>
+__device__ __forceinline__ void st16pol(uint8_t* p, u32x4 v) {
+  if constexpr (POL == 0) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  } else if constexpr (POL == 1) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (POL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (POL == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  }
+}
+
 // Wave max of 11-bit values by ballots, MSB first (no LDS round trips).
 __device__ __forceinline__ uint32_t wave_max11(uint32_t v) {
   uint32_t mx = 0;
@@ -1140,7 +1159,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t lane, u
 // line end: the zero-padded parity of SURVEY.md Appendix A, for output slots
 // that have the room -- the write-granularity probe of round 6); 4 = no tail
 // logic (every window XORed whole, in place: the VALU probe of round 6, not
-// exact).
+// exact); 8 = parity stores through the caches (not nontemporal); 16 = payload
+// loads through the caches (both exact: the cache-policy probe of round 6);
+// bits 5-7 = P != 0: parity stores with explicit policy st16pol<P> (exact).
 template <bool RECOVER, int WAVES, int GPB, int U = 2, bool PF = true, bool AL = true, int DIAG = 0>
 __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
   static_assert(GPB >= 2 && GPB <= 64, "group slots are lanes of wave 0");
@@ -1307,7 +1328,7 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
       // byte cannot leave that byte's page.  Otherwise the 16 bytes ending at
       // the packet end, shifted down.
       inp[u] = full || (AL && win < ln && (at & 15u) == 0u) || (DIAG & 4);
-      v[u] = ld16t<true>(a.bytes + (inp[u] ? at : at - win + ln - 16u));
+      v[u] = ld16t<(DIAG & 16) == 0>(a.bytes + (inp[u] ? at : at - win + ln - 16u));
       sh[u] = full ? 0u : min(win + 16u - ln, 15u);
       tt[u] = f < W ? (md[u].z >> 16) * kAccWords + (f - md[u].w) : 0xFFFFFFFFu;
     }
@@ -1342,14 +1363,21 @@ __device__ __forceinline__ void ragged_block_body(const RaggedArgs& a) {
     if ((DIAG & 1) && plen != 0xFFFFFu) continue;  // never a real length: no stores
     if (DIAG & 2) {  // whole lines: the accumulator is zero past plen
       const u32x4 z = {0u, 0u, 0u, 0u};
-      st16t<true>(dst + 16u * t, t < (uint32_t)kParWin ? lds_get16<1>(ac, t) : z);
+      st16t<(DIAG & 8) == 0>(dst + 16u * t, t < (uint32_t)kParWin ? lds_get16<1>(ac, t) : z);
       continue;
     }
     if (16u * t + 16u <= plen) {
-      st16t<true>(dst + 16u * t, lds_get16<1>(ac, t));
+      if constexpr ((DIAG >> 5) != 0)
+        st16pol<(DIAG >> 5)>(dst + 16u * t, lds_get16<1>(ac, t));
+      else
+        st16t<(DIAG & 8) == 0>(dst + 16u * t, lds_get16<1>(ac, t));
     } else {
       const uint32_t o = plen - 16u * t;  // 1..15
-      st16t<true>(dst + plen - 16u, bytes16_at(lds_get16<1>(ac, t - 1u), lds_get16<1>(ac, t), o));
+      const u32x4 x = bytes16_at(lds_get16<1>(ac, t - 1u), lds_get16<1>(ac, t), o);
+      if constexpr ((DIAG >> 5) != 0)
+        st16pol<(DIAG >> 5)>(dst + plen - 16u, x);
+      else
+        st16t<(DIAG & 8) == 0>(dst + plen - 16u, x);
     }
   }
 }

@@ -9,7 +9,9 @@
 //     palign 1: byte-packed.  slot: parity / revived row stride per group.
 //     mode 1: also the DIAG forms (whole-line stores; no stores; no tail);
 //     mode 2: the block kernel against ragged_multi_kernel (two groups per
-//     wave) on the given group shape (round 6's band table).
+//     wave) on the given group shape (round 6's band table); mode 3: the
+//     payload loads / parity stores through the caches instead of nontemporal;
+//     mode 4: parity stores with explicit cache policies (sc1, sc0 sc1, nt sc1, ...).
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_rblock.hip \
 //          -o tools/tune/build/tune_rblock
@@ -179,6 +181,22 @@ int main(int argc, char** argv) {
   vs.push_back({"product AL U2 encode (again)", false, BLK(false, 2, false)});
   vs.push_back({"product AL U2 recover", true, BLK(true, 2, false)});
   vs.push_back({"product AL U1 recover", true, BLK(true, 1, false)});
+  if (mode == 3) {  // round 6: cache policy of the payload loads / parity stores
+    vs.push_back({"cached stores encode", false, BLKD(false, 8)});
+    vs.push_back({"cached stores recover", true, BLKD(true, 8)});
+    vs.push_back({"cached loads encode", false, BLKD(false, 16)});
+    vs.push_back({"cached loads recover", true, BLKD(true, 16)});
+    vs.push_back({"cached both encode", false, BLKD(false, 24)});
+    vs.push_back({"cached both recover", true, BLKD(true, 24)});
+  }
+  if (mode == 4) {  // round 6: explicit store policies (st16pol)
+    vs.push_back({"stores sc1 encode", false, BLKD(false, 32)});
+    vs.push_back({"stores sc0 sc1 encode", false, BLKD(false, 64)});
+    vs.push_back({"stores nt sc1 encode", false, BLKD(false, 96)});
+    vs.push_back({"stores nt sc0 sc1 encode", false, BLKD(false, 128)});
+    vs.push_back({"stores sc1 recover", true, BLKD(true, 32)});
+    vs.push_back({"stores nt sc1 recover", true, BLKD(true, 96)});
+  }
   const bool diag = mode == 1;
   if (diag) {
     vs.push_back({"whole-line stores encode", false, BLKD(false, 2)});
