@@ -2203,8 +2203,12 @@ int qfec_service_warm(qfec_ctx* ctx) {
   // of the 100 us to assemble its batch still finds it resident)
   if (ctx && ctx->svc_on && ctx->svc_sh &&
       __atomic_load_n(&ctx->svc_sh->alive, __ATOMIC_SEQ_CST) != 0u) {
-    __atomic_store_n(&ctx->svc_used_ns, steady_ns(), __ATOMIC_RELEASE);
-    __atomic_store_n(&ctx->svc_sh->warm, ctx->svc_sh->warm + 1u, __ATOMIC_RELEASE);
+    const uint64_t now = steady_ns();
+    __atomic_store_n(&ctx->svc_used_ns, now, __ATOMIC_RELEASE);
+    // (not past the residency bound: warm calls alone, with no job for
+    // svc_submit to rotate at, must not keep a worker on its hardware queue)
+    if (now - ctx->svc_launch_ns < ctx->svc_max_resident_ns)
+      __atomic_store_n(&ctx->svc_sh->warm, ctx->svc_sh->warm + 1u, __ATOMIC_RELEASE);
     return QFEC_OK;
   }
   int rc = bind(ctx);

@@ -485,14 +485,15 @@ def test_warm_restarts_the_idle_time():
     worker resident.  Warm calls 50 us apart for 2 ms, no job: without the
     restart the worker would leave every ~100 us and be relaunched ~15 times;
     with it, it stays (each hiccup of the Python loop longer than the idle
-    time may cost one relaunch)."""
+    time may cost one relaunch).  Past the residency bound a warm call no
+    longer restarts it (warm calls alone have no job to rotate the worker
+    at): with the bound at 0.5 ms the same loop over 4 ms relaunches it
+    several times."""
     z, want_l = _mapped_case(2, g0=47000, kmin=10, kmax=10, lmin=1350, lmax=1350, seed=4)
     ctx = qfec.Context(0)
-    try:
-        _check(ctx, z, want_l)
-        ctx.service_warm()
-        before = ctx.debug_service()["launches"]
-        t_end = time.perf_counter() + 0.002
+
+    def warm_loop(seconds):
+        t_end = time.perf_counter() + seconds
         nxt = time.perf_counter()
         calls = 0
         while time.perf_counter() < t_end:
@@ -500,12 +501,27 @@ def test_warm_restarts_the_idle_time():
                 ctx.service_warm()
                 calls += 1
                 nxt += 50e-6
+        return calls
+
+    try:
+        _check(ctx, z, want_l)
+        ctx.debug_service_resident(50_000_000)  # 50 ms: the restart alone
+        ctx.service_warm()
+        before = ctx.debug_service()["launches"]
+        calls = warm_loop(0.002)
         st = ctx.debug_service()
         print(f"{calls} warm calls over 2 ms: {st['launches'] - before} relaunches; {st}")
         assert calls >= 20
         assert st["launches"] - before <= 6, st  # (~20 without the restart)
+        ctx.debug_service_resident(500_000)  # 0.5 ms
+        before = ctx.debug_service()["launches"]
+        calls = warm_loop(0.004)
+        st = ctx.debug_service()
+        print(f"bound 0.5 ms: {calls} warm calls over 4 ms: {st['launches'] - before} relaunches")
+        assert st["launches"] - before >= 2, st
         _check(ctx, z, want_l)
     finally:
+        ctx.debug_service_resident(2_000_000)
         ctx.close()
 
 
