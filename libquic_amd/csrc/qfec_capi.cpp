@@ -404,6 +404,9 @@ struct SvcTabs {
 // meanwhile -- a wait of at most ~2 ms for the other work, one relaunch per
 // 2 ms for the service, and no wait on the connection thread.
 constexpr uint64_t kSvcMaxResidentNs = 2000000;
+// a job of more groups is split over the worker's workgroups (the leader's
+// waves take up to this many: qfec_kernels.hip kSvcWaves)
+constexpr uint64_t kSvcSplitGroups = 8;
 void svc_abandon(qfec_ctx* ctx);
 
 int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover, uint32_t token,
@@ -413,7 +416,15 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
   const uint64_t now = steady_ns();
   __atomic_store_n(&ctx->svc_used_ns, now, __ATOMIC_RELEASE);
   qfec::SvcShared* sh = ctx->svc_sh;
-  if (ctx->svc_launch_ns != 0 && now - ctx->svc_launch_ns >= ctx->svc_max_resident_ns &&
+  // Not while a split job is outstanding: its followers may still be
+  // waiting for CUs (dispatched behind another kernel), the old kernel
+  // cannot end before they have done their shares, and its successor -- with
+  // every later job -- would wait behind them too.
+  bool split_pending = false;
+  for (const auto& op : ctx->async_ops)
+    split_pending = split_pending || (op.live && op.svc && op.cnt > kSvcSplitGroups);
+  if (!split_pending && ctx->svc_launch_ns != 0 &&
+      now - ctx->svc_launch_ns >= ctx->svc_max_resident_ns &&
       __atomic_load_n(&sh->alive, __ATOMIC_SEQ_CST) != 0u) {
     // rotate without waiting for it (round 6: a synchronous stop cost the
     // one-connection path ~0.35 us a group, profiles/round6/bench_r6fin2.json):

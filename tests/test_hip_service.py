@@ -529,11 +529,11 @@ def test_rotation_at_every_job_with_jobs_in_flight():
     """Round 6: a rotation does not wait for the worker -- it is told to leave
     between turns (published jobs or not) and its successor is queued behind
     it, starting at what it consumed.  With the bound at 0 every job published
-    while a worker runs rotates it: up to three asynchronous jobs in flight
-    (1 group: the leader's; 9-64 groups: split over the workgroups, whose
-    followers leave by their own launch epoch), completed in order and out of
-    order, encode and recover -- every byte exact, and the worker was rotated
-    at most jobs."""
+    while a worker runs rotates it (unless a split job is outstanding: the
+    test below): up to three asynchronous jobs in flight (1 group: the
+    leader's; 9-64 groups: split over the workgroups, whose followers leave by
+    their own launch epoch), completed in order and out of order, encode and
+    recover -- every byte exact, and the worker was rotated many times."""
     from test_hip_mapped import _mapped_case as mc
     ctx = qfec.Context(0)
     bufs = []
@@ -614,6 +614,59 @@ def test_quiet_service_context_leaves_the_phased_grid_whole():
     finally:
         a.close()
         b.close()
+
+
+def test_no_rotation_while_a_split_job_waits_for_late_followers():
+    """Round 6: a rotation is skipped while a split job is outstanding.  Its
+    followers may still be waiting for CUs (test hook: held at their start);
+    the old kernel cannot end before they have done their shares, so a
+    successor queued behind it would hold up every later job too.  With the
+    residency bound at 0 (rotate at every job) and the followers held, the
+    one-group jobs behind the split job still complete (the leader serves
+    them) and nothing is rotated; once the split job is claimed, rotation
+    resumes."""
+    ctx = qfec.Context(0)
+    z, want_l = _mapped_case(40, g0=96000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=23)
+    z1, want_1 = _mapped_case(2, g0=97000, kmin=2, kmax=12, lmin=16, lmax=1350, seed=24)
+    data, data1 = qfec.HostBuffer(len(z["data"])), qfec.HostBuffer(len(z1["data"]))
+    data.array[:] = z["data"]
+    data1.array[:] = z1["data"]
+    par, par1 = qfec.HostBuffer(z["parity"].size), qfec.HostBuffer(z1["parity"].size)
+    try:
+        ctx.debug_service_resident(0)
+        ctx.debug_service(on=False)  # no worker resident: the next job launches one
+        ctx.debug_service(on=True)
+        ctx.debug_service_hold(True)
+        par.array[:] = 0
+        plen = np.zeros(40, np.uint16)
+        ctx.encode_ragged(data.array, z["pkt_off"], z["pkt_len"], z["grp_ptr"], 40, par.array,
+                          z["parity_off"], plen, mapped=True, async_=True)
+        t = ctx.async_ticket()
+        before = ctx.debug_service()["rotations"]
+        for _ in range(2):  # (the split job holds one of the 3 slots)
+            par1.array[:] = 0
+            plen1 = np.zeros(2, np.uint16)
+            ctx.encode_ragged(data1.array, z1["pkt_off"], z1["pkt_len"], z1["grp_ptr"], 2,
+                              par1.array, z1["parity_off"], plen1, mapped=True, async_=True)
+            assert ctx.complete_ticket(ctx.async_ticket()) == 0
+            assert np.array_equal(par1.array, z1["parity"])
+        assert ctx.debug_service()["rotations"] == before
+        ctx.debug_service_hold(False)
+        assert ctx.complete_ticket(t) == 0
+        assert np.array_equal(plen, want_l)
+        assert np.array_equal(par.array, z["parity"])
+        ctx.service_warm()
+        for _ in range(3):
+            _check(ctx, z1, want_1)
+        assert ctx.debug_service()["rotations"] > before
+    finally:
+        ctx.debug_service_hold(False)
+        ctx.debug_service_resident(2_000_000)
+        data.close()
+        data1.close()
+        par.close()
+        par1.close()
+        ctx.close()
 
 
 def test_split_job_waits_for_late_followers():
