@@ -14,7 +14,7 @@ clocks are not compared directly: the host's wait (published -> token seen)
 minus the worker's (job seen -> token stored) is the two one-way link
 latencies (publish -> poll sees it, token store -> host sees it) together.
 
-  python tools/svc_trace.py [calls=300]
+  python tools/svc_trace.py [calls=300] [groups=1,64] [gaps=0,30,80]
 
 One JSON line per (groups, gap): medians over the calls (microseconds).
 """
@@ -42,13 +42,15 @@ def main():
     ctx = qfec.Context(0)
     try:
         ctx.debug_service_stamps(True)
-        for n in (1, 64):
+        ns = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 64]
+        gaps = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 30, 80]
+        for n in ns:
             z, _ = _mapped_case(n, g0=5000, kmin=10, kmax=10, lmin=1350, lmax=1350)
             data = qfec.HostBuffer(z["data"].nbytes)
             data.array[:] = z["data"]
             par = qfec.HostBuffer(z["parity"].size)
             plen = np.zeros(n, np.uint16)
-            for gap in (0, 30, 80):
+            for gap in gaps:
                 rows = []
                 for it in range(calls):
                     ctx.service_warm()
