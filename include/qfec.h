@@ -510,6 +510,12 @@ int qfec_debug_service_hold(qfec_ctx* ctx, int hold);
  * the successor queued behind it, no wait); returns the previous bound, or 0
  * for a null ctx. */
 uint64_t qfec_debug_service_resident(qfec_ctx* ctx, uint64_t ns);
+/* Test hook (round 6): the small-batch worker's idle time in us (default
+ * 100), for workers launched from now on; returns the previous value, or 0
+ * for a null ctx.  (A test that holds the followers back keeps the leader
+ * resident with it: a leader that idles out meanwhile has its successor
+ * queued behind the held kernel.) */
+uint64_t qfec_debug_service_idle(qfec_ctx* ctx, uint64_t us);
 
 /* ---- synthetic inputs (bench / parity-test support, device pointers) ---- */
 /* Counter-based bytes: byte j of packet (g, i) is little-endian byte j%8 of

@@ -155,6 +155,7 @@ struct qfec_ctx {
   uint64_t svc_used_ns = 0;  // steady clock of the last service job / warm (other_service_cus)
   uint64_t svc_launch_ns = 0;  // steady clock of the worker's last launch (kSvcMaxResidentNs)
   uint64_t svc_max_resident_ns;  // the residency bound (kSvcMaxResidentNs; test hook)
+  uint64_t svc_idle_ticks;       // the worker's idle time (kSvcIdleTicks; test hook)
   // measurement hook (stamps on): the last service call's host stamps, steady
   // ns: entry, published, token seen, return (qfec_debug_service_trace)
   uint64_t svc_hst[4] = {0, 0, 0, 0};
@@ -437,7 +438,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
     __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
     const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev,
                                                      ctx->svc_ring_dev, ctx->h_flag_dev,
-                                                     kSvcIdleTicks, ++ctx->svc_epoch,
+                                                     ctx->svc_idle_ticks, ++ctx->svc_epoch,
                                                      ctx->svc_stream);
     if (e != hipSuccess) {
       svc_abandon(ctx);  // every worker gone, the ring rewound, the service off
@@ -486,7 +487,7 @@ int svc_submit(qfec_ctx* ctx, int slot, const qfec::RaggedArgs& a, bool recover,
         bind(ctx) != QFEC_OK
             ? hipErrorInvalidDevice
             : qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev, ctx->svc_ring_dev,
-                                          ctx->h_flag_dev, kSvcIdleTicks, ++ctx->svc_epoch,
+                                          ctx->h_flag_dev, ctx->svc_idle_ticks, ++ctx->svc_epoch,
                                           ctx->svc_stream);
     if (e != hipSuccess) {
       // no worker runs (none was alive): take the job back, so that no later
@@ -1184,6 +1185,7 @@ qfec_ctx* qfec_create(int device) {
   ctx->ncu = ncu > 0 ? (uint32_t)ncu : 0;
   ctx->stream = ctx->own_stream;
   ctx->svc_max_resident_ns = kSvcMaxResidentNs;
+  ctx->svc_idle_ticks = kSvcIdleTicks;
   // (measurement knob: QFEC_SVC_RESIDENT_US overrides the residency bound)
   if (const char* r = std::getenv("QFEC_SVC_RESIDENT_US"))
     ctx->svc_max_resident_ns = std::strtoull(r, nullptr, 10) * 1000ull;
@@ -2233,7 +2235,7 @@ int qfec_service_warm(qfec_ctx* ctx) {
   // look: a spare one queued behind it on the stream idles out in turn
   __atomic_store_n(&sh->alive, 1u, __ATOMIC_SEQ_CST);
   const hipError_t e = qfec::launch_ragged_service(ctx->svc_sh_dev, ctx->svc_dev, ctx->svc_ring_dev,
-                                                   ctx->h_flag_dev, kSvcIdleTicks, ++ctx->svc_epoch,
+                                                   ctx->h_flag_dev, ctx->svc_idle_ticks, ++ctx->svc_epoch,
                                                    ctx->svc_stream);
   if (e != hipSuccess) {
     __atomic_store_n(&sh->alive, 0u, __ATOMIC_SEQ_CST);
@@ -2304,6 +2306,13 @@ int qfec_debug_service_trace(qfec_ctx* ctx, uint64_t* out) {
       out[8 + 4 * w + q] = __atomic_load_n(&ctx->svc_sh->wg_stamps[w][q], __ATOMIC_ACQUIRE);
   for (int q = 0; q < 4; ++q) out[8 + 4 * qfec::kSvcWgs + q] = ctx->svc_hst[q];
   return QFEC_OK;
+}
+
+uint64_t qfec_debug_service_idle(qfec_ctx* ctx, uint64_t us) {
+  if (!ctx) return 0;
+  const uint64_t prev = ctx->svc_idle_ticks / 100u;
+  ctx->svc_idle_ticks = us * 100u;  // 100-MHz ticks
+  return prev;
 }
 
 uint64_t qfec_debug_service_resident(qfec_ctx* ctx, uint64_t ns) {

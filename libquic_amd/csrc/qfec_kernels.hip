@@ -1976,23 +1976,36 @@ __global__ __launch_bounds__(64 * kSvcWaves) void ragged_service_kernel(
     }
     const uint64_t n = J.a.n_groups;
     const uint64_t step = split ? (uint64_t)kSvcWaves * kSvcWgs : (uint64_t)kSvcWaves;
-    if (n == 1u) {
-      // one group: every wave of the leader on it (its slots dealt round
-      // the waves: a wave issues an instruction every few cycles, and one
-      // wave alone spent ~1 us issuing a group's loads and shifting its
-      // windows), the partial windows XORed out of LDS by two waves
-      const WinOut o =
-          J.recover ? window_group<true, true, kSvcPB, kSvcWaves>(
-                          a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1])
-                    : window_group<false, true, kSvcPB, kSvcWaves>(
-                          a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], wv, s_red[0], s_red[1]);
+    if (n <= 2u) {
+      // one or two groups: each on 8 / n waves of the leader -- its slots
+      // dealt round its waves (a
+      // wave issues an instruction every few cycles: one group alone on one
+      // wave took ~7.5 us from its entry to its stores, on all 8 waves 3.9,
+      // profiles/round6/svc_trace_n_r6t.txt), each group's partial windows
+      // XORed out of LDS by two of its waves
+      const uint32_t NPn = n == 1u ? (uint32_t)kSvcWaves : 4u;
+      const uint32_t q = wv / NPn, part = wv - q * NPn;
+      u32x4* const r0 = s_red[0] + q * NPn * 64u;
+      u32x4* const r1 = s_red[1] + q * NPn * 64u;
+      WinOut o{nullptr, 0u, 0u, 0u, false};
+      if (q < n) {
+        if (n == 1u)
+          o = J.recover ? window_group<true, true, kSvcPB, kSvcWaves>(
+                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], part, r0, r1)
+                        : window_group<false, true, kSvcPB, kSvcWaves>(
+                              a, 0, lane, s_par[wv], s_head[wv], s_meta[wv], part, r0, r1);
+        else
+          o = J.recover ? window_group<true, true, kSvcPB, 4>(
+                              a, q, lane, s_par[wv], s_head[wv], s_meta[wv], part, r0, r1)
+                        : window_group<false, true, kSvcPB, 4>(
+                              a, q, lane, s_par[wv], s_head[wv], s_meta[wv], part, r0, r1);
+      }
       __syncthreads();
-      if (o.red && wv < 2u) {
-        const u32x4* r = s_red[wv];
+      if (q < n && o.red && part < 2u) {
+        const u32x4* r = part == 0u ? r0 : r1;
         u32x4 x = r[lane];
-#pragma unroll
-        for (int q = 1; q < kSvcWaves; ++q) x ^= r[q * 64 + lane];
-        if (lane + 64u * wv < o.nwin) st16t<true>(o.dst + (wv == 0u ? o.w0 : o.w1), x);
+        for (uint32_t p = 1; p < NPn; ++p) x ^= r[p * 64u + lane];
+        if (lane + 64u * part < o.nwin) st16t<true>(o.dst + (part == 0u ? o.w0 : o.w1), x);
       }
       if (tid == 0) st[2] = wall_clock64();
     } else {

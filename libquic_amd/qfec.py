@@ -113,6 +113,7 @@ SIGNATURES = [
     ("qfec_debug_service_trace", C.c_int, [_vp, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_feed", C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64)]),
     ("qfec_debug_service_resident", C.c_uint64, [_vp, C.c_uint64]),
+    ("qfec_debug_service_idle", C.c_uint64, [_vp, C.c_uint64]),
     ("qfec_debug_service_hold", C.c_int, [_vp, C.c_int]),
     ("qfec_complete", C.c_int, [_vp, C.c_int]),
     ("qfec_async_ticket", C.c_uint64, [_vp]),
@@ -501,6 +502,11 @@ class Context:
         """Test hook: the worker's residency bound in ns (0: rotate at every
         job); returns the previous bound."""
         return int(self.lib.qfec_debug_service_resident(self.ctx, int(ns)))
+
+    def debug_service_idle(self, us):
+        """Test hook: the worker's idle time in us for later launches (default
+        100); returns the previous value."""
+        return int(self.lib.qfec_debug_service_idle(self.ctx, int(us)))
 
     def debug_phase_regsteps(self, on):
         """Test hook: phased launches with (True) or without their register-held steps."""

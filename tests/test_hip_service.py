@@ -95,6 +95,27 @@ def test_service_one_group_on_all_waves(k, shape):
         ctx.close()
 
 
+@pytest.mark.parametrize("k", [1, 2, 10, 13, 33, 65])
+@pytest.mark.parametrize("shape", ["full", "wide", "short"])
+def test_service_two_groups_on_four_waves_each(k, shape):
+    """Round 6: a two-group job runs each group on 4 of the leader's waves
+    (its slots dealt round them, partial windows XORed out of LDS by two of
+    them; a group out of the fast form by its first wave alone), as the
+    one-group job runs on all 8.  Exact, encode and recover, the two groups
+    of different sizes, over repeated jobs."""
+    kw = {"full": dict(lmin=1452, lmax=1452), "wide": dict(lmin=16, lmax=1452),
+          "short": dict(lmin=1, lmax=40)}[shape]
+    ctx = qfec.Context(0)
+    try:
+        for rep in range(3):
+            z, want_l = _mapped_case(2, g0=48000 + 11 * k + rep, kmin=max(1, k - 3), kmax=k,
+                                     seed=300 * k + rep, **kw)
+            _check(ctx, z, want_l)
+        assert ctx.debug_service()["jobs"] >= 6
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("n", [8, 9, 17, 33, 63, 64])
 def test_service_split_jobs(n):
     """Round 5: a job of more than 8 groups is spread over the worker's 8
@@ -634,6 +655,7 @@ def test_no_rotation_while_a_split_job_waits_for_late_followers():
     par, par1 = qfec.HostBuffer(z["parity"].size), qfec.HostBuffer(z1["parity"].size)
     try:
         ctx.debug_service_resident(0)
+        ctx.debug_service_idle(200_000)  # the leader stays while the followers are held
         ctx.debug_service(on=False)  # no worker resident: the next job launches one
         ctx.debug_service(on=True)
         ctx.debug_service_hold(True)
@@ -662,6 +684,7 @@ def test_no_rotation_while_a_split_job_waits_for_late_followers():
     finally:
         ctx.debug_service_hold(False)
         ctx.debug_service_resident(2_000_000)
+        ctx.debug_service_idle(100)
         data.close()
         data1.close()
         par.close()
@@ -687,6 +710,10 @@ def test_split_job_waits_for_late_followers():
     data1.array[:] = z1["data"]
     par, par1 = qfec.HostBuffer(z["parity"].size), qfec.HostBuffer(z1["parity"].size)
     try:
+        # the leader's idle time 5 ms: the one-group jobs below arrive within
+        # it on any host (a leader that idled out before them would have its
+        # successor queued behind the held kernel); the 20-ms pause passes it
+        ctx.debug_service_idle(5_000)
         ctx.debug_service(on=False)  # no worker resident: the next job launches one
         ctx.debug_service(on=True)
         ctx.debug_service_hold(True)
@@ -717,6 +744,7 @@ def test_split_job_waits_for_late_followers():
             _check(ctx, z1, want_1)
     finally:
         ctx.debug_service_hold(False)
+        ctx.debug_service_idle(100)
         data.close()
         data1.close()
         par.close()
